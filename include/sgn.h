@@ -1,0 +1,327 @@
+/*
+ * sgn.h — C ABI of libsgn, the MI355X-native packet-level network core for Shadow.
+ *
+ * libsgn replaces the data-parallel half of Shadow's simulation round (reference:
+ * iiins0mn1a/shadow-gen, a Shadow 3.3.0 fork). Every entry point below names the
+ * reference interface it replaces (file:line relative to the reference's src/main/ unless
+ * stated). Conventions:
+ *   - plain C types only, no torch/HIP types; caller owns every input array for the
+ *     duration of the call, the library owns all device buffers;
+ *   - every function returns int status: 0 = ok, negative = errno-style failure, with a
+ *     message in sgn_last_error(ctx). Nothing unwinds or aborts across the ABI;
+ *   - times are EmulatedTime nanoseconds (since the Unix epoch) unless a field says
+ *     "_rel"/"_ns" (SimulationTime, nanoseconds since SIMULATION_START)
+ *     (lib/shadow-shim-helper-rs/src/emulated_time.rs:25-50);
+ *   - HostId is the u32 index of the host in hostname-sorted order (core/manager.rs:377-382).
+ */
+#ifndef SGN_H
+#define SGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGN_ABI_VERSION 1
+
+/* emulated_time.rs:27-40 */
+#define SGN_SIMULATION_START 946684800000000000ULL
+#define SGN_EMUTIME_INVALID 0xFFFFFFFFFFFFFFFFULL
+#define SGN_EMUTIME_MAX 0xFFFFFFFFFFFFFFFEULL
+
+/* core/definitions.h:124 */
+#define SGN_CONFIG_MTU 1500u
+/* IPv4 header (network/packet.rs:477-484) + UDP header (network/packet.rs:737-740) */
+#define SGN_UDP_HEADER_BYTES 28u
+
+/* status codes */
+#define SGN_OK 0
+#define SGN_EINVAL (-22)
+#define SGN_ENOMEM (-12)
+#define SGN_ENOENT (-2)
+#define SGN_ERANGE (-34)
+#define SGN_EDEVICE (-5)    /* HIP runtime failure */
+#define SGN_ESTATE (-71)    /* call out of order (e.g. round before sim_init) */
+#define SGN_EOVERFLOW (-75) /* a device capacity was exceeded; message names which */
+
+typedef struct sgn_ctx sgn_ctx;
+
+/* ------------------------------------------------------------------------------------ */
+/* Context                                                                              */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sgn_create_opts {
+  int32_t device;      /* HIP device ordinal */
+  uint32_t shard_rank; /* this process's shard (0 for a single GPU) */
+  uint32_t shard_count;/* number of shards (1 for a single GPU) */
+  uint32_t flags;      /* SGN_CREATE_* */
+} sgn_create_opts;
+
+#define SGN_CREATE_TIME_KERNELS 1u /* record HIP events around every launch (sgn_kernel_times) */
+
+/* Creates a context bound to one GPU. Replaces WorkerShared construction
+ * (core/manager.rs:447-470) for the data-parallel state. */
+int sgn_create(sgn_ctx** out, const sgn_create_opts* opts);
+void sgn_destroy(sgn_ctx* ctx);
+/* Last error message for ctx (or for a failed sgn_create when ctx == NULL). */
+const char* sgn_last_error(const sgn_ctx* ctx);
+/* ABI version compiled into the library. */
+int sgn_abi_version(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* Routing (network/graph/mod.rs:181-250, core/sim_config.rs:411-448)                   */
+/* ------------------------------------------------------------------------------------ */
+
+/* A parsed network graph: what NetworkGraph::parse (network/graph/mod.rs:132-179) produces.
+ * Node i (0-based) is petgraph NodeIndex i; edges keep GML order. Self-loops are edges. */
+typedef struct sgn_graph {
+  uint32_t n_nodes;
+  const uint32_t* node_id;          /* [n_nodes] GML ids */
+  uint32_t n_edges;
+  const uint32_t* edge_src;         /* [n_edges] GML ids */
+  const uint32_t* edge_dst;         /* [n_edges] GML ids */
+  const uint64_t* edge_latency_ns;  /* [n_edges] > 0 (graph/mod.rs:103) */
+  const float* edge_loss;           /* [n_edges] in [0,1] (graph/mod.rs:99) */
+  int32_t directed;
+} sgn_graph;
+
+/* Builds the U x U routing table {latency u64 ns, packet_loss f32} between the used nodes.
+ * Replaces generate_routing_info (core/sim_config.rs:411) ->
+ * NetworkGraph::compute_shortest_paths (graph/mod.rs:181) when use_shortest_path != 0, or
+ * get_direct_paths (graph/mod.rs:228) otherwise. Entry (i,j) is the path from
+ * used_node_ids[i] to used_node_ids[j]; (i,i) is the node's single self-loop edge
+ * (graph/mod.rs:209-215). Errors (not aborts): unknown node, missing/duplicate self-loop,
+ * disconnected used pair, missing/duplicate direct edge. */
+int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* graph, const uint32_t* used_node_ids,
+                     uint32_t n_used, int32_t use_shortest_path);
+/* RoutingInfo::path (graph/mod.rs:442) by GML node ids. SGN_ENOENT if not a used pair. */
+int sgn_route_get(sgn_ctx* ctx, uint32_t src_node_id, uint32_t dst_node_id,
+                  uint64_t* latency_ns, float* packet_loss);
+/* Copies the whole table (row-major, used-node order) to host arrays of n_used^2 entries. */
+int sgn_routes_copy(sgn_ctx* ctx, uint64_t* latency_ns, float* packet_loss);
+/* RoutingInfo::get_smallest_latency_ns (graph/mod.rs:472): min over all U^2 entries. */
+int sgn_min_latency(sgn_ctx* ctx, uint64_t* latency_ns);
+/* Device time of the last sgn_routes_build (ms), split into its phases. */
+typedef struct sgn_routes_timing {
+  double total_ms;      /* whole build incl. upload/extract, device-timed */
+  double latency_ms;    /* blocked min-plus (Floyd-Warshall) phase */
+  double loss_ms;       /* tight-edge loss fold phase */
+  uint32_t loss_iters;  /* sweeps to the fixed point */
+  uint32_t tile;        /* min-plus tile edge T */
+  uint64_t n_tight_edges;
+} sgn_routes_timing;
+int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
+
+/* ------------------------------------------------------------------------------------ */
+/* Hosts (core/sim_config.rs:47-164,211-291; host/host.rs:234,283-295)                  */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sgn_hosts {
+  uint32_t n_hosts;            /* hosts in HostId order */
+  const uint32_t* ip;          /* [n] IPv4 address, host byte order */
+  const uint32_t* node_id;     /* [n] GML node id (must be a used node of the route table) */
+  const uint64_t* bw_up_bits;  /* [n] HostInfo::bandwidth_up_bits (note sim_config.rs:252-254) */
+  const uint64_t* bw_down_bits;/* [n] HostInfo::bandwidth_down_bits */
+  const uint64_t* seed;        /* [n] HostInfo::seed = r ^ SipHash13(name) (sim_config.rs:242) */
+} sgn_hosts;
+
+/* Registers every host of the simulation (all shards pass the full list; each shard
+ * keeps the contiguous HostId range it owns). Replaces DNS registration
+ * (network/dns.rs:97-131: unspecified/loopback/broadcast/multicast and duplicate
+ * addresses are errors) and Host::new's RNG/relay construction. */
+int sgn_hosts_set(sgn_ctx* ctx, const sgn_hosts* hosts);
+
+/* Derives per-host seeds exactly as SimConfig::new + build_host do
+ * (core/sim_config.rs:50-54,220-242): G = Xoshiro256++::seed_from_u64(sim_seed);
+ * r = G.next_u64(); seed[i] = r ^ SipHash13_{k0=k1=0}(names[i] || 0xFF). Host-side only. */
+int sgn_derive_host_seeds(uint32_t sim_seed, const char* const* names, uint32_t n,
+                          uint64_t* seeds_out);
+
+/* ------------------------------------------------------------------------------------ */
+/* Simulation rounds (core/manager.rs:541-656, host/host.rs:762-834, core/worker.rs:330-403)*/
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sgn_sim_config {
+  uint64_t stop_time_ns;        /* general.stop_time (controller.rs:29-31) */
+  uint64_t bootstrap_end_ns;    /* general.bootstrap_end_time (manager.rs:353-355) */
+  uint64_t runahead_ns;         /* experimental.runahead; 0 = None (runahead.rs:55) */
+  int32_t use_dynamic_runahead; /* experimental.use_dynamic_runahead (runahead.rs:61-67) */
+  uint32_t out_fifo_cap;        /* synthetic socket send-queue entries per host (>= 1) */
+  uint32_t codel_cap;           /* device CoDel ring slots per host (reference: unlimited;
+                                   exceeding it is SGN_EOVERFLOW, never a silent drop) */
+  uint32_t reserved0;
+  uint64_t event_capacity;      /* in-flight packet-event slots per shard (0 = auto) */
+} sgn_sim_config;
+
+/* Synthetic traffic (stands in for the managed processes, which stay on the CPU in
+ * Shadow). Hosts talk UDP through the reference's own relay/router path. Workload
+ * functions are defined once in sgn_workload.h. */
+#define SGN_TRAFFIC_PERIODIC 1u /* configs B/D: every host sends one datagram per period */
+#define SGN_TRAFFIC_TGEN 2u     /* config C: clients fetch files from servers as MTU trains */
+
+typedef struct sgn_traffic {
+  uint32_t kind;
+  uint32_t payload_len;          /* PERIODIC datagram payload bytes */
+  uint64_t flow_seed;
+  uint64_t start_ns;             /* first app event (sim time) */
+  uint64_t start_jitter_ns;      /* + H(i) % (jitter + 1) */
+  uint64_t period_ns;            /* PERIODIC send period / TGEN think time */
+  uint64_t period_jitter_ns;     /* TGEN: think time + H % (jitter + 1) */
+  uint32_t unknown_dst_permille; /* PERIODIC: sends to an address outside the simulation */
+  uint32_t req_payload;          /* TGEN request datagram payload */
+  uint32_t n_servers;            /* TGEN */
+  uint32_t reserved0;
+  const uint32_t* server_hosts;  /* TGEN [n_servers] HostIds of servers (ascending) */
+  uint64_t file_bytes[3];        /* TGEN file sizes (e.g. 50 KiB, 1 MiB, 5 MiB) */
+} sgn_traffic;
+
+/* Uploads state and schedules each host's first app event. Must follow routes_build and
+ * hosts_set. Host RNGs are Xoshiro256++::seed_from_u64(seed) (host/host.rs:234). */
+int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* traffic);
+
+/* The current window [start, end) (EmulatedTime). The first is
+ * [SIMULATION_START, SIMULATION_START + 1 ns) (manager.rs:506-509). active = 0 once
+ * Controller::manager_finished_current_round returned None (controller.rs:88-112). */
+int sgn_window(sgn_ctx* ctx, uint64_t* start, uint64_t* end, int32_t* active);
+
+/* Runs one round on the current window: every owned host executes its events with
+ * time < end (Host::execute, host.rs:762-830), packets are routed (Worker::send_packet,
+ * worker.rs:330-403), events are queued at their destinations (push_packet_to_host,
+ * worker.rs:603-613), then min_next_event = min over all queue heads (manager.rs:580-628)
+ * and the next window is computed on the device. Synchronous. */
+int sgn_round(sgn_ctx* ctx, uint64_t* min_next_event);
+
+/* Runs up to max_rounds rounds without a host synchronisation per round (rounds are
+ * enqueued in batches; the window lives on the device). Stops early when the simulation
+ * ends. rounds_done may be NULL. */
+int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done);
+
+/* Whole-simulation counters (summed over owned hosts). */
+typedef struct sgn_stats {
+  uint64_t rounds;
+  uint64_t packets_sent;       /* send_packet executions that passed the DNS check */
+  uint64_t packets_loss_dropped;/* ... of which dropped by path reliability (worker.rs:371) */
+  uint64_t packets_unknown_dst;/* InetDropped: destination not in the simulation (:347) */
+  uint64_t packet_events_popped;/* packet events executed at destinations (host.rs:797) */
+  uint64_t codel_dropped;      /* RouterDropped by CoDel (codel_queue.rs:319) */
+  uint64_t delivered;          /* inbound packets handed to the host interface */
+  uint64_t local_delivered;    /* packets to the host's own address (relay is_local) */
+  uint64_t app_blocked;        /* synthetic sends refused by a full send queue */
+  uint64_t local_events;       /* local (task) events executed */
+  uint64_t bytes_delivered;    /* payload bytes handed to the interface */
+  uint64_t min_used_latency_ns;/* Runahead::min_used_latency, SGN_EMUTIME_INVALID if none */
+  uint64_t max_codel_len;      /* high-water mark of any CoDel ring (capacity planning) */
+  uint64_t max_pending_events; /* high-water mark of in-flight packet events */
+} sgn_stats;
+int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out);
+
+/* Per-host order-sensitive digests (sgn_workload.h: SGN_DIGEST_*), counters and final RNG
+ * state for the owned range [host_lo, host_hi). Arrays hold (host_hi - host_lo) entries;
+ * any pointer may be NULL. Used by parity tests at full sizes. */
+typedef struct sgn_host_digest {
+  uint64_t tx;        /* every send_packet outcome, in order */
+  uint64_t rx;        /* every packet event popped, in order (event order proof) */
+  uint64_t app;       /* every interface delivery / CoDel drop, in order */
+  uint64_t rng[4];    /* Xoshiro256++ state */
+  uint64_t next_event_id;
+  uint64_t n_sent, n_popped, n_delivered, n_codel_dropped;
+} sgn_host_digest;
+int sgn_host_digests(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, sgn_host_digest* out);
+
+/* Host::next_event_time (host.rs:832): backs worker_maxEventRunaheadTime (worker.rs:774).
+ * SGN_EMUTIME_INVALID when the queue is empty. Only valid between rounds. */
+int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t);
+
+/* Per-packet trace (for bit-exact comparison at small sizes). Enable before sim_init. */
+#define SGN_TRACE_SEND 1u   /* a = now, b = deliver time (0 if dropped/unknown), c = event id */
+#define SGN_TRACE_POP 2u    /* a = event time, b = 0, c = src event id */
+#define SGN_TRACE_DELIVER 3u/* a = now, b = 0, c = src event id */
+#define SGN_TRACE_CODEL_DROP 4u
+typedef struct sgn_trace_rec {
+  uint32_t kind;     /* SGN_TRACE_* */
+  uint32_t host;     /* host where it happened */
+  uint32_t peer;     /* SEND: dst HostId (0xFFFFFFFF unknown); others: src HostId */
+  uint32_t flags;    /* SEND: 0 sent, 1 loss-dropped, 2 unknown dst */
+  uint64_t a, b, c;
+  uint64_t seq;      /* per-host sequence number of this record */
+} sgn_trace_rec;
+int sgn_trace_enable(sgn_ctx* ctx, uint64_t capacity);
+/* Copies up to cap records (unordered; sort by (host, seq)). n_total = records produced. */
+int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_total);
+
+/* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS). */
+typedef struct sgn_kernel_times {
+  uint64_t launches[8];
+  double ms[8];
+  const char* name[8];
+  uint32_t n_kernels;
+} sgn_kernel_times;
+int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out);
+
+/* ------------------------------------------------------------------------------------ */
+/* Multi-GPU shard exchange (round edge). Hosts are partitioned into contiguous HostId   */
+/* ranges; events for remote hosts leave through per-peer slots and the window minimum */
+/* is reduced across shards. The library drives RCCL itself on its own stream.         */
+/* ------------------------------------------------------------------------------------ */
+
+/* Size of the opaque RCCL unique id blob (ncclUniqueId). */
+#define SGN_COMM_ID_BYTES 128
+/* Rank 0 produces the id; the caller broadcasts it (e.g. torch.distributed) to all ranks. */
+int sgn_comm_get_unique_id(uint8_t id_out[SGN_COMM_ID_BYTES]);
+/* Creates the communicator over shard_count ranks; this ctx is rank shard_rank.
+ * exchange_slot_events = capacity (events) of each per-peer slot per round. */
+int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES],
+                  uint64_t exchange_slot_events);
+/* Owned HostId range of a shard (same split on every rank). */
+int sgn_shard_range(uint32_t n_hosts, uint32_t shard_rank, uint32_t shard_count,
+                    uint32_t* host_lo, uint32_t* host_hi);
+
+/* ------------------------------------------------------------------------------------ */
+/* CPU-side consumers (core/worker.rs:657-690, host/host.rs:1325-1336)                  */
+/* ------------------------------------------------------------------------------------ */
+
+/* worker_getLatency (worker.rs:657-667): addresses in NETWORK byte order; returns
+ * SimulationTime ns or SGN_EMUTIME_INVALID (= SIMTIME_INVALID) if either is unknown. */
+uint64_t sgn_worker_get_latency(sgn_ctx* ctx, uint32_t src_be, uint32_t dst_be);
+/* worker_isRoutable (worker.rs:684-690). */
+int32_t sgn_worker_is_routable(sgn_ctx* ctx, uint32_t src_be, uint32_t dst_be);
+/* worker_getBandwidth{Up,Down}Bytes (worker.rs:670-681): bits / 8; 0 if unknown. */
+uint64_t sgn_worker_get_bandwidth_up_bytes(sgn_ctx* ctx, uint32_t ip_be);
+uint64_t sgn_worker_get_bandwidth_down_bytes(sgn_ctx* ctx, uint32_t ip_be);
+/* Dns::addr_to_host_id (network/dns.rs:174): 0 and *host set, or SGN_ENOENT. */
+int sgn_addr_to_host_id(sgn_ctx* ctx, uint32_t ip, uint32_t* host);
+
+/* ------------------------------------------------------------------------------------ */
+/* Front end (drop-in graph ingest): GML text -> sgn_graph (lib/gml-parser, graph/mod.rs)*/
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sgn_gml sgn_gml;
+/* Parses GML text as gml_parser::parse + NetworkGraph::parse do (lib/gml-parser/src/
+ * parser.rs:66-230, network/graph/mod.rs:28-179, units.rs:406-440). On failure returns
+ * SGN_EINVAL and, if err/err_len given, a message. */
+int sgn_gml_parse(const char* text, size_t len, sgn_gml** out, char* err, size_t err_len);
+void sgn_gml_free(sgn_gml* g);
+/* Borrowed view valid until sgn_gml_free. */
+int sgn_gml_graph(const sgn_gml* g, sgn_graph* out);
+/* Node bandwidths from host_bandwidth_up/_down (bits/s); has_* = 0 when absent. */
+int sgn_gml_node_bandwidth(const sgn_gml* g, uint32_t node_index, uint64_t* up_bits,
+                           int32_t* has_up, uint64_t* down_bits, int32_t* has_down);
+
+/* units.rs:406-440 FromStr + convert(): parse "10 ms" / "81920 Kibit" / "1 GiB".
+ * kind: 0 Time -> ns, 1 Bytes -> bytes, 2 BitsPerSec -> bits/s. */
+int sgn_units_parse(int32_t kind, const char* text, uint64_t* value_base);
+
+/* ------------------------------------------------------------------------------------ */
+/* Test hooks (not part of the reference interface)                                      */
+/* ------------------------------------------------------------------------------------ */
+
+/* Device CoDel control-law increments round(1e8 / sqrt(count)) for count in [0, n)
+ * (router/codel_queue.rs:285-298), for checking device f64 rounding against the host. */
+int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGN_H */

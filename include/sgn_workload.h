@@ -1,0 +1,105 @@
+/*
+ * sgn_workload.h — the synthetic workload and digest definitions shared by every
+ * implementation of the packet core (the HIP engine and the parity oracle).
+ *
+ * These are NOT reference semantics: they define the synthetic applications that stand
+ * in for Shadow's managed processes (which stay on the CPU per the north star) and the
+ * order-sensitive digests used to compare runs. Reference semantics (routing, RNG draws,
+ * event order, relays, token buckets, CoDel, runahead) are implemented separately by each
+ * side. Pure functions of integers; no state.
+ */
+#ifndef SGN_WORKLOAD_H
+#define SGN_WORKLOAD_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SGN_HD __host__ __device__ __forceinline__
+#else
+#define SGN_HD static inline
+#endif
+
+/* SplitMix64 finalizer (also the SplitMix64 output function). */
+SGN_HD uint64_t sgn_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+/* Workload hash H(seed, a, b): independent streams per (host, counter). */
+SGN_HD uint64_t sgn_flow_hash(uint64_t seed, uint64_t a, uint64_t b) {
+  return sgn_mix64(sgn_mix64(seed ^ (0x9e3779b97f4a7c15ULL * (a + 1))) ^
+                   (0xd1b54a32d192ed03ULL * (b + 1)));
+}
+
+#define SGN_SALT_START 0xFFFFFFFF00000001ULL
+#define SGN_SALT_THINK 0xFFFFFFFF00000002ULL
+
+/* Address space for sends to destinations outside the simulation (never assigned:
+ * automatic IPs start at 11.0.0.1, graph/mod.rs:359-417; the library rejects explicit
+ * host addresses inside 10.255.0.0/16). */
+#define SGN_UNKNOWN_IP_BASE 0x0AFF0000u /* 10.255.0.0 */
+
+/* First app event of host i. */
+SGN_HD uint64_t sgn_app_start_rel(uint64_t flow_seed, uint32_t host, uint64_t start_ns,
+                                  uint64_t jitter_ns) {
+  uint64_t j = jitter_ns ? sgn_flow_hash(flow_seed, host, SGN_SALT_START) % (jitter_ns + 1) : 0;
+  return start_ns + j;
+}
+
+/* PERIODIC: destination of the k-th datagram of host i.
+ * Returns 1 and *peer_host when addressed to a host, 0 and *unknown_ip otherwise. */
+SGN_HD int sgn_periodic_dst(uint64_t flow_seed, uint32_t host, uint64_t k, uint32_t n_hosts,
+                            uint32_t unknown_permille, uint32_t* peer_host,
+                            uint32_t* unknown_ip) {
+  uint64_t r = sgn_flow_hash(flow_seed, host, k);
+  if ((uint32_t)(r % 1000u) < unknown_permille) {
+    *unknown_ip = SGN_UNKNOWN_IP_BASE + (uint32_t)((r >> 32) & 0xFFFFu);
+    return 0;
+  }
+  *peer_host = (uint32_t)((r >> 16) % (uint64_t)n_hosts);
+  return 1;
+}
+
+/* TGEN: the k-th fetch of client i: server index into server_hosts and file size class. */
+SGN_HD void sgn_tgen_fetch(uint64_t flow_seed, uint32_t host, uint64_t k, uint32_t n_servers,
+                           uint32_t* server_idx, uint32_t* size_class) {
+  uint64_t r = sgn_flow_hash(flow_seed, host, k);
+  *server_idx = (uint32_t)((r >> 8) % (uint64_t)n_servers);
+  *size_class = (uint32_t)((r >> 40) % 3u);
+}
+
+/* TGEN: think time after the k-th fetch of client i. */
+SGN_HD uint64_t sgn_tgen_think(uint64_t flow_seed, uint32_t host, uint64_t k, uint64_t think_ns,
+                               uint64_t jitter_ns) {
+  uint64_t j = jitter_ns ? sgn_flow_hash(flow_seed ^ SGN_SALT_THINK, host, k) % (jitter_ns + 1)
+                         : 0;
+  return think_ns + j;
+}
+
+/* UDP payload per full datagram of a TGEN response train (1500 B on the wire). */
+#define SGN_TGEN_MSS 1472u /* 1500 - 20 (IPv4) - 8 (UDP) */
+
+/* Packet tags (carried opaque through the core; the synthetic apps interpret them). */
+#define SGN_TAG_DATA 0u        /* PERIODIC datagram */
+#define SGN_TAG_REQ 0x10000u   /* TGEN request | size class */
+#define SGN_TAG_RESP 0x20000u  /* TGEN response datagram */
+
+/* Order-sensitive per-host digest step. */
+SGN_HD uint64_t sgn_digest3(uint64_t h, uint64_t a, uint64_t b, uint64_t c) {
+  h = sgn_mix64(h ^ a);
+  h = sgn_mix64(h ^ (b + 0x632be59bd9b4e019ULL));
+  h = sgn_mix64(h ^ (c + 0x8cb92ba72f3d8dd7ULL));
+  return h;
+}
+
+/* What each digest covers (identical on every implementation):
+ *  tx : per send_packet call past the is_completed check, (now, dst_host|outcome<<32,
+ *       deliver_time_or_0), outcome 0 sent / 1 loss-dropped / 2 unknown destination
+ *       (dst_host = 0xFFFFFFFF for unknown).
+ *  rx : per packet event popped, (event_time, src_host, src_event_id).
+ *  app: per interface delivery (now, src_host, src_event_id) and per CoDel drop
+ *       (now, src_host | 1<<63, src_event_id).                                          */
+#define SGN_DIGEST_SEED 0x5eed5eed5eed5eedULL
+
+#endif /* SGN_WORKLOAD_H */

@@ -1,0 +1,1643 @@
+// engine.hip — the per-round packet path of Shadow on gfx950.
+//
+// One simulation round (core/manager.rs:541-656) is six launches on one stream:
+//   k_count      count the calendar events due in [ws, we) per destination host
+//   k_scan_*     exclusive scan of the counts -> per-host segment offsets
+//   k_scatter    place due events into their destination's segment; survivors of the
+//                partially consumed bucket move to the spare slab
+//   k_execute    one lane per host: order the segment by (time, src host, src event id)
+//                (core/work/event.rs:84-183), merge it with the host's local events and run
+//                Host::execute (host/host.rs:762-830) — router/CoDel, relays, token
+//                buckets, Worker::send_packet — emitting new events into the calendar
+//   k_finalize   bucket bookkeeping, min next event over queue heads (manager.rs:580-628),
+//                Controller::manager_finished_current_round (controller.rs:88-112)
+// The window lives in device memory (Ctrl), so rounds are enqueued back to back without a
+// host round trip; every kernel returns immediately once the simulation has ended.
+//
+// Bit-exactness notes: all time/byte/event-id arithmetic is u64 integer; the only floating
+// point is (a) reliability = (f64)(1.0f - loss) vs the f64 draw (x >> 11) * 2^-53
+// (core/worker.rs:363-371, exact on any IEEE device), and (b) the CoDel control law
+// round(1e8 / sqrt(count)) in f64 (router/codel_queue.rs:285-298), which relies on
+// correctly rounded f64 sqrt/div (checked on the GPU by tests/test_gpu_parity.py).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "sgn_internal.h"
+#include "sgn_workload.h"
+
+namespace sgn {
+
+enum : uint32_t { RELAY_IDLE = 0, RELAY_PENDING = 1, RELAY_FORWARDING = 2 };
+
+constexpr uint64_t CODEL_TARGET = 10000000ULL;      // codel_queue.rs:23
+constexpr uint64_t CODEL_INTERVAL = 100000000ULL;   // codel_queue.rs:28
+constexpr uint64_t SIMTIME_MAX = 17500059273709551614ULL;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) {
+  return (x << k) | (x >> (64 - k));
+}
+__device__ __forceinline__ uint64_t sat_sub(uint64_t a, uint64_t b) { return a > b ? a - b : 0; }
+__device__ __forceinline__ uint64_t mul_sat(uint64_t a, uint64_t b, uint64_t cap) {
+  uint64_t hi = __umul64hi(a, b);
+  uint64_t lo = a * b;
+  return (hi != 0 || lo > cap) ? cap : lo;
+}
+// EmulatedTime::saturating_add (emulated_time.rs:106-111)
+__device__ __forceinline__ uint64_t emu_sat_add(uint64_t t, uint64_t d) {
+  uint64_t x = t + d;
+  return (x < t || x > EMU_MAX) ? EMU_MAX : x;
+}
+
+__device__ __forceinline__ bool ev_less(const EvRec& a, const EvRec& b) {
+  if (a.time != b.time) return a.time < b.time;
+  if (a.src != b.src) return a.src < b.src;
+  return a.eid < b.eid;
+}
+
+__device__ __forceinline__ uint32_t bucket_of(const DevSim& S, uint64_t t) {
+  return (uint32_t)(((t - SIM_START) / S.BW) % (uint64_t)S.NB);
+}
+
+// CoDel control law (router/codel_queue.rs:285-298)
+__device__ __forceinline__ uint64_t codel_law(uint64_t time, uint64_t count) {
+  double sq = count == 0 ? 1.0 : sqrt((double)count);
+  double div = 100000000.0 / sq;
+  uint64_t inc = (uint64_t)round(div);
+  uint64_t orig = time - SIM_START;
+  uint64_t adj = orig + inc;
+  if (adj < orig || adj > SIMTIME_MAX) adj = SIMTIME_MAX;
+  return SIM_START + adj;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    uint32_t lo = __shfl_xor((uint32_t)v, off, 64);
+    uint32_t hi = __shfl_xor((uint32_t)(v >> 32), off, 64);
+    uint64_t o = ((uint64_t)hi << 32) | lo;
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// block-wide (256 threads) minimum, result valid in every thread
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* sh) {
+  v = wave_min_u64(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  uint64_t r = sh[0];
+  const int nw = blockDim.x >> 6;
+  for (int i = 1; i < nw; i++) r = sh[i] < r ? sh[i] : r;
+  __syncthreads();
+  return r;
+}
+
+struct Pkt {
+  uint32_t src;
+  uint32_t dst_ip;
+  uint32_t payload;
+  uint32_t tag;
+  uint64_t eid;
+};
+
+// ------------------------------------------------------------------------------------
+// Per-host executor: the host's whole state lives in registers for the round.
+// ------------------------------------------------------------------------------------
+struct HostExec {
+  const DevSim& S;
+  Ctrl* C;
+  uint32_t h, gid, my_ip, my_unode;
+  uint64_t now, we, b1_keep_base;
+  uint32_t b1;
+  // RNG (host/host.rs:234) and counters (host.rs:259-263)
+  uint64_t r0, r1, r2, r3;
+  uint64_t eid, app_k;
+  uint64_t st0, st1, st2, se0, se1, se2;  // local event slots: relay out, relay in, app
+  uint32_t fl;
+  uint32_t ro_dst, ro_pay, ro_tag;
+  uint32_t ri_src, ri_pay, ri_tag;
+  uint64_t ri_eid;
+  uint64_t tbb0, tbl0, tbc0, tbi0, tbb1, tbl1, tbc1, tbi1;
+  uint32_t cq_head, cq_len;
+  uint64_t cq_bytes, cq_ie, cq_dn, cq_cur, cq_prev;
+  uint32_t fq_head, fq_len;
+  uint64_t dtx, drx, dapp;
+  uint64_t c_sent, c_loss, c_unknown, c_popped, c_codel, c_deliv, c_ldeliv, c_blocked,
+      c_localev, c_bytes, c_maxcodel;
+  uint64_t tseq;
+  uint64_t lat_cache;
+
+  __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint64_t kb)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1_keep_base(kb), b1(bucket1) {
+    const uint32_t nH = S.nH;
+    gid = S.lo + h;
+    my_ip = S.ip[gid];
+    my_unode = S.unode[gid];
+    r0 = S.rng0[h];
+    r1 = S.rng1[h];
+    r2 = S.rng2[h];
+    r3 = S.rng3[h];
+    eid = S.eid[h];
+    app_k = S.app_k[h];
+    st0 = S.slot_t[h];
+    st1 = S.slot_t[nH + h];
+    st2 = S.slot_t[2 * nH + h];
+    se0 = S.slot_e[h];
+    se1 = S.slot_e[nH + h];
+    se2 = S.slot_e[2 * nH + h];
+    fl = S.flags[h];
+    ro_dst = S.ro_dst[h];
+    ro_pay = S.ro_pay[h];
+    ro_tag = S.ro_tag[h];
+    ri_src = S.ri_src[h];
+    ri_pay = S.ri_pay[h];
+    ri_tag = S.ri_tag[h];
+    ri_eid = S.ri_eid[h];
+    tbb0 = S.tb_bal[h];
+    tbl0 = S.tb_last[h];
+    tbc0 = S.tb_cap[h];
+    tbi0 = S.tb_inc[h];
+    tbb1 = S.tb_bal[nH + h];
+    tbl1 = S.tb_last[nH + h];
+    tbc1 = S.tb_cap[nH + h];
+    tbi1 = S.tb_inc[nH + h];
+    cq_head = S.cq_head[h];
+    cq_len = S.cq_len[h];
+    cq_bytes = S.cq_bytes[h];
+    cq_ie = S.cq_ie[h];
+    cq_dn = S.cq_dn[h];
+    cq_cur = S.cq_cur[h];
+    cq_prev = S.cq_prev[h];
+    fq_head = S.fq_head[h];
+    fq_len = S.fq_len[h];
+    dtx = S.d_tx[h];
+    drx = S.d_rx[h];
+    dapp = S.d_app[h];
+    c_sent = c_loss = c_unknown = c_popped = c_codel = c_deliv = c_ldeliv = c_blocked =
+        c_localev = c_bytes = 0;
+    c_maxcodel = S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
+    tseq = S.trace_seq[h];
+    lat_cache = INVALID;
+  }
+
+  __device__ void store() {
+    const uint32_t nH = S.nH;
+    S.rng0[h] = r0;
+    S.rng1[h] = r1;
+    S.rng2[h] = r2;
+    S.rng3[h] = r3;
+    S.eid[h] = eid;
+    S.app_k[h] = app_k;
+    S.slot_t[h] = st0;
+    S.slot_t[nH + h] = st1;
+    S.slot_t[2 * nH + h] = st2;
+    S.slot_e[h] = se0;
+    S.slot_e[nH + h] = se1;
+    S.slot_e[2 * nH + h] = se2;
+    S.flags[h] = fl;
+    S.ro_dst[h] = ro_dst;
+    S.ro_pay[h] = ro_pay;
+    S.ro_tag[h] = ro_tag;
+    S.ri_src[h] = ri_src;
+    S.ri_pay[h] = ri_pay;
+    S.ri_tag[h] = ri_tag;
+    S.ri_eid[h] = ri_eid;
+    S.tb_bal[h] = tbb0;
+    S.tb_last[h] = tbl0;
+    S.tb_bal[nH + h] = tbb1;
+    S.tb_last[nH + h] = tbl1;
+    S.cq_head[h] = cq_head;
+    S.cq_len[h] = cq_len;
+    S.cq_bytes[h] = cq_bytes;
+    S.cq_ie[h] = cq_ie;
+    S.cq_dn[h] = cq_dn;
+    S.cq_cur[h] = cq_cur;
+    S.cq_prev[h] = cq_prev;
+    S.fq_head[h] = fq_head;
+    S.fq_len[h] = fq_len;
+    S.d_tx[h] = dtx;
+    S.d_rx[h] = drx;
+    S.d_app[h] = dapp;
+    uint64_t* c = S.cnt;
+    const size_t n = nH;
+    c[CNT_SENT * n + h] += c_sent;
+    c[CNT_LOSS * n + h] += c_loss;
+    c[CNT_UNKNOWN * n + h] += c_unknown;
+    c[CNT_POPPED * n + h] += c_popped;
+    c[CNT_CODEL * n + h] += c_codel;
+    c[CNT_DELIV * n + h] += c_deliv;
+    c[CNT_LOCAL_DELIV * n + h] += c_ldeliv;
+    c[CNT_BLOCKED * n + h] += c_blocked;
+    c[CNT_LOCAL_EV * n + h] += c_localev;
+    c[CNT_BYTES * n + h] += c_bytes;
+    c[CNT_MAX_CODEL * n + h] = c_maxcodel;
+    S.trace_seq[h] = tseq;
+  }
+
+  __device__ uint64_t next_local_time() const {
+    uint64_t m = st0;
+    m = st1 < m ? st1 : m;
+    m = st2 < m ? st2 : m;
+    return m;
+  }
+
+  // ---- Xoshiro256++ (rand_xoshiro 0.7.0) + rand 0.9.2 StandardUniform f64 ----
+  __device__ __forceinline__ uint64_t rng_next() {
+    const uint64_t result = rotl64(r0 + r3, 23) + r0;
+    const uint64_t t = r1 << 17;
+    r2 ^= r0;
+    r3 ^= r1;
+    r1 ^= r2;
+    r0 ^= r3;
+    r2 ^= t;
+    r3 = rotl64(r3, 45);
+    return result;
+  }
+  __device__ __forceinline__ double rng_f64() {
+    return (double)(rng_next() >> 11) * 0x1.0p-53;
+  }
+
+  __device__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
+                        uint64_t c) {
+    uint64_t seq = tseq++;
+    if (!S.trace_on) return;
+    uint64_t pos = atomicAdd((unsigned long long*)&C->trace_n, 1ULL);
+    if (pos >= S.trace_cap) {
+      atomicOr(&C->overflow, OVF_TRACE);
+      return;
+    }
+    sgn_trace_rec r;
+    r.kind = kind;
+    r.host = gid;
+    r.peer = peer;
+    r.flags = flags;
+    r.a = a;
+    r.b = b;
+    r.c = c;
+    r.seq = seq;
+    S.trace[pos] = r;
+  }
+
+  __device__ void overflow(uint32_t bit) {
+    if ((atomicOr(&C->overflow, bit) & bit) == 0) C->overflow_info = gid;
+  }
+
+  // ---- local event slots: Host::schedule_task_* / push_local_event (host.rs:703-722);
+  //      Event::new_local consumes an event id even if the event is then dropped ----
+  template <int SL>
+  __device__ __forceinline__ void schedule(uint64_t t) {
+    uint64_t e = eid++;
+    if (t >= S.end_time) return;
+    if (SL == SLOT_RO) { st0 = t; se0 = e; }
+    if (SL == SLOT_RI) { st1 = t; se1 = e; }
+    if (SL == SLOT_APP) { st2 = t; se2 = e; }
+  }
+
+  template <int W>
+  __device__ __forceinline__ uint32_t relay_state() const {
+    return W == 0 ? (fl & 3u) : ((fl >> F_RI_STATE_SHIFT) & 3u);
+  }
+  template <int W>
+  __device__ __forceinline__ void set_relay_state(uint32_t v) {
+    if (W == 0)
+      fl = (fl & ~3u) | v;
+    else
+      fl = (fl & ~(3u << F_RI_STATE_SHIFT)) | (v << F_RI_STATE_SHIFT);
+  }
+
+  // Relay::notify (relay/mod.rs:111-136) and forward_later (:145-163)
+  template <int W>
+  __device__ __forceinline__ void forward_later(uint64_t delay) {
+    set_relay_state<W>(RELAY_PENDING);
+    schedule<W == 0 ? SLOT_RO : SLOT_RI>(now + delay);
+  }
+  template <int W>
+  __device__ __forceinline__ void relay_notify() {
+    if (relay_state<W>() == RELAY_IDLE) forward_later<W>(0);
+  }
+
+  // ---- TokenBucket::comforming_remove (network/relay/token_bucket.rs:65-154) ----
+  template <int W>
+  __device__ bool tb_remove(uint64_t dec, uint64_t* dur) {
+    uint64_t& bal = W == 0 ? tbb0 : tbb1;
+    uint64_t& last = W == 0 ? tbl0 : tbl1;
+    const uint64_t cap = W == 0 ? tbc0 : tbc1;
+    const uint64_t inc = W == 0 ? tbi0 : tbi1;
+    const uint64_t interval = 1000000ULL;  // relay/mod.rs:279
+    // lazy_refill
+    uint64_t span = now - last;
+    if (span >= interval) {
+      uint64_t nref = span / interval;
+      uint64_t ntok = mul_sat(inc, nref, ~0ULL);
+      uint64_t b = bal + ntok;
+      if (b < bal) b = ~0ULL;
+      bal = b > cap ? cap : b;
+      uint64_t adv = mul_sat(interval, nref, SIMTIME_MAX);
+      last = emu_sat_add(last, adv);
+      span = now - last;
+    }
+    uint64_t next_refill_span = interval - span;
+    if (dec > bal) {
+      // compute_conforming_duration (:91-117)
+      uint64_t req = dec - bal;
+      uint64_t n = req / inc + ((req % inc) ? 1 : 0);
+      if (n == 0)
+        *dur = 0;
+      else if (n == 1)
+        *dur = next_refill_span;
+      else {
+        uint64_t m = mul_sat(interval, n - 1, SIMTIME_MAX);
+        uint64_t s = next_refill_span + m;
+        if (s < next_refill_span || s > SIMTIME_MAX) s = SIMTIME_MAX;
+        *dur = s;
+      }
+      return false;
+    }
+    bal -= dec;
+    return true;
+  }
+
+  // ---- CoDel (router/codel_queue.rs) on a per-host ring ----
+  __device__ __forceinline__ CodelEnt* cq_slot(uint32_t i) {
+    uint32_t idx = cq_head + i;
+    if (idx >= S.codel_cap) idx -= S.codel_cap;
+    return S.codel + (size_t)h * S.codel_cap + idx;
+  }
+  __device__ void codel_push(const EvRec& ev) {  // :303-317
+    if (cq_len >= S.codel_cap) {
+      overflow(OVF_CODEL);
+      return;
+    }
+    CodelEnt e;
+    e.enqueue_ts = now;
+    e.eid = ev.eid;
+    e.src = ev.src;
+    e.payload = ev.payload;
+    e.tag = ev.tag;
+    e.pad = 0;
+    *cq_slot(cq_len) = e;
+    cq_len++;
+    cq_bytes += (uint64_t)ev.payload + SGN_UDP_HEADER_BYTES;
+    if (cq_len > c_maxcodel) c_maxcodel = cq_len;
+  }
+  // process_standing_delay (:231-262)
+  __device__ bool codel_standing(uint64_t sd) {
+    if (sd < CODEL_TARGET || cq_bytes <= SGN_CONFIG_MTU) {
+      fl &= ~F_CODEL_IE;
+      return false;
+    }
+    if (fl & F_CODEL_IE) return now >= cq_ie;
+    fl |= F_CODEL_IE;
+    cq_ie = emu_sat_add(now, CODEL_INTERVAL);
+    return false;
+  }
+  // codel_pop (:204-227)
+  __device__ bool codel_pop_raw(Pkt* p, bool* ok_to_drop) {
+    if (cq_len == 0) {
+      fl &= ~F_CODEL_IE;
+      return false;
+    }
+    CodelEnt e = *cq_slot(0);
+    cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
+    cq_len--;
+    cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + SGN_UDP_HEADER_BYTES);
+    *ok_to_drop = codel_standing(sat_sub(now, e.enqueue_ts));
+    p->src = e.src;
+    p->dst_ip = my_ip;
+    p->payload = e.payload;
+    p->tag = e.tag;
+    p->eid = e.eid;
+    return true;
+  }
+  __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
+    c_codel++;
+    dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 63), p.eid);
+    trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
+  }
+  __device__ bool codel_was_dropping_recently() const {  // :273-281
+    if (!(fl & F_CODEL_DN)) return false;
+    return sat_sub(now, cq_dn) < CODEL_INTERVAL * 16;
+  }
+  // CoDelQueue::pop (:125-201)
+  __device__ bool codel_pop(Pkt* out) {
+    Pkt p;
+    bool okd;
+    if (!codel_pop_raw(&p, &okd)) {
+      fl &= ~F_CODEL_DROP;
+      return false;
+    }
+    if (!okd) {
+      fl &= ~F_CODEL_DROP;
+      *out = p;
+      return true;
+    }
+    if (!(fl & F_CODEL_DROP)) {
+      // drop_from_store_mode (:150-170)
+      codel_drop(p);
+      Pkt n;
+      bool nok;
+      bool has_n = codel_pop_raw(&n, &nok);
+      fl |= F_CODEL_DROP;
+      uint64_t delta = sat_sub(cq_cur, cq_prev);
+      cq_cur = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      fl |= F_CODEL_DN;
+      cq_dn = codel_law(now, cq_cur);
+      cq_prev = cq_cur;
+      if (has_n) *out = n;
+      return has_n;
+    }
+    // drop_from_drop_mode (:172-201)
+    bool has_item = true;
+    Pkt item = p;
+    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= cq_dn) {
+      codel_drop(item);
+      cq_cur++;
+      bool iok = false;
+      has_item = codel_pop_raw(&item, &iok);
+      if (has_item && iok)
+        cq_dn = codel_law(cq_dn, cq_cur);
+      else
+        fl &= ~F_CODEL_DROP;
+    }
+    if (has_item) *out = item;
+    return has_item;
+  }
+
+  // ---- synthetic socket send queue (interface qdisc source for relay_inet_out) ----
+  __device__ __forceinline__ FifoEnt* fq_slot(uint32_t i) {
+    uint32_t idx = fq_head + i;
+    if (idx >= S.fifo_cap) idx -= S.fifo_cap;
+    return S.fifo + (size_t)h * S.fifo_cap + idx;
+  }
+  __device__ bool fifo_push(uint32_t dst_ip, uint32_t payload, uint32_t last, uint32_t count,
+                            uint32_t tag) {
+    if (fq_len >= S.fifo_cap) return false;
+    FifoEnt e;
+    e.dst_ip = dst_ip;
+    e.pay = (payload & 0xFFFFu) | (last << 16);
+    e.count = count;
+    e.tag = tag;
+    *fq_slot(fq_len) = e;
+    fq_len++;
+    return true;
+  }
+  __device__ bool fifo_pop(Pkt* p) {
+    if (fq_len == 0) return false;
+    FifoEnt* s = fq_slot(0);
+    FifoEnt e = *s;
+    p->src = gid;
+    p->dst_ip = e.dst_ip;
+    p->payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
+    p->tag = e.tag;
+    p->eid = 0;
+    if (e.count == 1) {
+      fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
+      fq_len--;
+    } else {
+      s->count = e.count - 1;
+    }
+    return true;
+  }
+
+  // ---- Dns::addr_to_host_id (network/dns.rs:174) ----
+  __device__ __forceinline__ bool dns_lookup(uint32_t ip, uint32_t* host) const {
+    uint32_t i = (ip * 0x9E3779B1u) & S.dns_mask;
+    while (true) {
+      uint32_t k = S.dns_key[i];
+      if (k == ip) {
+        *host = S.dns_val[i];
+        return true;
+      }
+      if (k == 0) return false;
+      i = (i + 1) & S.dns_mask;
+    }
+  }
+
+  // push_packet_to_host (core/worker.rs:603-613) into the calendar / exchange slot
+  __device__ void emit(uint32_t dst, uint64_t t, uint32_t payload, uint32_t tag, uint64_t e) {
+    EvRec r;
+    r.time = t;
+    r.eid = e;
+    r.src = gid;
+    r.dst = dst;
+    r.payload = payload;
+    r.tag = tag;
+    if (dst - S.lo < S.nH) {
+      uint32_t b = bucket_of(S, t);
+      uint32_t pos;
+      uint64_t base;
+      if (b == b1) {
+        pos = atomicAdd(&C->keep_n, 1u);
+        base = b1_keep_base;
+        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)t);
+      } else {
+        pos = atomicAdd(&S.bucket_n[b], 1u);
+        base = S.bucket_base[b];
+        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)t);
+      }
+      if (pos >= S.BC) {
+        overflow(OVF_BUCKET);
+        return;
+      }
+      S.pool[base + pos] = r;
+    } else {
+      // owner rank of dst: contiguous ranges
+      uint32_t lo = 0, hi = S.n_ranks;
+      while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
+      }
+      uint32_t pos = atomicAdd(&S.xout_n[lo], 1u);
+      if (pos >= S.xslot) {
+        overflow(OVF_EXCHANGE);
+        return;
+      }
+      S.xout[(size_t)lo * S.xslot + pos] = r;
+    }
+  }
+
+  // ---- Worker::send_packet (core/worker.rs:330-403) ----
+  __device__ void send_packet(const Pkt& p) {
+    if (now >= S.end_time) return;  // is_completed: no draw, nothing recorded
+    const bool boot = now < S.boot_end;
+    uint32_t dst;
+    if (!dns_lookup(p.dst_ip, &dst)) {  // InetDropped, no draw (:347-357)
+      c_unknown++;
+      dtx = sgn_digest3(dtx, now, 0xFFFFFFFFULL | (2ULL << 32), 0);
+      trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+      return;
+    }
+    const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
+    const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);  // :532-537 (f32), widened :363-365
+    const double reliability = (double)rel32;
+    const double chance = rng_f64();                   // :366
+    if (!boot && chance >= reliability && p.payload > 0) {  // :371
+      c_loss++;
+      dtx = sgn_digest3(dtx, now, (uint64_t)dst | (1ULL << 32), 0);
+      trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+      return;
+    }
+    const uint64_t delay = S.rlat[ri];  // :376
+    if (S.dynamic && delay < lat_cache) {  // update_lowest_used_latency (:297-308)
+      lat_cache = delay;
+      atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
+    }
+    uint64_t deliver = now + delay;  // :387-390
+    if (deliver < we) deliver = we;
+    const uint64_t e = eid++;  // Event::new_packet: the SOURCE host's counter (event.rs:27)
+    c_sent++;
+    dtx = sgn_digest3(dtx, now, (uint64_t)dst, deliver);
+    trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+    emit(dst, deliver, p.payload, p.tag, e);
+  }
+
+  // interface delivery to the synthetic app (NetworkInterface::push -> socket)
+  __device__ void deliver_to_app(const Pkt& p, bool local) {
+    if (local) {
+      c_ldeliv++;
+      dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 62), p.payload);
+      return;
+    }
+    c_deliv++;
+    c_bytes += p.payload;
+    dapp = sgn_digest3(dapp, now, p.src, p.eid);
+    trace(SGN_TRACE_DELIVER, p.src, 0, now, 0, p.eid);
+    if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (p.tag & SGN_TAG_REQ)) {
+      const uint64_t size = S.file_bytes[p.tag & 3u];
+      const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
+      if (n == 0) return;
+      const uint32_t last = (uint32_t)(size - (n - 1) * SGN_TGEN_MSS);
+      if (fifo_push(S.ip[p.src], SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
+        relay_notify<0>();
+      else
+        c_blocked++;
+    }
+  }
+
+  // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) ----
+  template <int W>
+  __device__ bool forward_until_blocked(uint64_t* dur) {
+    const bool boot = now < S.boot_end;
+    set_relay_state<W>(RELAY_FORWARDING);
+    const uint32_t src_addr = W == 0 ? my_ip : 0u;  // eth0 / router (0.0.0.0)
+    while (true) {
+      Pkt p;
+      const uint32_t next_bit = W == 0 ? F_RO_NEXT : F_RI_NEXT;
+      if (fl & next_bit) {
+        fl &= ~next_bit;
+        if (W == 0) {
+          p.src = gid;
+          p.dst_ip = ro_dst;
+          p.payload = ro_pay;
+          p.tag = ro_tag;
+          p.eid = 0;
+        } else {
+          p.src = ri_src;
+          p.dst_ip = my_ip;
+          p.payload = ri_pay;
+          p.tag = ri_tag;
+          p.eid = ri_eid;
+        }
+      } else {
+        bool got = W == 0 ? fifo_pop(&p) : codel_pop(&p);
+        if (!got) {
+          set_relay_state<W>(RELAY_IDLE);
+          return false;
+        }
+      }
+      const bool is_local = src_addr == p.dst_ip;
+      if (!boot && !is_local) {
+        if (!tb_remove<W>((uint64_t)p.payload + SGN_UDP_HEADER_BYTES, dur)) {
+          fl |= next_bit;
+          if (W == 0) {
+            ro_dst = p.dst_ip;
+            ro_pay = p.payload;
+            ro_tag = p.tag;
+          } else {
+            ri_src = p.src;
+            ri_pay = p.payload;
+            ri_tag = p.tag;
+            ri_eid = p.eid;
+          }
+          set_relay_state<W>(RELAY_IDLE);
+          return true;
+        }
+      }
+      if (is_local)
+        deliver_to_app(p, true);
+      else if (W == 0)
+        send_packet(p);  // Router::push -> route_outgoing_packet (router/mod.rs:48-73)
+      else
+        deliver_to_app(p, false);
+    }
+  }
+
+  // run_forward_task + forward_now (relay/mod.rs:166-187)
+  template <int W>
+  __device__ void run_forward_task() {
+    set_relay_state<W>(RELAY_IDLE);
+    uint64_t dur;
+    if (forward_until_blocked<W>(&dur)) forward_later<W>(dur);
+  }
+
+  __device__ void app_task() {
+    const uint64_t k = app_k++;
+    uint32_t dst_ip, payload, tag;
+    uint64_t next_delay;
+    if (S.tkind == SGN_TRAFFIC_PERIODIC) {
+      uint32_t peer = 0, uip = 0;
+      if (sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip))
+        dst_ip = S.ip[peer];
+      else
+        dst_ip = uip;
+      payload = S.payload_len;
+      tag = SGN_TAG_DATA;
+      next_delay = S.period;
+    } else {
+      uint32_t si = 0, cls = 0;
+      sgn_tgen_fetch(S.flow_seed, gid, k, S.n_servers, &si, &cls);
+      dst_ip = S.ip[S.servers[si]];
+      payload = S.req_payload;
+      tag = SGN_TAG_REQ | cls;
+      next_delay = sgn_tgen_think(S.flow_seed, gid, k, S.period, S.period_jitter);
+    }
+    if (fifo_push(dst_ip, payload, payload, 1, tag))
+      relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
+    else
+      c_blocked++;
+    schedule<SLOT_APP>(now + next_delay);
+  }
+
+  // ---- Host::execute (host.rs:762-830) over the ordered segment + local slots ----
+  __device__ void run(uint32_t s0, uint32_t s1) {
+    EvRec* seg = S.seg;
+    // order the segment by (time, src host, src event id)
+    for (uint32_t i = s0 + 1; i < s1; i++) {
+      EvRec x = seg[i];
+      uint32_t j = i;
+      while (j > s0) {
+        EvRec y = seg[j - 1];
+        if (!ev_less(x, y)) break;
+        seg[j] = y;
+        j--;
+      }
+      seg[j] = x;
+    }
+    uint32_t pi = s0;
+    while (true) {
+      // earliest local event by (time, event id)
+      uint64_t lt = st0, le = se0;
+      int ls = 0;
+      if (st1 < lt || (st1 == lt && se1 < le)) { lt = st1; le = se1; ls = 1; }
+      if (st2 < lt || (st2 == lt && se2 < le)) { lt = st2; le = se2; ls = 2; }
+      if (pi < s1) {
+        const uint64_t pt = seg[pi].time;
+        if (pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+          EvRec ev = seg[pi];
+          pi++;
+          now = ev.time;
+          c_popped++;
+          drx = sgn_digest3(drx, ev.time, ev.src, ev.eid);
+          trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid);
+          codel_push(ev);     // Router::route_incoming_packet (router/mod.rs:55-57)
+          relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
+          continue;
+        }
+      }
+      if (lt >= we) break;
+      now = lt;
+      c_localev++;
+      if (ls == 0) {
+        st0 = INVALID;
+        run_forward_task<0>();
+      } else if (ls == 1) {
+        st1 = INVALID;
+        run_forward_task<1>();
+      } else {
+        st2 = INVALID;
+        app_task();
+      }
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Round kernels
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void due_buckets(const DevSim& S, const Ctrl* C, uint32_t* b0,
+                                            uint32_t* b1, uint32_t* n0, uint32_t* n1) {
+  *b0 = bucket_of(S, C->ws);
+  *b1 = bucket_of(S, C->we - 1);
+  *n0 = S.bucket_n[*b0];
+  *n1 = *b1 != *b0 ? S.bucket_n[*b1] : 0;
+}
+
+__global__ __launch_bounds__(256) void k_count(DevSim S) {
+  const Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint64_t we = C->we;
+  uint32_t b0, b1, n0, n1;
+  due_buckets(S, C, &b0, &b1, &n0, &n1);
+  n0 = min(n0, S.BC);
+  n1 = min(n1, S.BC);
+  const uint32_t total = n0 + n1;
+  const uint64_t base0 = S.bucket_base[b0], base1 = S.bucket_base[b1];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const EvRec* e = i < n0 ? &S.pool[base0 + i] : &S.pool[base1 + (i - n0)];
+    const uint64_t t = e->time;
+    if (t < we) atomicAdd(&S.hist[e->dst - S.lo], 1u);
+  }
+}
+
+// per-block sums of hist over SCAN_BLOCKS tiles
+__global__ __launch_bounds__(256) void k_scan_reduce(DevSim S) {
+  const Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint32_t nH = S.nH;
+  const uint32_t tile = (nH + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
+  const uint32_t beg = blockIdx.x * tile;
+  const uint32_t end = min(nH, beg + tile);
+  uint32_t s = 0;
+  for (uint32_t i = beg + threadIdx.x; i < end; i += blockDim.x) s += S.hist[i];
+  __shared__ uint32_t sh[4];
+  s = wave_sum_u32(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) S.block_sums[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint32_t nH = S.nH;
+  const uint32_t tile = (nH + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
+  const uint32_t beg = blockIdx.x * tile;
+  const uint32_t end = min(nH, beg + tile);
+  __shared__ uint32_t sh[8];
+  // prefix of earlier tiles
+  uint32_t p = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += blockDim.x) p += S.block_sums[i];
+  p = wave_sum_u32(p);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = p;
+  __syncthreads();
+  uint32_t carry = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t c0 = beg; c0 < end; c0 += blockDim.x) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t v = i < end ? S.hist[i] : 0;
+    // inclusive wave scan
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (int k = 0; k < w; k++) wpre += sh[k];
+    const uint32_t total = sh[0] + sh[1] + sh[2] + sh[3];
+    const uint32_t excl = carry + wpre + x - v;
+    if (i < end) {
+      S.seg_start[i] = excl;
+      S.cursor[i] = excl;
+    }
+    carry += total;
+    __syncthreads();
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    // grand total (every tile's sum) closes the offsets
+    uint32_t tot = 0;
+    for (int i = 0; i < SCAN_BLOCKS; i++) tot += S.block_sums[i];
+    S.seg_start[nH] = tot;
+    if (tot > S.seg_cap) {
+      if ((atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0) C->overflow_info = tot;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scatter(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint64_t we = C->we;
+  uint32_t b0, b1, n0, n1;
+  due_buckets(S, C, &b0, &b1, &n0, &n1);
+  n0 = min(n0, S.BC);
+  n1 = min(n1, S.BC);
+  const uint32_t total = n0 + n1;
+  const uint64_t base0 = S.bucket_base[b0], base1 = S.bucket_base[b1];
+  const uint64_t keep_base = C->keep_base;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const EvRec e = i < n0 ? S.pool[base0 + i] : S.pool[base1 + (i - n0)];
+    if (e.time < we) {
+      const uint32_t pos = atomicAdd(&S.cursor[e.dst - S.lo], 1u);
+      if (pos < S.seg_cap) S.seg[pos] = e;
+    } else {
+      const uint32_t pos = atomicAdd(&C->keep_n, 1u);
+      atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)e.time);
+      if (pos < S.BC)
+        S.pool[keep_base + pos] = e;
+      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+        C->overflow_info = e.dst;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_execute(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  __shared__ uint64_t sh[4];
+  const uint64_t we = C->we;
+  const uint32_t b1 = bucket_of(S, we - 1);
+  const uint64_t keep_base = C->keep_base;
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t my_min = INVALID;
+  if (h < S.nH) {
+    const uint32_t s0 = S.seg_start[h], s1 = S.seg_start[h + 1];
+    S.hist[h] = 0;
+    const uint32_t nH = S.nH;
+    const uint64_t t0 = S.slot_t[h], t1 = S.slot_t[nH + h], t2 = S.slot_t[2 * nH + h];
+    uint64_t lmin = t0 < t1 ? t0 : t1;
+    lmin = t2 < lmin ? t2 : lmin;
+    if (s0 == s1 && lmin >= we) {
+      my_min = lmin;  // nothing due: the host sleeps through this window
+    } else {
+      HostExec ex(S, h, we, b1, keep_base);
+      ex.run(s0, s1);
+      my_min = ex.next_local_time();
+      ex.store();
+    }
+  }
+  const uint64_t m = block_min_u64(my_min, sh);
+  if (threadIdx.x == 0 && m != INVALID)
+    atomicMin((unsigned long long*)&C->round_min, (unsigned long long)m);
+}
+
+// Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
+// window; multi-shard runs reduce C->round_min/min_used across ranks first.
+__global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  __shared__ uint64_t sh[16];
+  __shared__ uint32_t shb0, shb1;
+  if (threadIdx.x == 0) {
+    const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
+    if (b0 != b1) {
+      S.bucket_n[b0] = 0;
+      S.bucket_min[b0] = INVALID;
+    }
+    const uint64_t old = S.bucket_base[b1];
+    S.bucket_base[b1] = C->keep_base;
+    C->keep_base = old;
+    const uint32_t kn = C->keep_n;
+    S.bucket_n[b1] = kn;
+    S.bucket_min[b1] = C->keep_min;
+    C->keep_n = 0;
+    C->keep_min = INVALID;
+    shb0 = b0;
+    shb1 = b1;
+  }
+  __syncthreads();
+  uint64_t m = INVALID;
+  uint32_t mx = 0;
+  for (uint32_t b = threadIdx.x; b < S.NB; b += blockDim.x) {
+    const uint32_t n = S.bucket_n[b];
+    if (n > 0) {
+      const uint64_t bm = S.bucket_min[b];
+      m = bm < m ? bm : m;
+    }
+    mx = n > mx ? n : mx;
+  }
+  m = wave_min_u64(m);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = __shfl_xor(mx, off, 64);
+    mx = o > mx ? o : mx;
+  }
+  __shared__ uint32_t shx[16];
+  if ((threadIdx.x & 63) == 0) {
+    sh[threadIdx.x >> 6] = m;
+    shx[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) {
+      m = sh[i] < m ? sh[i] : m;
+      mx = shx[i] > mx ? shx[i] : mx;
+    }
+    if (mx > C->max_bucket) C->max_bucket = mx;
+    m = C->round_min < m ? C->round_min : m;
+    C->round_min = m;  // local minimum (reduced across shards when advance == 0)
+    if (advance) {
+      const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
+      C->last_min_next = min_next;
+      // Runahead::get (runahead.rs:44-57)
+      uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
+      ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+      // Controller::manager_finished_current_round (controller.rs:88-112)
+      uint64_t ne = min_next + ra;
+      if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
+      ne = ne < S.end_time ? ne : S.end_time;
+      C->active = min_next < ne ? 1u : 0u;
+      C->ws = min_next;
+      C->we = ne;
+      C->round_min = INVALID;
+      C->rounds++;
+    }
+  }
+  (void)shb0;
+  (void)shb1;
+}
+
+// Multi-shard: window advance from the all-reduced {min_next, min_used}.
+__global__ void k_advance(DevSim S, const uint64_t* red) {
+  Ctrl* C = S.ctrl;
+  if (!C->active || threadIdx.x != 0) return;
+  const uint64_t m = red[0];
+  if (S.dynamic && red[1] != INVALID && red[1] < C->min_used) C->min_used = red[1];
+  const uint64_t min_next = m == INVALID ? EMU_MAX : m;
+  C->last_min_next = min_next;
+  uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
+  ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+  uint64_t ne = min_next + ra;
+  if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
+  ne = ne < S.end_time ? ne : S.end_time;
+  C->active = min_next < ne ? 1u : 0u;
+  C->ws = min_next;
+  C->we = ne;
+  C->round_min = INVALID;
+  C->remote_min = INVALID;
+  C->rounds++;
+}
+
+// Multi-shard: file received events into the local calendar.
+__global__ __launch_bounds__(256) void k_import(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint32_t b1 = bucket_of(S, C->we - 1);
+  const uint64_t keep_base = C->keep_base;
+  for (uint32_t r = 0; r < S.n_ranks; r++) {
+    const uint32_t n = min(S.xin_n[r], S.xslot);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += gridDim.x * blockDim.x) {
+      const EvRec e = S.xin[(size_t)r * S.xslot + i];
+      const uint32_t b = bucket_of(S, e.time);
+      uint32_t pos;
+      uint64_t base;
+      if (b == b1) {
+        pos = atomicAdd(&C->keep_n, 1u);
+        base = keep_base;
+        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)e.time);
+      } else {
+        pos = atomicAdd(&S.bucket_n[b], 1u);
+        base = S.bucket_base[b];
+        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)e.time);
+      }
+      if (pos < S.BC)
+        S.pool[base + pos] = e;
+      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+        C->overflow_info = e.dst;
+    }
+  }
+}
+
+// CoDel control-law self test (f64 sqrt/div/round on the device vs the host).
+__global__ void k_codel_law_test(uint64_t n, uint64_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = codel_law(SIM_START, i) - SIM_START;
+}
+
+}  // namespace sgn
+
+// ====================================================================================
+// Host side: sim init, round launch, readback
+// ====================================================================================
+using namespace sgn;
+
+namespace {
+
+inline uint64_t host_splitmix(uint64_t& s) {
+  s += 0x9e3779b97f4a7c15ULL;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+T* dalloc(sgn_ctx* ctx, size_t n) {
+  return (T*)dev_alloc(ctx, n * sizeof(T));
+}
+
+enum { K_COUNT = 0, K_SCAN_R, K_SCAN_A, K_SCATTER, K_EXECUTE, K_FINALIZE, K_IMPORT, K_ADVANCE };
+const char* kKernelNames[8] = {"k_count", "k_scan_reduce", "k_scan_apply", "k_scatter",
+                               "k_execute", "k_finalize", "k_import", "k_advance"};
+
+int launch_round(sgn_ctx* ctx);
+
+}  // namespace
+
+
+namespace {
+
+int launch_round(sgn_ctx* ctx) {
+  DevSim& S = ctx->S;
+  hipStream_t st = ctx->stream;
+  const uint32_t grid_ev = 1024;
+  const uint32_t grid_h = (S.nH + 255) / 256;
+  time_begin(ctx, K_COUNT);
+  hipLaunchKernelGGL(k_count, dim3(grid_ev), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_SCAN_R);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(SCAN_BLOCKS), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_SCAN_A);
+  hipLaunchKernelGGL(k_scan_apply, dim3(SCAN_BLOCKS), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_SCATTER);
+  hipLaunchKernelGGL(k_scatter, dim3(grid_ev), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_EXECUTE);
+  hipLaunchKernelGGL(k_execute, dim3(grid_h), dim3(256), 0, st, S);
+  time_end(ctx);
+  if (ctx->nranks > 1) {
+    // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
+    int rc = comm_round_exchange(ctx);
+    if (rc) return rc;
+  } else {
+    time_begin(ctx, K_FINALIZE);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, st, S, 1);
+    time_end(ctx);
+  }
+  SGN_HIP(ctx, hipGetLastError());
+  ctx->rounds_enqueued++;
+  return 0;
+}
+
+int check_overflow(sgn_ctx* ctx) {
+  const Ctrl& c = *ctx->h_ctrl;
+  if (c.overflow == 0) return 0;
+  std::string what;
+  if (c.overflow & OVF_BUCKET) what += " calendar bucket (raise sgn_sim_config.event_capacity)";
+  if (c.overflow & OVF_CODEL) what += " CoDel ring (raise sgn_sim_config.codel_cap)";
+  if (c.overflow & OVF_SEG) what += " due-event segment buffer";
+  if (c.overflow & OVF_EXCHANGE) what += " exchange slot (raise exchange_slot_events)";
+  if (c.overflow & OVF_TRACE) what += " trace buffer";
+  return set_error(ctx, SGN_EOVERFLOW,
+                   "device capacity exceeded:" + what + " (info " +
+                       std::to_string(c.overflow_info) + "); results are invalid");
+}
+
+int sync_ctrl(sgn_ctx* ctx) {
+  SGN_HIP(ctx, hipMemcpyAsync(ctx->h_ctrl, ctx->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  time_collect(ctx);
+  return check_overflow(ctx);
+}
+
+}  // namespace
+
+namespace sgn {
+
+void time_begin(sgn_ctx* ctx, int kernel) {
+  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  if (ctx->ev_next >= ctx->ev_pool.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+    ctx->ev_pool.push_back({a, b});
+  }
+  hipEventRecord(ctx->ev_pool[ctx->ev_next].first, ctx->stream);
+  ctx->ev_pending.push_back({kernel, ctx->ev_next});
+}
+
+void time_end(sgn_ctx* ctx) {
+  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  if (ctx->ev_pending.empty() || ctx->ev_pending.back().second != ctx->ev_next) return;
+  hipEventRecord(ctx->ev_pool[ctx->ev_next].second, ctx->stream);
+  ctx->ev_next++;
+}
+
+void time_collect(sgn_ctx* ctx) {
+  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  for (auto& p : ctx->ev_pending) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->ev_pool[p.second].first, ctx->ev_pool[p.second].second) ==
+        hipSuccess) {
+      ctx->kt[p.first].ms += ms;
+      ctx->kt[p.first].launches++;
+    }
+  }
+  ctx->ev_pending.clear();
+  ctx->ev_next = 0;
+}
+
+void free_sim(sgn_ctx* ctx) {
+  for (void* p : ctx->allocs) hipFree(p);
+  ctx->allocs.clear();
+  if (ctx->h_ctrl) {
+    hipHostFree(ctx->h_ctrl);
+    ctx->h_ctrl = nullptr;
+  }
+  ctx->sim_ready = false;
+}
+
+}  // namespace sgn
+
+extern "C" {
+
+int sgn_trace_enable(sgn_ctx* ctx, uint64_t capacity) {
+  if (!ctx) return SGN_EINVAL;
+  if (ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "sgn_trace_enable must precede sgn_sim_init");
+  ctx->trace_cap = capacity;
+  return 0;
+}
+
+int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr) {
+  if (!ctx || !cfg || !tr) return SGN_EINVAL;
+  if (!ctx->routes_ready) return set_error(ctx, SGN_ESTATE, "sgn_routes_build must precede sgn_sim_init");
+  if (!ctx->hosts_ready) return set_error(ctx, SGN_ESTATE, "sgn_hosts_set must precede sgn_sim_init");
+  if (tr->kind != SGN_TRAFFIC_PERIODIC && tr->kind != SGN_TRAFFIC_TGEN)
+    return set_error(ctx, SGN_EINVAL, "unknown traffic kind");
+  if (cfg->out_fifo_cap == 0 || cfg->codel_cap == 0)
+    return set_error(ctx, SGN_EINVAL, "out_fifo_cap and codel_cap must be >= 1");
+  if (tr->kind == SGN_TRAFFIC_PERIODIC && tr->payload_len > 0xFFFFu)
+    return set_error(ctx, SGN_EINVAL, "payload_len must fit a UDP datagram");
+  if (tr->kind == SGN_TRAFFIC_TGEN && (tr->n_servers == 0 || !tr->server_hosts))
+    return set_error(ctx, SGN_EINVAL, "TGEN traffic needs servers");
+  if (tr->kind == SGN_TRAFFIC_TGEN && tr->req_payload > 0xFFFFu)
+    return set_error(ctx, SGN_EINVAL, "req_payload must fit a UDP datagram");
+  if (ctx->sim_ready) free_sim(ctx);
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+
+  DevSim S{};
+  const uint32_t nH = ctx->hi - ctx->lo;
+  const uint32_t N = ctx->n_all;
+  S.n_all = N;
+  S.lo = ctx->lo;
+  S.nH = nH;
+  S.U = ctx->U;
+  S.end_time = SIM_START + cfg->stop_time_ns;
+  S.boot_end = SIM_START + cfg->bootstrap_end_ns;
+  S.runahead_cfg = cfg->runahead_ns;
+  S.dynamic = cfg->use_dynamic_runahead ? 1 : 0;
+  S.fifo_cap = cfg->out_fifo_cap;
+  S.codel_cap = cfg->codel_cap;
+  S.trace_on = ctx->trace_cap > 0;
+  S.tkind = tr->kind;
+  S.payload_len = tr->payload_len;
+  S.unknown_permille = tr->unknown_dst_permille;
+  S.req_payload = tr->req_payload;
+  S.n_servers = tr->kind == SGN_TRAFFIC_TGEN ? tr->n_servers : 0;
+  S.flow_seed = tr->flow_seed;
+  S.period = tr->period_ns;
+  S.period_jitter = tr->period_jitter_ns;
+  for (int i = 0; i < 3; i++) S.file_bytes[i] = tr->file_bytes[i];
+
+  uint64_t min_possible = ~0ULL, max_lat = 0;
+  for (uint64_t v : ctx->h_lat) {
+    min_possible = std::min(min_possible, v);
+    max_lat = std::max(max_lat, v);
+  }
+  S.min_possible = min_possible;
+  if (min_possible == 0) return set_error(ctx, SGN_EINVAL, "route latency 0 (Runahead::new asserts)");
+
+  // routing (device copies made by sgn_routes_build)
+  S.rlat = ctx->d_lat;
+  S.rloss = ctx->d_loss;
+  uint32_t* d_unode = dalloc<uint32_t>(ctx, N);
+  uint32_t* d_ip = dalloc<uint32_t>(ctx, N);
+  uint32_t* d_dk = dalloc<uint32_t>(ctx, ctx->dns_key.size());
+  uint32_t* d_dv = dalloc<uint32_t>(ctx, ctx->dns_val.size());
+  if (!d_unode || !d_ip || !d_dk || !d_dv) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+  SGN_HIP(ctx, hipMemcpy(d_unode, ctx->unode.data(), N * 4, hipMemcpyHostToDevice));
+  SGN_HIP(ctx, hipMemcpy(d_ip, ctx->ip.data(), N * 4, hipMemcpyHostToDevice));
+  SGN_HIP(ctx, hipMemcpy(d_dk, ctx->dns_key.data(), ctx->dns_key.size() * 4, hipMemcpyHostToDevice));
+  SGN_HIP(ctx, hipMemcpy(d_dv, ctx->dns_val.data(), ctx->dns_val.size() * 4, hipMemcpyHostToDevice));
+  S.unode = d_unode;
+  S.ip = d_ip;
+  S.dns_key = d_dk;
+  S.dns_val = d_dv;
+  S.dns_mask = ctx->dns_mask;
+  std::vector<uint8_t> is_server(N, 0);
+  if (tr->kind == SGN_TRAFFIC_TGEN) {
+    uint32_t* d_sv = dalloc<uint32_t>(ctx, tr->n_servers);
+    if (!d_sv) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+    for (uint32_t i = 0; i < tr->n_servers; i++) {
+      if (tr->server_hosts[i] >= N) return set_error(ctx, SGN_EINVAL, "server host out of range");
+      is_server[tr->server_hosts[i]] = 1;
+    }
+    SGN_HIP(ctx, hipMemcpy(d_sv, tr->server_hosts, tr->n_servers * 4, hipMemcpyHostToDevice));
+    S.servers = d_sv;
+  }
+
+  // ---- per-host state, initialised on the host ----
+  std::vector<uint64_t> r0(nH), r1(nH), r2(nH), r3(nH), eid(nH, 0), app_k(nH, 0);
+  std::vector<uint64_t> slot_t(3 * (size_t)nH, INVALID), slot_e(3 * (size_t)nH, 0);
+  std::vector<uint32_t> flags(nH, 0);
+  std::vector<uint64_t> tb_bal(2 * (size_t)nH), tb_last(2 * (size_t)nH, SIM_START),
+      tb_cap(2 * (size_t)nH), tb_inc(2 * (size_t)nH);
+  std::vector<uint64_t> dig(nH, SGN_DIGEST_SEED);
+  for (uint32_t h = 0; h < nH; h++) {
+    const uint32_t g = ctx->lo + h;
+    // Xoshiro256PlusPlus::seed_from_u64 (SplitMix64 fill), host.rs:234
+    uint64_t sm = ctx->seed[g];
+    r0[h] = host_splitmix(sm);
+    r1[h] = host_splitmix(sm);
+    r2[h] = host_splitmix(sm);
+    r3[h] = host_splitmix(sm);
+    // create_token_bucket (relay/mod.rs:278-288) for inet_out (up) and inet_in (down)
+    for (int w = 0; w < 2; w++) {
+      const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
+      const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
+      tb_inc[(size_t)w * nH + h] = inc;
+      tb_cap[(size_t)w * nH + h] = inc + SGN_CONFIG_MTU;
+      tb_bal[(size_t)w * nH + h] = inc + SGN_CONFIG_MTU;
+    }
+    if (is_server[g]) flags[h] |= F_SERVER;
+    const bool has_app = tr->kind == SGN_TRAFFIC_PERIODIC || (tr->kind == SGN_TRAFFIC_TGEN && !is_server[g]);
+    if (has_app) {
+      flags[h] |= F_HAS_APP;
+      const uint64_t t = SIM_START + sgn_app_start_rel(tr->flow_seed, g, tr->start_ns, tr->start_jitter_ns);
+      const uint64_t e = eid[h]++;
+      if (t < S.end_time) {
+        slot_t[2 * (size_t)nH + h] = t;
+        slot_e[2 * (size_t)nH + h] = e;
+      }
+    }
+  }
+  auto up64 = [&](const std::vector<uint64_t>& v, uint64_t** out) -> int {
+    *out = dalloc<uint64_t>(ctx, v.size());
+    if (!*out) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+    SGN_HIP(ctx, hipMemcpy(*out, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+    return 0;
+  };
+  auto up32 = [&](const std::vector<uint32_t>& v, uint32_t** out) -> int {
+    *out = dalloc<uint32_t>(ctx, v.size());
+    if (!*out) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+    SGN_HIP(ctx, hipMemcpy(*out, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    return 0;
+  };
+  int rc = 0;
+  if ((rc = up64(r0, &S.rng0)) || (rc = up64(r1, &S.rng1)) || (rc = up64(r2, &S.rng2)) ||
+      (rc = up64(r3, &S.rng3)) || (rc = up64(eid, &S.eid)) || (rc = up64(app_k, &S.app_k)) ||
+      (rc = up64(slot_t, &S.slot_t)) || (rc = up64(slot_e, &S.slot_e)) ||
+      (rc = up32(flags, &S.flags)) || (rc = up64(tb_bal, &S.tb_bal)) ||
+      (rc = up64(tb_last, &S.tb_last)) || (rc = up64(tb_cap, &S.tb_cap)) ||
+      (rc = up64(tb_inc, &S.tb_inc)) || (rc = up64(dig, &S.d_tx)) || (rc = up64(dig, &S.d_rx)) ||
+      (rc = up64(dig, &S.d_app)))
+    return rc;
+  S.ro_dst = dalloc<uint32_t>(ctx, nH);
+  S.ro_pay = dalloc<uint32_t>(ctx, nH);
+  S.ro_tag = dalloc<uint32_t>(ctx, nH);
+  S.ri_src = dalloc<uint32_t>(ctx, nH);
+  S.ri_pay = dalloc<uint32_t>(ctx, nH);
+  S.ri_tag = dalloc<uint32_t>(ctx, nH);
+  S.ri_eid = dalloc<uint64_t>(ctx, nH);
+  S.codel = dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
+  S.cq_head = dalloc<uint32_t>(ctx, nH);
+  S.cq_len = dalloc<uint32_t>(ctx, nH);
+  S.cq_bytes = dalloc<uint64_t>(ctx, nH);
+  S.cq_ie = dalloc<uint64_t>(ctx, nH);
+  S.cq_dn = dalloc<uint64_t>(ctx, nH);
+  S.cq_cur = dalloc<uint64_t>(ctx, nH);
+  S.cq_prev = dalloc<uint64_t>(ctx, nH);
+  S.fifo = dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
+  S.fq_head = dalloc<uint32_t>(ctx, nH);
+  S.fq_len = dalloc<uint32_t>(ctx, nH);
+  S.cnt = dalloc<uint64_t>(ctx, (size_t)NCNT * nH);
+  S.trace_seq = dalloc<uint64_t>(ctx, nH);
+  if (!S.ro_dst || !S.ro_pay || !S.ro_tag || !S.ri_src || !S.ri_pay || !S.ri_tag || !S.ri_eid ||
+      !S.codel || !S.cq_head || !S.cq_len || !S.cq_bytes || !S.cq_ie || !S.cq_dn || !S.cq_cur ||
+      !S.cq_prev || !S.fifo || !S.fq_head || !S.fq_len || !S.cnt || !S.trace_seq)
+    return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
+
+  // ---- calendar: bucket width >= any window length, horizon > max latency ----
+  uint64_t rmax = S.dynamic ? std::max(max_lat, cfg->runahead_ns)
+                            : std::max(min_possible, cfg->runahead_ns);
+  uint64_t BW = std::max<uint64_t>(1, rmax);
+  uint64_t NB = max_lat / BW + 4;
+  if (NB > (1u << 20)) return set_error(ctx, SGN_EINVAL, "calendar would need > 2^20 buckets");
+  uint64_t cap = cfg->event_capacity ? cfg->event_capacity : (1ULL << 22);
+  uint64_t BC = cap / (NB + 1);
+  if (BC < 256) BC = 256;
+  if (BC > 0x7FFFFFFFULL) BC = 0x7FFFFFFFULL;
+  S.NB = (uint32_t)NB;
+  S.BC = (uint32_t)BC;
+  S.BW = BW;
+  S.pool = dalloc<EvRec>(ctx, (NB + 1) * BC);
+  std::vector<uint64_t> bbase(NB);
+  for (uint64_t b = 0; b < NB; b++) bbase[b] = b * BC;
+  if (!S.pool) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event pool)");
+  if ((rc = up64(bbase, &S.bucket_base))) return rc;
+  S.bucket_n = dalloc<uint32_t>(ctx, NB);
+  std::vector<uint64_t> bmin(NB, INVALID);
+  if ((rc = up64(bmin, &S.bucket_min))) return rc;
+  uint64_t segcap = std::min<uint64_t>(2 * BC, 0xFFFFFFF0ULL);
+  S.seg_cap = (uint32_t)segcap;
+  S.seg = dalloc<EvRec>(ctx, segcap);
+  S.hist = dalloc<uint32_t>(ctx, nH + 1);
+  S.seg_start = dalloc<uint32_t>(ctx, nH + 1);
+  S.cursor = dalloc<uint32_t>(ctx, nH + 1);
+  S.block_sums = dalloc<uint32_t>(ctx, SCAN_BLOCKS);
+  if (!S.bucket_n || !S.seg || !S.hist || !S.seg_start || !S.cursor || !S.block_sums)
+    return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar)");
+  if (ctx->trace_cap) {
+    S.trace = dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
+    if (!S.trace) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
+    S.trace_cap = ctx->trace_cap;
+  }
+  // multi-GPU exchange slots
+  S.n_ranks = ctx->nranks;
+  S.rank = ctx->rank;
+  {
+    std::vector<uint32_t> rl(ctx->nranks + 1);
+    for (uint32_t r = 0; r <= ctx->nranks; r++) {
+      uint32_t lo = 0, hi = 0;
+      sgn_shard_range(N, r < ctx->nranks ? r : ctx->nranks - 1, ctx->nranks, &lo, &hi);
+      rl[r] = r < ctx->nranks ? lo : N;
+    }
+    if ((rc = up32(rl, (uint32_t**)&S.rank_lo))) return rc;
+  }
+  if (ctx->nranks > 1) {
+    if (!ctx->comm) return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init before sgn_sim_init");
+    S.xslot = (uint32_t)ctx->xslot;
+    S.xout = dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
+    S.xin = dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
+    S.xout_n = dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    S.xin_n = dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
+  }
+  Ctrl c{};
+  c.ws = SIM_START;  // initial window (manager.rs:506-509)
+  c.we = SIM_START + 1;
+  c.active = 1;
+  c.round_min = INVALID;
+  c.min_used = INVALID;
+  c.keep_base = NB * BC;
+  c.keep_min = INVALID;
+  c.last_min_next = INVALID;
+  c.remote_min = INVALID;
+  S.ctrl = dalloc<Ctrl>(ctx, 1);
+  if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+  SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
+  if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
+  *ctx->h_ctrl = c;
+  SGN_HIP(ctx, hipDeviceSynchronize());
+  ctx->S = S;
+  ctx->sim_ready = true;
+  ctx->rounds_enqueued = 0;
+  for (int i = 0; i < 8; i++) ctx->kt[i] = {kKernelNames[i], 0, 0.0};
+  return 0;
+}
+
+int sgn_window(sgn_ctx* ctx, uint64_t* start, uint64_t* end, int32_t* active) {
+  if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  int rc = sync_ctrl(ctx);
+  if (start) *start = ctx->h_ctrl->ws;
+  if (end) *end = ctx->h_ctrl->we;
+  if (active) *active = (int32_t)ctx->h_ctrl->active;
+  return rc;
+}
+
+int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
+  if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  if (!ctx->h_ctrl->active) return set_error(ctx, SGN_ESTATE, "simulation already finished");
+  if ((rc = launch_round(ctx))) return rc;
+  rc = sync_ctrl(ctx);
+  if (min_next) *min_next = ctx->h_ctrl->last_min_next;
+  return rc;
+}
+
+int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
+  if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  const uint64_t r_start = ctx->h_ctrl->rounds;
+  uint64_t enq = 0;
+  const uint64_t batch = ctx->nranks > 1 ? 1 : 64;
+  while (ctx->h_ctrl->active && enq < max_rounds) {
+    const uint64_t n = std::min<uint64_t>(batch, max_rounds - enq);
+    for (uint64_t i = 0; i < n; i++)
+      if ((rc = launch_round(ctx))) return rc;
+    enq += n;
+    if ((rc = sync_ctrl(ctx))) return rc;
+  }
+  if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
+  return 0;
+}
+
+int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  int rc = sync_ctrl(ctx);
+  const uint32_t nH = ctx->S.nH;
+  std::vector<uint64_t> cnt((size_t)NCNT * nH);
+  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.cnt, cnt.size() * 8, hipMemcpyDeviceToHost));
+  sgn_stats s{};
+  auto sum = [&](int k) {
+    uint64_t t = 0;
+    for (uint32_t h = 0; h < nH; h++) t += cnt[(size_t)k * nH + h];
+    return t;
+  };
+  s.rounds = ctx->h_ctrl->rounds;
+  s.packets_sent = sum(CNT_SENT);
+  s.packets_loss_dropped = sum(CNT_LOSS);
+  s.packets_sent += 0;
+  s.packets_unknown_dst = sum(CNT_UNKNOWN);
+  s.packet_events_popped = sum(CNT_POPPED);
+  s.codel_dropped = sum(CNT_CODEL);
+  s.delivered = sum(CNT_DELIV);
+  s.local_delivered = sum(CNT_LOCAL_DELIV);
+  s.app_blocked = sum(CNT_BLOCKED);
+  s.local_events = sum(CNT_LOCAL_EV);
+  s.bytes_delivered = sum(CNT_BYTES);
+  s.min_used_latency_ns = ctx->h_ctrl->min_used;
+  uint64_t mc = 0;
+  for (uint32_t h = 0; h < nH; h++) mc = std::max(mc, cnt[(size_t)CNT_MAX_CODEL * nH + h]);
+  s.max_codel_len = mc;
+  s.max_pending_events = ctx->h_ctrl->max_bucket;
+  *out = s;
+  return rc;
+}
+
+int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  if (lo < ctx->lo || hi > ctx->hi || lo > hi) return set_error(ctx, SGN_EINVAL, "range outside the owned shard");
+  int rc = sync_ctrl(ctx);
+  const uint32_t n = hi - lo, off = lo - ctx->lo, nH = ctx->S.nH;
+  if (n == 0) return rc;
+  std::vector<uint64_t> tx(n), rx(n), ap(n), a(n), b(n), c(n), d(n), e(n);
+  std::vector<uint64_t> cnt((size_t)NCNT * nH);
+  SGN_HIP(ctx, hipMemcpy(tx.data(), ctx->S.d_tx + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(rx.data(), ctx->S.d_rx + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(ap.data(), ctx->S.d_app + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(a.data(), ctx->S.rng0 + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(b.data(), ctx->S.rng1 + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(c.data(), ctx->S.rng2 + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(d.data(), ctx->S.rng3 + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(e.data(), ctx->S.eid + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.cnt, cnt.size() * 8, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n; i++) {
+    sgn_host_digest& o = out[i];
+    o.tx = tx[i];
+    o.rx = rx[i];
+    o.app = ap[i];
+    o.rng[0] = a[i];
+    o.rng[1] = b[i];
+    o.rng[2] = c[i];
+    o.rng[3] = d[i];
+    o.next_event_id = e[i];
+    const size_t h = off + i;
+    o.n_sent = cnt[(size_t)CNT_SENT * nH + h];
+    o.n_popped = cnt[(size_t)CNT_POPPED * nH + h];
+    o.n_delivered = cnt[(size_t)CNT_DELIV * nH + h];
+    o.n_codel_dropped = cnt[(size_t)CNT_CODEL * nH + h];
+  }
+  return rc;
+}
+
+int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
+  if (!ctx || !t) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  const uint32_t h = host - ctx->lo, nH = ctx->S.nH;
+  uint64_t m = INVALID;
+  for (int s = 0; s < NSLOT; s++) {
+    uint64_t v;
+    SGN_HIP(ctx, hipMemcpy(&v, ctx->S.slot_t + (size_t)s * nH + h, 8, hipMemcpyDeviceToHost));
+    m = std::min(m, v);
+  }
+  // pending packet events for this host anywhere in the calendar
+  const uint64_t total = (uint64_t)(ctx->S.NB + 1) * ctx->S.BC;
+  std::vector<uint32_t> bn(ctx->S.NB);
+  std::vector<uint64_t> bb(ctx->S.NB);
+  SGN_HIP(ctx, hipMemcpy(bn.data(), ctx->S.bucket_n, bn.size() * 4, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(bb.data(), ctx->S.bucket_base, bb.size() * 8, hipMemcpyDeviceToHost));
+  (void)total;
+  for (uint32_t b = 0; b < ctx->S.NB; b++) {
+    const uint32_t n = std::min(bn[b], ctx->S.BC);
+    if (!n) continue;
+    std::vector<EvRec> ev(n);
+    SGN_HIP(ctx, hipMemcpy(ev.data(), ctx->S.pool + bb[b], n * sizeof(EvRec), hipMemcpyDeviceToHost));
+    for (const EvRec& e : ev)
+      if (e.dst == host) m = std::min(m, e.time);
+  }
+  *t = m;
+  return 0;
+}
+
+int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_total) {
+  if (!ctx) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  int rc = sync_ctrl(ctx);
+  const uint64_t n = std::min<uint64_t>(ctx->h_ctrl->trace_n, ctx->S.trace_cap);
+  if (n_total) *n_total = ctx->h_ctrl->trace_n;
+  const uint64_t k = std::min(n, cap);
+  if (k && out) SGN_HIP(ctx, hipMemcpy(out, ctx->S.trace, k * sizeof(sgn_trace_rec), hipMemcpyDeviceToHost));
+  return rc;
+}
+
+int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  if (ctx->sim_ready) {
+    int rc = sync_ctrl(ctx);
+    if (rc) return rc;
+  }
+  std::memset(out, 0, sizeof(*out));
+  out->n_kernels = 8;
+  for (int i = 0; i < 8; i++) {
+    out->launches[i] = ctx->kt[i].launches;
+    out->ms[i] = ctx->kt[i].ms;
+    out->name[i] = kKernelNames[i];
+  }
+  return 0;
+}
+
+// Test hook: device CoDel control-law increments for count in [0, n).
+int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  uint64_t* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, n * 8));
+  hipLaunchKernelGGL(k_codel_law_test, dim3(1024), dim3(256), 0, ctx->stream, n, d);
+  hipError_t e = hipMemcpyAsync(out, d, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "codel law selftest");
+  return 0;
+}
+
+}  // extern "C"
+
+// hooks used by comm.cpp
+namespace sgn {
+void launch_finalize_local(sgn_ctx* ctx) {
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->S, 0);
+}
+void launch_import(sgn_ctx* ctx) {
+  hipLaunchKernelGGL(k_import, dim3(256), dim3(256), 0, ctx->stream, ctx->S);
+}
+void launch_advance(sgn_ctx* ctx, const uint64_t* red) {
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, ctx->stream, ctx->S, red);
+}
+}  // namespace sgn

@@ -1,0 +1,412 @@
+// routes.hip — the routing table (NetworkGraph::compute_shortest_paths,
+// network/graph/mod.rs:181-226, and get_direct_paths, :228-250) on gfx950.
+//
+// Shadow runs one petgraph Dijkstra per used source with the lexicographic cost
+// (latency u64, then loss f32) and the non-associative f32 fold
+//   loss' = 1f - (1f - loss) * (1f - edge_loss)            (graph/mod.rs:316-325).
+// Because the fold is isotone and latencies are strictly positive, Dijkstra's result is
+// the lexicographic minimum over all paths; it is computed here in two exact phases:
+//   1. latency: blocked min-plus Floyd-Warshall over all V graph nodes, 64x64 u64 tiles
+//      staged through LDS (VALU/LDS-bound, no MFMA: min-plus is not multiply-accumulate);
+//   2. loss: per used source, a Bellman-Ford sweep over the *tight* arcs
+//      (d[s][u] + lat(u,v) == d[s][v]) to the fixed point
+//      loss[v] = min over tight u->v of fold(loss[u], p(u,v)), loss[s] = 0, with every f32
+//      operation rounded individually (__fsub_rn/__fmul_rn; Rust never contracts).
+//      A Floyd-Warshall over (lat, loss) pairs would combine sub-path aggregates and is
+//      NOT bit-exact (fold(fold(fold(0,.1),.2),.3) != fold(fold(0,.1),fold(.2,.3))).
+// Then each used node's (n,n) entry is replaced by its single self-loop edge
+// (graph/mod.rs:209-215).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+#include "sgn_internal.h"
+
+namespace sgn {
+
+constexpr int FW_T = 64;
+constexpr uint64_t FW_INF = 1ULL << 62;  // sums of two stay below 2^63
+
+__global__ void fw_init(uint64_t* D, uint32_t Vp) {
+  const uint64_t n = (uint64_t)Vp * Vp;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = i / Vp, c = i % Vp;
+    D[i] = r == c ? 0 : FW_INF;
+  }
+}
+
+__global__ void fw_edges(uint64_t* D, uint32_t Vp, const uint32_t* eu, const uint32_t* ev,
+                         const uint64_t* el, uint32_t E, int directed) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < E; k += gridDim.x * blockDim.x) {
+    const uint32_t u = eu[k], v = ev[k];
+    if (u == v) continue;  // the zero-length path always beats a self-loop
+    atomicMin((unsigned long long*)&D[(uint64_t)u * Vp + v], (unsigned long long)el[k]);
+    if (!directed)
+      atomicMin((unsigned long long*)&D[(uint64_t)v * Vp + u], (unsigned long long)el[k]);
+  }
+}
+
+// thread (ty, tx) of 256 owns rows ty + 16a and columns tx + 16b, a, b in 0..3
+#define FW_LOAD_TILE(dst, bi, bj)                                                  \
+  for (int a = 0; a < 4; a++)                                                      \
+    for (int b = 0; b < 4; b++)                                                    \
+      dst[ty + 16 * a][tx + 16 * b] =                                              \
+          D[(uint64_t)((bi) * FW_T + ty + 16 * a) * Vp + (bj) * FW_T + tx + 16 * b];
+
+__global__ __launch_bounds__(256) void fw_phase1(uint64_t* D, uint32_t Vp, int kb) {
+  __shared__ uint64_t P[FW_T][FW_T + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  FW_LOAD_TILE(P, kb, kb);
+  __syncthreads();
+  for (int k = 0; k < FW_T; k++) {
+    for (int a = 0; a < 4; a++) {
+      const uint64_t pik = P[ty + 16 * a][k];
+      for (int b = 0; b < 4; b++) {
+        const uint64_t s = pik + P[k][tx + 16 * b];
+        uint64_t& c = P[ty + 16 * a][tx + 16 * b];
+        c = s < c ? s : c;
+      }
+    }
+    __syncthreads();
+  }
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 4; b++)
+      D[(uint64_t)(kb * FW_T + ty + 16 * a) * Vp + kb * FW_T + tx + 16 * b] =
+          P[ty + 16 * a][tx + 16 * b];
+}
+
+// row panel (kb, j) and column panel (i, kb) against the finished pivot tile
+__global__ __launch_bounds__(256) void fw_phase2(uint64_t* D, uint32_t Vp, int kb, int nb) {
+  __shared__ uint64_t P[FW_T][FW_T + 1];
+  __shared__ uint64_t Q[FW_T][FW_T + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  int idx = blockIdx.x;
+  const bool row = idx < nb - 1;
+  if (!row) idx -= nb - 1;
+  const int other = idx < kb ? idx : idx + 1;
+  const int bi = row ? kb : other, bj = row ? other : kb;
+  FW_LOAD_TILE(P, kb, kb);
+  FW_LOAD_TILE(Q, bi, bj);
+  __syncthreads();
+  for (int k = 0; k < FW_T; k++) {
+    for (int a = 0; a < 4; a++) {
+      const uint64_t left = row ? P[ty + 16 * a][k] : Q[ty + 16 * a][k];
+      for (int b = 0; b < 4; b++) {
+        const uint64_t up = row ? Q[k][tx + 16 * b] : P[k][tx + 16 * b];
+        const uint64_t s = left + up;
+        uint64_t& c = Q[ty + 16 * a][tx + 16 * b];
+        c = s < c ? s : c;
+      }
+    }
+    __syncthreads();
+  }
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 4; b++)
+      D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b] =
+          Q[ty + 16 * a][tx + 16 * b];
+}
+
+// all remaining tiles: C = min(C, A (bi,kb) (+) B (kb,bj)), k order irrelevant
+__global__ __launch_bounds__(256) void fw_phase3(uint64_t* D, uint32_t Vp, int kb, int nb) {
+  __shared__ uint64_t A[FW_T][FW_T + 1];
+  __shared__ uint64_t B[FW_T][FW_T];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m = nb - 1;
+  const int lin = blockIdx.x;
+  const int i0 = lin / m, j0 = lin % m;
+  const int bi = i0 < kb ? i0 : i0 + 1;
+  const int bj = j0 < kb ? j0 : j0 + 1;
+  FW_LOAD_TILE(A, bi, kb);
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 4; b++)
+      B[ty + 16 * a][tx + 16 * b] =
+          D[(uint64_t)(kb * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b];
+  uint64_t c[4][4];
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 4; b++)
+      c[a][b] = D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b];
+  __syncthreads();
+#pragma unroll 4
+  for (int k = 0; k < FW_T; k++) {
+    uint64_t bk[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) bk[b] = B[k][tx + 16 * b];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+      const uint64_t aik = A[ty + 16 * a][k];
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint64_t s = aik + bk[b];
+        c[a][b] = s < c[a][b] ? s : c[a][b];
+      }
+    }
+  }
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 4; b++)
+      D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b] = c[a][b];
+}
+
+// Tight-arc loss fold, one workgroup per used source. LDS: D row (u64) + loss row (f32).
+__global__ __launch_bounds__(256) void loss_pass(const uint64_t* D, uint32_t Vp,
+                                                 const uint32_t* usrc, const uint32_t* au,
+                                                 const uint32_t* av, const uint64_t* al,
+                                                 const float* ap, uint32_t E2, float* Lout,
+                                                 uint32_t* iters) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* Dr = (uint64_t*)smem;
+  float* L = (float*)(Dr + Vp);
+  int& changed = *(int*)(L + Vp);  // in the dynamic region: no static LDS ahead of it
+  const uint32_t s = usrc[blockIdx.x];
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) {
+    Dr[v] = D[(uint64_t)s * Vp + v];
+    L[v] = 2.0f;  // "no path yet": larger than any loss in [0, 1]
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) L[s] = 0.0f;  // the source's score is PathProperties::default()
+  uint32_t it = 0;
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < E2; e += blockDim.x) {
+      const uint32_t u = au[e];
+      const uint64_t du = Dr[u];
+      if (du >= FW_INF) continue;
+      const uint32_t v = av[e];
+      if (du + al[e] != Dr[v]) continue;  // not on a shortest-latency path
+      const float lu = L[u];
+      if (lu > 1.0f) continue;
+      const float cand = __fsub_rn(1.0f, __fmul_rn(__fsub_rn(1.0f, lu), __fsub_rn(1.0f, ap[e])));
+      const uint32_t cb = __float_as_uint(cand);
+      if (cb < __float_as_uint(L[v])) {
+        const uint32_t old = atomicMin((unsigned int*)&L[v], cb);
+        if (cb < old) changed = 1;
+      }
+    }
+    __syncthreads();
+    it++;
+    if (!changed) break;
+  }
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) Lout[(uint64_t)blockIdx.x * Vp + v] = L[v];
+  if (threadIdx.x == 0) iters[blockIdx.x] = it;
+}
+
+__global__ void extract(const uint64_t* D, uint32_t Vp, const float* Lrows, const uint32_t* uidx,
+                        uint32_t U, uint64_t* lat, float* loss) {
+  const uint64_t n = (uint64_t)U * U;
+  for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = (uint32_t)(x / U), j = (uint32_t)(x % U);
+    lat[x] = D[(uint64_t)uidx[i] * Vp + uidx[j]];
+    loss[x] = Lrows[(uint64_t)i * Vp + uidx[j]];
+  }
+}
+
+}  // namespace sgn
+
+using namespace sgn;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+};
+
+template <typename T>
+int upload(sgn_ctx* ctx, DevBuf& b, const T* src, size_t n) {
+  SGN_HIP(ctx, hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(T)));
+  if (n) SGN_HIP(ctx, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t* used,
+                                uint32_t U, int32_t use_shortest_path) {
+  if (!ctx || !g || (!used && U)) return SGN_EINVAL;
+  if (U == 0) return set_error(ctx, SGN_EINVAL, "no used nodes");
+  if (g->n_nodes == 0) return set_error(ctx, SGN_EINVAL, "graph has no nodes");
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  const uint32_t V = g->n_nodes, E = g->n_edges;
+  std::unordered_map<uint32_t, uint32_t> idx;  // GML id -> NodeIndex (last wins, mod.rs:159)
+  idx.reserve(V * 2);
+  for (uint32_t i = 0; i < V; i++) idx[g->node_id[i]] = i;
+  std::vector<uint32_t> uidx(U), es(E), ed(E);
+  for (uint32_t i = 0; i < U; i++) {
+    auto it = idx.find(used[i]);
+    if (it == idx.end())
+      return set_error(ctx, SGN_EINVAL, "used node " + std::to_string(used[i]) + " is not in the graph");
+    uidx[i] = it->second;
+  }
+  for (uint32_t k = 0; k < E; k++) {
+    auto a = idx.find(g->edge_src[k]);
+    auto b = idx.find(g->edge_dst[k]);
+    if (a == idx.end()) return set_error(ctx, SGN_EINVAL, "Edge source " + std::to_string(g->edge_src[k]) + " doesn't exist");
+    if (b == idx.end()) return set_error(ctx, SGN_EINVAL, "Edge target " + std::to_string(g->edge_dst[k]) + " doesn't exist");
+    if (g->edge_latency_ns[k] == 0) return set_error(ctx, SGN_EINVAL, "Edge 'latency' must not be 0");
+    if (g->edge_latency_ns[k] >= (1ULL << 60)) return set_error(ctx, SGN_ERANGE, "edge latency too large");
+    const float p = g->edge_loss[k];
+    if (!(p >= 0.0f && p <= 1.0f)) return set_error(ctx, SGN_EINVAL, "Edge 'packet_loss' is not in the range [0,1]");
+    es[k] = a->second;
+    ed[k] = b->second;
+  }
+  // exactly-one-edge lookup (get_edge_weight, graph/mod.rs:254-287; undirected counts both
+  // orientations, a self-loop once)
+  auto key = [](uint32_t a, uint32_t b) { return ((uint64_t)a << 32) | b; };
+  std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> pairs;  // (count, first edge)
+  const bool need_pairs = !use_shortest_path;
+  std::vector<uint32_t> self_count(V, 0), self_edge(V, 0);
+  for (uint32_t k = 0; k < E; k++) {
+    if (es[k] == ed[k]) {
+      if (self_count[es[k]]++ == 0) self_edge[es[k]] = k;
+    }
+    if (need_pairs) {
+      auto add = [&](uint64_t kk) {
+        auto& e = pairs[kk];
+        if (e.first++ == 0) e.second = k;
+      };
+      add(key(es[k], ed[k]));
+      if (!g->directed && es[k] != ed[k]) add(key(ed[k], es[k]));
+    }
+  }
+  auto edge_msg = [&](uint32_t c, uint32_t a, uint32_t b) {
+    return std::string(c == 0 ? "No edge connecting node " : "More than one edge connecting node ") +
+           std::to_string(g->node_id[a]) + " to " + std::to_string(g->node_id[b]);
+  };
+  std::vector<uint64_t> lat((size_t)U * U);
+  std::vector<float> loss((size_t)U * U);
+  hipEvent_t e0, e1, e2, e3;
+  SGN_HIP(ctx, hipEventCreate(&e0));
+  SGN_HIP(ctx, hipEventCreate(&e1));
+  SGN_HIP(ctx, hipEventCreate(&e2));
+  SGN_HIP(ctx, hipEventCreate(&e3));
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int i = 0; i < 4; i++) hipEventDestroy(e[i]);
+    }
+  };
+  hipEvent_t evs[4] = {e0, e1, e2, e3};
+  EvGuard guard{evs};
+  sgn_routes_timing tm{};
+  tm.tile = FW_T;
+  if (!use_shortest_path) {
+    for (uint32_t i = 0; i < U; i++)
+      for (uint32_t j = 0; j < U; j++) {
+        auto it = pairs.find(key(uidx[i], uidx[j]));
+        const uint32_t c = it == pairs.end() ? 0 : it->second.first;
+        if (c != 1) return set_error(ctx, SGN_EINVAL, edge_msg(c, uidx[i], uidx[j]));
+        const uint32_t k = it->second.second;
+        lat[(size_t)i * U + j] = g->edge_latency_ns[k];
+        loss[(size_t)i * U + j] = g->edge_loss[k];
+      }
+  } else {
+    for (uint32_t i = 0; i < U; i++)
+      if (self_count[uidx[i]] != 1)
+        return set_error(ctx, SGN_EINVAL, edge_msg(self_count[uidx[i]], uidx[i], uidx[i]));
+    const uint32_t nb = (V + FW_T - 1) / FW_T;
+    const uint32_t Vp = nb * FW_T;
+    const size_t lds = (size_t)Vp * 12 + 16;
+    if (lds > 160 * 1024)
+      return set_error(ctx, SGN_ERANGE, "graph too large for the LDS loss pass (V > 13632)");
+    // directed arcs (undirected edges both ways), self-loops excluded
+    std::vector<uint32_t> au, av;
+    std::vector<uint64_t> al;
+    std::vector<float> ap;
+    au.reserve(2 * (size_t)E);
+    for (uint32_t k = 0; k < E; k++) {
+      if (es[k] == ed[k]) continue;
+      au.push_back(es[k]); av.push_back(ed[k]); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
+      if (!g->directed) {
+        au.push_back(ed[k]); av.push_back(es[k]); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
+      }
+    }
+    const uint32_t E2 = (uint32_t)au.size();
+    DevBuf dD, deu, dev, del, dau, dav, dal, dap, dus, dL, dit, dlat, dloss;
+    int rc;
+    if ((rc = upload(ctx, deu, es.data(), E)) || (rc = upload(ctx, dev, ed.data(), E)) ||
+        (rc = upload(ctx, del, g->edge_latency_ns, E)) || (rc = upload(ctx, dau, au.data(), E2)) ||
+        (rc = upload(ctx, dav, av.data(), E2)) || (rc = upload(ctx, dal, al.data(), E2)) ||
+        (rc = upload(ctx, dap, ap.data(), E2)) || (rc = upload(ctx, dus, uidx.data(), U)))
+      return rc;
+    SGN_HIP(ctx, hipMalloc(&dD.p, (size_t)Vp * Vp * 8));
+    SGN_HIP(ctx, hipMalloc(&dL.p, (size_t)U * Vp * 4));
+    SGN_HIP(ctx, hipMalloc(&dit.p, (size_t)U * 4));
+    SGN_HIP(ctx, hipMalloc(&dlat.p, (size_t)U * U * 8));
+    SGN_HIP(ctx, hipMalloc(&dloss.p, (size_t)U * U * 4));
+    hipStream_t st = ctx->stream;
+    uint64_t* D = (uint64_t*)dD.p;
+    SGN_HIP(ctx, hipEventRecord(e0, st));
+    hipLaunchKernelGGL(fw_init, dim3(2048), dim3(256), 0, st, D, Vp);
+    hipLaunchKernelGGL(fw_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0, st,
+                       D, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
+                       (int)g->directed);
+    for (uint32_t kb = 0; kb < nb; kb++) {
+      hipLaunchKernelGGL(fw_phase1, dim3(1), dim3(256), 0, st, D, Vp, (int)kb);
+      if (nb > 1) {
+        hipLaunchKernelGGL(fw_phase2, dim3(2 * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
+        hipLaunchKernelGGL(fw_phase3, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
+      }
+    }
+    SGN_HIP(ctx, hipGetLastError());
+    SGN_HIP(ctx, hipEventRecord(e1, st));
+    hipLaunchKernelGGL(loss_pass, dim3(U), dim3(256), lds, st, D, Vp, (const uint32_t*)dus.p,
+                       (const uint32_t*)dau.p, (const uint32_t*)dav.p, (const uint64_t*)dal.p,
+                       (const float*)dap.p, E2, (float*)dL.p, (uint32_t*)dit.p);
+    SGN_HIP(ctx, hipGetLastError());
+    SGN_HIP(ctx, hipEventRecord(e2, st));
+    hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
+                       (const uint32_t*)dus.p, U, (uint64_t*)dlat.p, (float*)dloss.p);
+    SGN_HIP(ctx, hipGetLastError());
+    SGN_HIP(ctx, hipMemcpyAsync(lat.data(), dlat.p, (size_t)U * U * 8, hipMemcpyDeviceToHost, st));
+    SGN_HIP(ctx, hipMemcpyAsync(loss.data(), dloss.p, (size_t)U * U * 4, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> its(U);
+    SGN_HIP(ctx, hipMemcpyAsync(its.data(), dit.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
+    SGN_HIP(ctx, hipEventRecord(e3, st));
+    SGN_HIP(ctx, hipStreamSynchronize(st));
+    float ms_fw = 0, ms_loss = 0, ms_total = 0;
+    hipEventElapsedTime(&ms_fw, e0, e1);
+    hipEventElapsedTime(&ms_loss, e1, e2);
+    hipEventElapsedTime(&ms_total, e0, e3);
+    tm.latency_ms = ms_fw;
+    tm.loss_ms = ms_loss;
+    tm.total_ms = ms_total;
+    tm.loss_iters = its.empty() ? 0 : *std::max_element(its.begin(), its.end());
+    tm.n_tight_edges = E2;
+    for (uint32_t i = 0; i < U; i++)
+      for (uint32_t j = 0; j < U; j++)
+        if (lat[(size_t)i * U + j] >= FW_INF)
+          return set_error(ctx, SGN_EINVAL, "used nodes " + std::to_string(used[i]) + " -> " +
+                                                std::to_string(used[j]) + " are not connected");
+    // the single self-loop replaces the zero-length path (graph/mod.rs:209-215)
+    for (uint32_t i = 0; i < U; i++) {
+      const uint32_t k = self_edge[uidx[i]];
+      lat[(size_t)i * U + i] = g->edge_latency_ns[k];
+      loss[(size_t)i * U + i] = g->edge_loss[k];
+    }
+  }
+  // device copy for the engine
+  if (ctx->d_lat) hipFree(ctx->d_lat);
+  if (ctx->d_loss) hipFree(ctx->d_loss);
+  ctx->d_lat = nullptr;
+  ctx->d_loss = nullptr;
+  SGN_HIP(ctx, hipMalloc(&ctx->d_lat, (size_t)U * U * 8));
+  SGN_HIP(ctx, hipMalloc(&ctx->d_loss, (size_t)U * U * 4));
+  SGN_HIP(ctx, hipMemcpy(ctx->d_lat, lat.data(), (size_t)U * U * 8, hipMemcpyHostToDevice));
+  SGN_HIP(ctx, hipMemcpy(ctx->d_loss, loss.data(), (size_t)U * U * 4, hipMemcpyHostToDevice));
+  ctx->U = U;
+  ctx->used_ids.assign(used, used + U);
+  ctx->h_lat.swap(lat);
+  ctx->h_loss.swap(loss);
+  ctx->rt_timing = tm;
+  ctx->routes_ready = true;
+  ctx->hosts_ready = false;  // hosts map onto used nodes: re-register
+  return 0;
+}

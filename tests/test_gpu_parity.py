@@ -1,0 +1,234 @@
+"""GPU parity: libsgn (HIP, gfx950) against the oracle on identical inputs.
+
+Bar (BASELINE.json north_star): bit-exact routing tables, per-packet delivery times, drop
+decisions and event order. Small cases compare full per-packet traces; larger cases
+compare per-host order-sensitive digests ("checksum of checksums") and counters.
+"""
+import numpy as np
+import pytest
+
+import sgn
+
+pytestmark = pytest.mark.gpu
+
+SIM_START = sgn.SIMULATION_START
+
+
+@pytest.fixture(scope="module")
+def ctxf():
+    def make(**kw):
+        return sgn.Context(**kw)
+    return make
+
+
+def ref_graph(directed):
+    # network/graph/mod.rs:559-644 test_shortest_path
+    node = np.array([0, 1, 2])
+    src = [0, 1, 2, 0, 1, 0, 2]
+    dst = [0, 1, 2, 1, 0, 2, 1]
+    lat = [3333, 5555, 7777, 3, 5, 7, 11]
+    return sgn.GraphArrays(node, src, dst, lat, np.zeros(7, np.float32), directed)
+
+
+@pytest.mark.parametrize("directed", [True, False])
+def test_apsp_reference_shortest_path(ctxf, directed):
+    c = ctxf()
+    c.routes_build(ref_graph(directed), [0, 1, 2])
+    lat, _ = c.routes_copy()
+    if directed:
+        exp = [[3333, 3, 7], [5, 5555, 12], [16, 11, 7777]]
+    else:
+        exp = [[3333, 3, 7], [3, 5555, 10], [7, 10, 7777]]
+    assert lat.tolist() == exp
+
+
+@pytest.mark.parametrize("V,directed,seed", [(16, False, 1), (100, False, 2), (100, True, 3),
+                                             (333, False, 4), (1000, False, 42)])
+def test_apsp_random_vs_oracle(ctxf, oracle, V, directed, seed):
+    g = sgn.random_graph(V, seed=seed, loss_frac=0.5)
+    if directed:
+        # add reverse arcs so the directed graph stays strongly connected
+        rs = np.concatenate([g.src, g.dst[: len(g.src) - V]])
+        rd = np.concatenate([g.dst, g.src[: len(g.src) - V]])
+        rl = np.concatenate([g.lat, g.lat[: len(g.src) - V][::-1]])
+        rp = np.concatenate([g.loss, g.loss[: len(g.src) - V]])
+        g = sgn.GraphArrays(g.node_id, rs, rd, rl, rp, True)
+    rng = np.random.default_rng(seed)
+    used = np.sort(rng.choice(V, size=max(2, V * 3 // 4), replace=False))
+    ol, op = oracle.routes(g, used)
+    c = ctxf()
+    c.routes_build(g, used)
+    gl, gp = c.routes_copy()
+    assert np.array_equal(ol, gl)
+    assert np.array_equal(op.view(np.uint32), gp.view(np.uint32))
+
+
+def test_apsp_complete_graph_vs_oracle(ctxf, oracle):
+    g = sgn.tor_graph(200, seed=9)
+    used = np.arange(200)
+    ol, op = oracle.routes(g, used)
+    c = ctxf()
+    c.routes_build(g, used)
+    gl, gp = c.routes_copy()
+    assert np.array_equal(ol, gl)
+    assert np.array_equal(op.view(np.uint32), gp.view(np.uint32))
+    # direct-path mode (use_shortest_path: false) on the same complete graph
+    ol2, op2 = oracle.routes(g, used, shortest=False)
+    c.routes_build(g, used, shortest=False)
+    gl2, gp2 = c.routes_copy()
+    assert np.array_equal(ol2, gl2)
+    assert np.array_equal(op2.view(np.uint32), gp2.view(np.uint32))
+
+
+def test_apsp_errors(ctxf):
+    c = ctxf()
+    g = sgn.GraphArrays([0, 1], [0, 0, 1], [1, 0, 1], [5, 3, 3], [0, 0, 0], False)
+    c.routes_build(g, [0, 1])  # fine
+    bad = sgn.GraphArrays([0, 1], [0, 1], [1, 1], [5, 3], [0, 0], False)  # node 0: no self-loop
+    with pytest.raises(sgn.SgnError, match="No edge connecting node 0 to 0"):
+        c.routes_build(bad, [0, 1])
+    disc = sgn.GraphArrays([0, 1, 2], [0, 1, 2], [0, 1, 2], [1, 1, 1], [0, 0, 0], False)
+    with pytest.raises(sgn.SgnError, match="not connected"):
+        c.routes_build(disc, [0, 2])
+    dup = sgn.GraphArrays([0, 1], [0, 0, 1, 0], [0, 0, 1, 1], [1, 2, 1, 1], [0, 0, 0, 0], False)
+    with pytest.raises(sgn.SgnError, match="More than one edge"):
+        c.routes_build(dup, [0, 1])
+
+
+def test_codel_control_law_on_device(ctxf, oracle):
+    c = ctxf()
+    n = 1 << 20
+    out = np.zeros(n, dtype=np.uint64)
+    c.check(c.L.sgn_selftest_codel_law(c.h, n, sgn.ptr(out, sgn.C.c_uint64)))
+    x = 1e8 / np.sqrt(np.maximum(np.arange(n, dtype=np.float64), 1.0))
+    fl = np.floor(x)
+    exp = np.where(x - fl >= 0.5, fl + 1, fl).astype(np.uint64)  # f64::round, half away
+    assert np.array_equal(out, exp)
+    # spot-check against the oracle's restatement
+    for i in (0, 1, 2, 3, 7, 19, 1000, n - 1):
+        assert oracle.load().ora_codel_control_law(SIM_START, i) - SIM_START == int(out[i])
+
+
+def scenario(n=200, V=50, *, kind=sgn.TRAFFIC_PERIODIC, stop_ns=500_000_000, bw=10_000_000,
+             seed=1, graph_seed=1, dynamic=False, runahead_ns=1_000_000, bootstrap_ns=0,
+             unknown=10, period_ns=1_000_000, fifo=64, codel=4096, tgen_think=50_000_000,
+             tor=False):
+    g = sgn.tor_graph(V, seed=graph_seed) if tor else sgn.random_graph(V, seed=graph_seed)
+    used = np.arange(V)
+    names = sgn.host_names(n)
+    seeds = sgn.derive_seeds(seed, names)
+    bwv = bw if np.ndim(bw) else np.full(n, bw, dtype=np.uint64)
+    hosts = sgn.HostArrays(sgn.assign_ips(n), (np.arange(n) * 7) % V, bwv, bwv, seeds)
+    cfg = sgn.make_config(stop_ns, runahead_ns=runahead_ns, dynamic=dynamic,
+                          bootstrap_end_ns=bootstrap_ns, out_fifo_cap=fifo, codel_cap=codel,
+                          event_capacity=1 << 20)
+    if kind == sgn.TRAFFIC_PERIODIC:
+        tr = sgn.make_traffic(period_ns=period_ns, start_jitter_ns=3_000_000,
+                              unknown_dst_permille=unknown, payload_len=1024)
+    else:
+        servers = np.arange(0, n, 10)
+        tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, period_ns=tgen_think,
+                              period_jitter_ns=tgen_think, start_jitter_ns=20_000_000,
+                              servers=servers, file_bytes=(50 * 1024, 300 * 1024, 1024 * 1024))
+    return g, used, hosts, cfg, tr
+
+
+def run_both(ctxf, oracle, args, trace=True, round_by_round=0):
+    g, used, hosts, cfg, tr = args
+    lat, loss = oracle.routes(g, used)
+    o = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=trace)
+    c = ctxf()
+    c.routes_build(g, used)
+    c.hosts_set(hosts)
+    if trace:
+        c.trace_enable(1 << 22)
+    c.sim_init(cfg, tr)
+    for _ in range(round_by_round):
+        wo, wg = o.window(), c.window()
+        assert wo == wg
+        if not wo[2]:
+            break
+        assert o.round() == c.round()
+    o.run()
+    c.run()
+    return o, c
+
+
+def sort_trace(t):
+    return t[np.lexsort((t["seq"], t["host"]))]
+
+
+def assert_same_run(o, c, n, trace=True):
+    so, sg = o.stats(), c.stats()
+    for k in so:
+        if k in ("max_pending_events",):
+            continue
+        assert so[k] == sg[k], (k, so[k], sg[k])
+    assert o.window() == c.window()
+    do, dg = o.digests(0, n), c.digests(0, n)
+    for f in ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered",
+              "n_codel_dropped"):
+        assert np.array_equal(do[f], dg[f]), f
+    if trace:
+        to, tg = sort_trace(o.trace()), sort_trace(c.trace())
+        assert len(to) == len(tg)
+        for f in ("kind", "host", "peer", "flags", "a", "b", "c", "seq"):
+            bad = np.nonzero(to[f] != tg[f])[0]
+            assert len(bad) == 0, (f, to[bad[:3]], tg[bad[:3]])
+
+
+def test_engine_periodic_trace(ctxf, oracle):
+    args = scenario()
+    o, c = run_both(ctxf, oracle, args, round_by_round=300)
+    assert c.stats()["packets_sent"] > 10000
+    assert c.stats()["packets_unknown_dst"] > 0 and c.stats()["packets_loss_dropped"] > 0
+    assert_same_run(o, c, args[2].n)
+
+
+def test_engine_tgen_trace_codel(ctxf, oracle):
+    # slow down-links make CoDel queues stand and drop
+    bw = np.where(np.arange(300) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+    args = scenario(n=300, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=2_000_000_000, bw=bw, tor=True,
+                    tgen_think=200_000_000)
+    o, c = run_both(ctxf, oracle, args)
+    st = c.stats()
+    assert st["codel_dropped"] > 0, st
+    assert_same_run(o, c, args[2].n)
+
+
+def test_engine_dynamic_runahead_bootstrap(ctxf, oracle):
+    args = scenario(n=150, dynamic=True, runahead_ns=0, bootstrap_ns=100_000_000,
+                    stop_ns=400_000_000)
+    o, c = run_both(ctxf, oracle, args, round_by_round=100)
+    assert_same_run(o, c, args[2].n)
+
+
+def test_engine_tiny_fifo_blocks(ctxf, oracle):
+    args = scenario(n=100, bw=1_000_000, fifo=2, period_ns=500_000, stop_ns=300_000_000)
+    o, c = run_both(ctxf, oracle, args)
+    assert c.stats()["app_blocked"] > 0
+    assert_same_run(o, c, args[2].n)
+
+
+def test_engine_large_digests(ctxf, oracle):
+    n = 10000
+    args = scenario(n=n, V=1000, graph_seed=42, stop_ns=300_000_000, period_ns=10_000_000,
+                    bw=100_000_000)
+    o, c = run_both(ctxf, oracle, args, trace=False)
+    assert_same_run(o, c, n, trace=False)
+
+
+def test_worker_exports(ctxf, oracle):
+    g, used, hosts, cfg, tr = scenario(n=20, V=10)
+    c = ctxf()
+    c.routes_build(g, used)
+    c.hosts_set(hosts)
+    lat, _ = oracle.routes(g, used)
+    be = lambda ip: int.from_bytes(int(ip).to_bytes(4, "big"), "little")
+    for a in range(0, 20, 3):
+        for b in range(0, 20, 5):
+            got = c.L.sgn_worker_get_latency(c.h, be(hosts.ip[a]), be(hosts.ip[b]))
+            assert got == lat[hosts.node_id[a], hosts.node_id[b]]
+            assert c.L.sgn_worker_is_routable(c.h, be(hosts.ip[a]), be(hosts.ip[b])) == 1
+    assert c.L.sgn_worker_get_latency(c.h, be(0x0A000001), be(hosts.ip[0])) == sgn.EMUTIME_INVALID
+    assert c.L.sgn_worker_get_bandwidth_up_bytes(c.h, be(hosts.ip[3])) == hosts.bw_up[3] // 8
