@@ -1,0 +1,208 @@
+"""Headline benchmark: simulated packet events/s (whole node) at 100k hosts + APSP build time.
+
+Workload (BASELINE.json configs[2], "config C", the one the metric is quoted on: it fits a
+single MI355X): 100k synthetic hosts per GPU on a Tor-like 1000-node complete graph
+(latency 1 ms + 5..150 ms distance term, loss 0..0.5 %), Zipf(1.0) host placement,
+bandwidth classes 10M/100M/1G, 10 % servers; clients fetch 50 KiB / 1 MiB / 5 MiB files as
+1500 B UDP trains paced only by token buckets and CoDel (no TCP congestion control: the
+TCP stack is outside the GPU core). Synthetic data, seeded.
+
+A step = ROUNDS_PER_STEP simulation rounds (Shadow scheduling windows). A packet event =
+one send_packet call past the DNS check (sent or loss-dropped) or one packet event popped
+at its destination. value = all ranks' packet events / max-rank wall time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, hosts sharded, RCCL exchange inside libsgn).
+"""
+import argparse
+import json
+import os
+import pathlib
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "shadow-gen_amd"))
+import sgn  # noqa: E402
+
+METRIC = "simulated packet events/sec (whole node) at 100k hosts; APSP build time"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def build_workload(n_hosts, V, seed=1):
+    g = sgn.tor_graph(V, seed=42)
+    used = np.arange(V, dtype=np.uint32)
+    names = sgn.host_names(n_hosts)
+    seeds = sgn.derive_seeds(seed, names)
+    node = sgn.zipf_nodes(n_hosts, V, seed=5)
+    bw = sgn.bandwidth_classes(n_hosts, seed=3)
+    hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), node, bw, bw, seeds)
+    rng = np.random.default_rng(11)
+    servers = np.sort(rng.choice(n_hosts, size=max(1, n_hosts // 10), replace=False)).astype(np.uint32)
+    # first fetch uniform over one mean think time: the fetch process is stationary from t=0
+    tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, flow_seed=7, start_ns=0, start_jitter_ns=3_000_000_000,
+                          period_ns=2_000_000_000, period_jitter_ns=2_000_000_000,
+                          req_payload=64, servers=servers,
+                          file_bytes=(50 * 1024, 1024 * 1024, 5 * 1024 * 1024))
+    cfg = sgn.make_config(3600 * 1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64,
+                          codel_cap=16384, event_capacity=1 << 25)
+    return g, used, hosts, cfg, tr
+
+
+def events_of(st):
+    return st["packets_sent"] + st["packets_loss_dropped"] + st["packet_events_popped"]
+
+
+def cpu_baseline(g, used, hosts, cfg, tr, budget_s):
+    """The oracle (CPU restatement, single thread) on a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_py
+
+    lat, loss = oracle_py.routes(g, used)
+    t0 = time.perf_counter()
+    sim = oracle_py.Sim(used, lat, loss, hosts, cfg, tr)
+    rounds = 0
+    t1 = time.perf_counter()
+    while time.perf_counter() - t1 < budget_s:
+        sim.run(50)
+        rounds += 50
+    el = time.perf_counter() - t1
+    st = sim.stats()
+    ws, _, _ = sim.window()
+    return {
+        "value": events_of(st) / el,
+        "unit": "packet events/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle round loop over the same {hosts.n}-host workload from t=0 for "
+                  f"{rounds} rounds ({(ws - sgn.SIMULATION_START) / 1e6:.1f} simulated ms, "
+                  f"{events_of(st)} packet events, {el:.1f} s wall; setup {t1 - t0:.1f} s excluded)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--hosts", type=int, default=100_000, help="hosts per GPU")
+    ap.add_argument("--nodes", type=int, default=1000)
+    ap.add_argument("--rounds-per-step", type=int, default=100)
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    n_total = args.hosts * world
+    g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
+
+    ctx = sgn.Context(device=local, shard_rank=rank, shard_count=world,
+                      flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around k_execute
+    ctx.routes_build(g, used)
+    apsp = ctx.routes_timing()
+    ctx.hosts_set(hosts)
+    if world > 1:
+        import torch
+        idb = (sgn.C.c_uint8 * 128)()
+        if rank == 0:
+            ctx.check(ctx.L.sgn_comm_get_unique_id(idb))
+        t = torch.tensor(list(bytes(idb)), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        idb = (sgn.C.c_uint8 * 128)(*t.tolist())
+        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 17))
+    ctx.sim_init(cfg, tr)
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.run(args.rounds_per_step)
+    st0 = ctx.stats()
+    kt0 = ctx.kernel_times()["k_execute"]
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.run(args.rounds_per_step)
+    barrier()
+    el = time.perf_counter() - t0
+    st1 = ctx.stats()
+    kt1 = ctx.kernel_times()["k_execute"]
+    ev = events_of(st1) - events_of(st0)
+    if dist:
+        import torch
+        m = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        el = float(m.item())
+        e = torch.tensor([ev], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        ev = int(e.item())
+    d = {k: st1[k] - st0[k] for k in st1}
+    rounds = d["rounds"]
+    # roofline of the dominant kernel (k_execute): algorithmic bytes per launch, DESIGN.md
+    launches = kt1[0] - kt0[0]
+    exec_ms = kt1[1] - kt0[1]
+    pops = d["packet_events_popped"]
+    sends = d["packets_sent"] + d["packets_loss_dropped"] + d["packets_unknown_dst"]
+    local_ev = d["local_events"]
+    host_exec = d["host_executions"]
+    idle = rounds * (hosts.n // world) - host_exec
+    alg_bytes = 96 * pops + 64 * sends + 736 * host_exec + 36 * idle
+    roof = None
+    if launches and exec_ms > 0:
+        avg_s = exec_ms / launches / 1e3
+        achieved = alg_bytes / launches / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": "k_execute", "avg_launch_us": round(avg_s * 1e6, 2),
+                "alg_bytes_per_launch": int(alg_bytes / launches)}
+    out = {
+        "metric": METRIC,
+        "value": ev / el,
+        "unit": "packet events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": "C: Tor-like 1000-node complete graph, tgen-style UDP trains",
+            "hosts_per_gpu": args.hosts, "hosts_total": n_total, "graph_nodes": args.nodes,
+            "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
+            "parallelism": f"host-shard x{world}",
+        },
+        "apsp_build_ms": round(apsp["total_ms"], 3),
+        "apsp": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in apsp.items()},
+        "sim_ms_per_step": None,
+        "rounds_timed": rounds,
+        "packet_events_timed": ev,
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    ws, _, _ = ctx.window()
+    out["sim_time_reached_ms"] = (ws - sgn.SIMULATION_START) / 1e6
+    out["sim_ms_per_step"] = out["sim_time_reached_ms"] / (args.steps + args.warmup)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(g, used, hosts, cfg, tr, args.cpu_budget_s)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

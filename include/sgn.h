@@ -60,6 +60,7 @@ typedef struct sgn_create_opts {
 } sgn_create_opts;
 
 #define SGN_CREATE_TIME_KERNELS 1u /* record HIP events around every launch (sgn_kernel_times) */
+#define SGN_CREATE_TIME_EXECUTE 2u /* ... around the per-host execute kernel only */
 
 /* Creates a context bound to one GPU. Replaces WorkerShared construction
  * (core/manager.rs:447-470) for the data-parallel state. */
@@ -214,6 +215,7 @@ typedef struct sgn_stats {
   uint64_t min_used_latency_ns;/* Runahead::min_used_latency, SGN_EMUTIME_INVALID if none */
   uint64_t max_codel_len;      /* high-water mark of any CoDel ring (capacity planning) */
   uint64_t max_pending_events; /* high-water mark of in-flight packet events */
+  uint64_t host_executions;    /* sum over rounds of hosts that had an event due */
 } sgn_stats;
 int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out);
 

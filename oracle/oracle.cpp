@@ -1173,6 +1173,7 @@ struct ora_sim {
 
   // Host::execute (host.rs:762-830)
   void execute(Host& h, uint64_t until) {
+    if (!h.q.empty() && h.q.top().time < until) st.host_executions++;
     while (!h.q.empty() && h.q.top().time < until) {
       Event ev = h.q.top();
       h.q.pop();

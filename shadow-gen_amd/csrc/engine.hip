@@ -905,6 +905,7 @@ __global__ __launch_bounds__(256) void k_execute(DevSim S) {
   const uint64_t keep_base = C->keep_base;
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t my_min = INVALID;
+  bool executed = false;
   if (h < S.nH) {
     const uint32_t s0 = S.seg_start[h], s1 = S.seg_start[h + 1];
     S.hist[h] = 0;
@@ -919,8 +920,13 @@ __global__ __launch_bounds__(256) void k_execute(DevSim S) {
       ex.run(s0, s1);
       my_min = ex.next_local_time();
       ex.store();
+      executed = true;
     }
   }
+  // hosts that ran this round (roofline accounting: their state made a round trip)
+  const uint64_t ex_mask = __ballot(executed);
+  if ((threadIdx.x & 63) == 0 && ex_mask)
+    atomicAdd((unsigned long long*)&C->exec_hosts, (unsigned long long)__popcll(ex_mask));
   const uint64_t m = block_min_u64(my_min, sh);
   if (threadIdx.x == 0 && m != INVALID)
     atomicMin((unsigned long long*)&C->round_min, (unsigned long long)m);
@@ -1155,7 +1161,9 @@ int sync_ctrl(sgn_ctx* ctx) {
 namespace sgn {
 
 void time_begin(sgn_ctx* ctx, int kernel) {
-  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  const bool all = ctx->flags & SGN_CREATE_TIME_KERNELS;
+  const bool exec = (ctx->flags & SGN_CREATE_TIME_EXECUTE) && kernel == K_EXECUTE;
+  if (!all && !exec) return;
   if (ctx->ev_next >= ctx->ev_pool.size()) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
@@ -1166,14 +1174,14 @@ void time_begin(sgn_ctx* ctx, int kernel) {
 }
 
 void time_end(sgn_ctx* ctx) {
-  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  if (!(ctx->flags & (SGN_CREATE_TIME_KERNELS | SGN_CREATE_TIME_EXECUTE))) return;
   if (ctx->ev_pending.empty() || ctx->ev_pending.back().second != ctx->ev_next) return;
   hipEventRecord(ctx->ev_pool[ctx->ev_next].second, ctx->stream);
   ctx->ev_next++;
 }
 
 void time_collect(sgn_ctx* ctx) {
-  if (!(ctx->flags & SGN_CREATE_TIME_KERNELS)) return;
+  if (!(ctx->flags & (SGN_CREATE_TIME_KERNELS | SGN_CREATE_TIME_EXECUTE))) return;
   for (auto& p : ctx->ev_pending) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ctx->ev_pool[p.second].first, ctx->ev_pool[p.second].second) ==
@@ -1513,6 +1521,7 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   for (uint32_t h = 0; h < nH; h++) mc = std::max(mc, cnt[(size_t)CNT_MAX_CODEL * nH + h]);
   s.max_codel_len = mc;
   s.max_pending_events = ctx->h_ctrl->max_bucket;
+  s.host_executions = ctx->h_ctrl->exec_hosts;
   *out = s;
   return rc;
 }

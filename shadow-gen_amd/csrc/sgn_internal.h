@@ -73,7 +73,8 @@ struct Ctrl {
   uint64_t max_bucket;    // high-water mark of any bucket fill
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
-  uint64_t pad1[3];
+  uint64_t exec_hosts;    // cumulative host executions (hosts with due events per round)
+  uint64_t pad1[2];
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,

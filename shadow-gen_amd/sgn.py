@@ -87,7 +87,7 @@ class Stats(C.Structure):
         "rounds", "packets_sent", "packets_loss_dropped", "packets_unknown_dst",
         "packet_events_popped", "codel_dropped", "delivered", "local_delivered",
         "app_blocked", "local_events", "bytes_delivered", "min_used_latency_ns",
-        "max_codel_len", "max_pending_events")]
+        "max_codel_len", "max_pending_events", "host_executions")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
