@@ -255,9 +255,9 @@ int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_t
 
 /* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS). */
 typedef struct sgn_kernel_times {
-  uint64_t launches[8];
-  double ms[8];
-  const char* name[8];
+  uint64_t launches[16];
+  double ms[16];
+  const char* name[16];
   uint32_t n_kernels;
 } sgn_kernel_times;
 int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out);

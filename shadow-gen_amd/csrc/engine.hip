@@ -682,12 +682,186 @@ struct HostExec {
     }
   }
 
+  // A run of n identical datagrams pushed to the router at the same `now`: n consecutive
+  // Worker::send_packet calls (core/worker.rs:330-403). The DNS lookup, route entry,
+  // reliability and delivery time are the same for all of them, so they are computed
+  // once; the per-packet loss draws and digests stay sequential (same RNG stream, same
+  // order). Sent packets take consecutive source event ids and share one delivery time,
+  // so their events are reserved with one atomic and written as one contiguous run.
+  __device__ void send_batch(uint32_t dst_ip, uint32_t payload, uint32_t tag, uint32_t n) {
+    if (n == 0 || now >= S.end_time) return;
+    const bool boot = now < S.boot_end;
+    uint32_t dst;
+    if (!dns_lookup(dst_ip, &dst)) {
+      for (uint32_t j = 0; j < n; j++) {
+        c_unknown++;
+        dtx = sgn_digest3(dtx, now, 0xFFFFFFFFULL | (2ULL << 32), 0);
+        trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+      }
+      return;
+    }
+    const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
+    const double reliability = (double)__fsub_rn(1.0f, S.rloss[ri]);
+    const uint64_t delay = S.rlat[ri];
+    uint64_t deliver = now + delay;
+    if (deliver < we) deliver = we;
+    const uint64_t eid0 = eid;
+    for (uint32_t j = 0; j < n; j++) {
+      const double chance = rng_f64();
+      if (!boot && chance >= reliability && payload > 0) {
+        c_loss++;
+        dtx = sgn_digest3(dtx, now, (uint64_t)dst | (1ULL << 32), 0);
+        trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+      } else {
+        const uint64_t e = eid++;
+        dtx = sgn_digest3(dtx, now, (uint64_t)dst, deliver);
+        trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+      }
+    }
+    const uint32_t nsent = (uint32_t)(eid - eid0);
+    if (nsent == 0) return;
+    c_sent += nsent;
+    if (S.dynamic && delay < lat_cache) {
+      lat_cache = delay;
+      atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
+    }
+    EvRec* dstp;
+    uint32_t cap;
+    uint32_t pos;
+    const bool owned = dst - S.lo < S.nH;
+    if (owned) {
+      const uint32_t b = bucket_of(S, deliver);
+      uint64_t base;
+      if (b == b1) {
+        pos = atomicAdd(&C->keep_n, nsent);
+        base = b1_keep_base;
+        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)deliver);
+      } else {
+        pos = atomicAdd(&S.bucket_n[b], nsent);
+        base = S.bucket_base[b];
+        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)deliver);
+      }
+      dstp = S.pool + base;
+      cap = S.BC;
+    } else {
+      uint32_t lo = 0, hi = S.n_ranks;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
+      }
+      pos = atomicAdd(&S.xout_n[lo], nsent);
+      dstp = S.xout + (size_t)lo * S.xslot;
+      cap = S.xslot;
+    }
+    if (pos + nsent > cap) {
+      overflow(owned ? OVF_BUCKET : OVF_EXCHANGE);
+      return;
+    }
+    for (uint32_t m = 0; m < nsent; m++) {
+      EvRec r;
+      r.time = deliver;
+      r.eid = eid0 + m;
+      r.src = gid;
+      r.dst = dst;
+      r.payload = payload;
+      r.tag = tag;
+      dstp[pos + m] = r;
+    }
+  }
+
+  // Relay::forward_until_blocked for relay_inet_out (network/relay/mod.rs:201-273), taking
+  // the send queue a run at a time: a run is the leading datagrams of the head train that
+  // share a payload size. All of them see the same `now`, so after the first
+  // comforming_remove (which applies the lazy refill) no further refill happens and the
+  // number that conform is balance / wire_len; the first that does not is cached exactly
+  // like Relay::next_packet.
+  __device__ bool forward_out(uint64_t* dur) {
+    const bool boot = now < S.boot_end;
+    set_relay_state<0>(RELAY_FORWARDING);
+    if (fl & F_RO_NEXT) {
+      fl &= ~F_RO_NEXT;
+      const bool is_local = ro_dst == my_ip;
+      if (!boot && !is_local) {
+        if (!tb_remove<0>((uint64_t)ro_pay + SGN_UDP_HEADER_BYTES, dur)) {
+          fl |= F_RO_NEXT;
+          set_relay_state<0>(RELAY_IDLE);
+          return true;
+        }
+      }
+      Pkt p;
+      p.src = gid;
+      p.dst_ip = ro_dst;
+      p.payload = ro_pay;
+      p.tag = ro_tag;
+      p.eid = 0;
+      if (is_local)
+        deliver_to_app(p, true);
+      else
+        send_batch(ro_dst, ro_pay, ro_tag, 1);
+    }
+    while (fq_len > 0) {
+      FifoEnt* s = fq_slot(0);
+      const FifoEnt e = *s;
+      const uint32_t run = e.count == 1 ? 1u : e.count - 1;
+      const uint32_t payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
+      const uint64_t wire = (uint64_t)payload + SGN_UDP_HEADER_BYTES;
+      const bool is_local = e.dst_ip == my_ip;
+      uint32_t n_ok = run;
+      bool blocked = false;
+      if (!boot && !is_local) {
+        if (!tb_remove<0>(wire, dur)) {
+          n_ok = 0;
+          blocked = true;
+        } else if (run > 1) {
+          const uint64_t more = tbb0 / wire;
+          if (more >= run - 1) {
+            tbb0 -= (uint64_t)(run - 1) * wire;
+          } else {
+            tbb0 -= more * wire;
+            n_ok = 1 + (uint32_t)more;
+            blocked = true;
+            tb_remove<0>(wire, dur);  // fails: same `now`, gives the conforming duration
+          }
+        }
+      }
+      if (is_local) {
+        Pkt p;
+        p.src = gid;
+        p.dst_ip = e.dst_ip;
+        p.payload = payload;
+        p.tag = e.tag;
+        p.eid = 0;
+        for (uint32_t j = 0; j < n_ok; j++) deliver_to_app(p, true);
+      } else {
+        send_batch(e.dst_ip, payload, e.tag, n_ok);
+      }
+      const uint32_t consumed = n_ok + (blocked ? 1u : 0u);
+      if (consumed == e.count) {
+        fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
+        fq_len--;
+      } else {
+        s->count = e.count - consumed;
+      }
+      if (blocked) {
+        fl |= F_RO_NEXT;
+        ro_dst = e.dst_ip;
+        ro_pay = payload;
+        ro_tag = e.tag;
+        set_relay_state<0>(RELAY_IDLE);
+        return true;
+      }
+    }
+    set_relay_state<0>(RELAY_IDLE);
+    return false;
+  }
+
   // run_forward_task + forward_now (relay/mod.rs:166-187)
   template <int W>
   __device__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
     uint64_t dur;
-    if (forward_until_blocked<W>(&dur)) forward_later<W>(dur);
+    const bool blocked = W == 0 ? forward_out(&dur) : forward_until_blocked<W>(&dur);
+    if (blocked) forward_later<W>(dur);
   }
 
   __device__ void app_task() {
@@ -719,20 +893,9 @@ struct HostExec {
   }
 
   // ---- Host::execute (host.rs:762-830) over the ordered segment + local slots ----
+  // the segment [s0, s1) arrives ordered by (time, src host, src event id) (k_segsort_*)
   __device__ void run(uint32_t s0, uint32_t s1) {
-    EvRec* seg = S.seg;
-    // order the segment by (time, src host, src event id)
-    for (uint32_t i = s0 + 1; i < s1; i++) {
-      EvRec x = seg[i];
-      uint32_t j = i;
-      while (j > s0) {
-        EvRec y = seg[j - 1];
-        if (!ev_less(x, y)) break;
-        seg[j] = y;
-        j--;
-      }
-      seg[j] = x;
-    }
+    const EvRec* seg = S.seg;
     uint32_t pi = s0;
     while (true) {
       // earliest local event by (time, event id)
@@ -896,6 +1059,118 @@ __global__ __launch_bounds__(256) void k_scatter(DevSim S) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Segmented sort: each host's due events into Shadow's event order, (time, src host, src
+// event id) (core/work/event.rs:84-155). Keys are unique (a source never reuses an id).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src, 64);
+  const uint32_t hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void seg_bounds(const DevSim& S, uint32_t h, uint32_t* s0,
+                                           uint32_t* s1) {
+  // clamp: an oversubscribed round is flagged OVF_SEG by k_scan_apply and never faults
+  *s0 = min(S.seg_start[h], S.seg_cap);
+  *s1 = min(S.seg_start[h + 1], S.seg_cap);
+}
+
+// One wave per host: segments of up to 64 events are rank-sorted in registers, each lane
+// counting (via wave-wide broadcasts) how many keys precede its own. Longer segments are
+// queued for k_segsort_big.
+__global__ __launch_bounds__(256) void k_segsort_small(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= S.nH) return;
+  uint32_t s0, s1;
+  seg_bounds(S, w, &s0, &s1);
+  const uint32_t k = s1 - s0;
+  if (k <= 1) return;
+  if (k > 64) {
+    if (lane == 0) S.big_list[atomicAdd(&C->big_n, 1u)] = w;
+    return;
+  }
+  EvRec r;
+  r.time = ~0ULL;
+  r.src = ~0u;
+  r.eid = ~0ULL;
+  if ((uint32_t)lane < k) r = S.seg[s0 + lane];
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < k; j++) {
+    const uint64_t tj = shfl64(r.time, j);
+    const uint32_t sj = __shfl(r.src, j, 64);
+    const uint64_t ej = shfl64(r.eid, j);
+    rank += (tj < r.time || (tj == r.time && (sj < r.src || (sj == r.src && ej < r.eid)))) ? 1 : 0;
+  }
+  if ((uint32_t)lane < k) S.seg[s0 + rank] = r;
+}
+
+// One workgroup per long segment: bitonic sort of an index permutation over keys held in
+// LDS, then a gather through a per-workgroup scratch slab.
+__global__ __launch_bounds__(256) void k_segsort_big(DevSim S) {
+  Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  const uint32_t nbig = C->big_n;
+  if (blockIdx.x >= nbig) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* kt = (uint64_t*)smem;
+  uint64_t* ke = kt + SORT_MAX;
+  uint32_t* ks = (uint32_t*)(ke + SORT_MAX);
+  uint32_t* ix = ks + SORT_MAX;
+  EvRec* scratch = S.sort_scratch + (size_t)blockIdx.x * SORT_MAX;
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const uint32_t h = S.big_list[b];
+    uint32_t s0, s1;
+    seg_bounds(S, h, &s0, &s1);
+    const uint32_t k = s1 - s0;
+    if (k > (uint32_t)SORT_MAX) {
+      if (threadIdx.x == 0 && (atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0)
+        C->overflow_info = S.lo + h;
+      continue;
+    }
+    uint32_t P = 64;
+    while (P < k) P <<= 1;
+    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+      if (i < k) {
+        const EvRec& e = S.seg[s0 + i];
+        kt[i] = e.time;
+        ks[i] = e.src;
+        ke[i] = e.eid;
+      } else {
+        kt[i] = ~0ULL;
+        ks[i] = ~0u;
+        ke[i] = ~0ULL;
+      }
+      ix[i] = i;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
+          const uint32_t a = 2 * stride * (i / stride) + (i % stride);
+          const uint32_t bb = a + stride;
+          const uint32_t xa = ix[a], xb = ix[bb];
+          const bool b_less = kt[xb] < kt[xa] ||
+                              (kt[xb] == kt[xa] && (ks[xb] < ks[xa] || (ks[xb] == ks[xa] && ke[xb] < ke[xa])));
+          const bool asc = (a & size) == 0;
+          if (b_less == asc) {
+            ix[a] = xb;
+            ix[bb] = xa;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) scratch[i] = S.seg[s0 + ix[i]];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) S.seg[s0 + i] = scratch[i];
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_execute(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
@@ -907,7 +1182,8 @@ __global__ __launch_bounds__(256) void k_execute(DevSim S) {
   uint64_t my_min = INVALID;
   bool executed = false;
   if (h < S.nH) {
-    const uint32_t s0 = S.seg_start[h], s1 = S.seg_start[h + 1];
+    uint32_t s0, s1;
+    seg_bounds(S, h, &s0, &s1);
     S.hist[h] = 0;
     const uint32_t nH = S.nH;
     const uint64_t t0 = S.slot_t[h], t1 = S.slot_t[nH + h], t2 = S.slot_t[2 * nH + h];
@@ -952,6 +1228,7 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
     S.bucket_n[b1] = kn;
     S.bucket_min[b1] = C->keep_min;
     C->keep_n = 0;
+    C->big_n = 0;
     C->keep_min = INVALID;
     shb0 = b0;
     shb1 = b1;
@@ -1089,9 +1366,12 @@ T* dalloc(sgn_ctx* ctx, size_t n) {
   return (T*)dev_alloc(ctx, n * sizeof(T));
 }
 
-enum { K_COUNT = 0, K_SCAN_R, K_SCAN_A, K_SCATTER, K_EXECUTE, K_FINALIZE, K_IMPORT, K_ADVANCE };
-const char* kKernelNames[8] = {"k_count", "k_scan_reduce", "k_scan_apply", "k_scatter",
-                               "k_execute", "k_finalize", "k_import", "k_advance"};
+enum { K_COUNT = 0, K_SCAN_R, K_SCAN_A, K_SCATTER, K_EXECUTE, K_FINALIZE, K_IMPORT, K_ADVANCE,
+       K_SORT_S, K_SORT_B, K_NUM };
+const char* kKernelNames[K_NUM] = {"k_count", "k_scan_reduce", "k_scan_apply", "k_scatter",
+                                   "k_execute", "k_finalize", "k_import", "k_advance",
+                                   "k_segsort_small", "k_segsort_big"};
+constexpr size_t kSortLds = (size_t)SORT_MAX * 24;
 
 int launch_round(sgn_ctx* ctx);
 
@@ -1116,6 +1396,12 @@ int launch_round(sgn_ctx* ctx) {
   time_end(ctx);
   time_begin(ctx, K_SCATTER);
   hipLaunchKernelGGL(k_scatter, dim3(grid_ev), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_SORT_S);
+  hipLaunchKernelGGL(k_segsort_small, dim3((S.nH + 3) / 4), dim3(256), 0, st, S);
+  time_end(ctx);
+  time_begin(ctx, K_SORT_B);
+  hipLaunchKernelGGL(k_segsort_big, dim3(SORT_BLOCKS), dim3(256), kSortLds, st, S);
   time_end(ctx);
   time_begin(ctx, K_EXECUTE);
   hipLaunchKernelGGL(k_execute, dim3(grid_h), dim3(256), 0, st, S);
@@ -1402,7 +1688,12 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.seg_start = dalloc<uint32_t>(ctx, nH + 1);
   S.cursor = dalloc<uint32_t>(ctx, nH + 1);
   S.block_sums = dalloc<uint32_t>(ctx, SCAN_BLOCKS);
-  if (!S.bucket_n || !S.seg || !S.hist || !S.seg_start || !S.cursor || !S.block_sums)
+  S.big_list = dalloc<uint32_t>(ctx, nH + 1);
+  S.sort_scratch = dalloc<EvRec>(ctx, (size_t)SORT_BLOCKS * SORT_MAX);
+  SGN_HIP(ctx, hipFuncSetAttribute((const void*)k_segsort_big,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortLds));
+  if (!S.bucket_n || !S.seg || !S.hist || !S.seg_start || !S.cursor || !S.block_sums ||
+      !S.big_list || !S.sort_scratch)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar)");
   if (ctx->trace_cap) {
     S.trace = dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
@@ -1449,7 +1740,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   ctx->S = S;
   ctx->sim_ready = true;
   ctx->rounds_enqueued = 0;
-  for (int i = 0; i < 8; i++) ctx->kt[i] = {kKernelNames[i], 0, 0.0};
+  for (int i = 0; i < K_NUM; i++) ctx->kt[i] = {kKernelNames[i], 0, 0.0};
   return 0;
 }
 
@@ -1613,8 +1904,8 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
     if (rc) return rc;
   }
   std::memset(out, 0, sizeof(*out));
-  out->n_kernels = 8;
-  for (int i = 0; i < 8; i++) {
+  out->n_kernels = K_NUM;
+  for (int i = 0; i < K_NUM; i++) {
     out->launches[i] = ctx->kt[i].launches;
     out->ms[i] = ctx->kt[i].ms;
     out->name[i] = kKernelNames[i];

@@ -74,7 +74,9 @@ struct Ctrl {
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
   uint64_t exec_hosts;    // cumulative host executions (hosts with due events per round)
-  uint64_t pad1[2];
+  uint32_t big_n;         // hosts whose segment needs the block-level sort this round
+  uint32_t pad2;
+  uint64_t pad1[1];
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -175,6 +177,8 @@ struct DevSim {
   uint32_t* seg_start;  // [nH + 1]
   uint32_t* cursor;     // [nH]
   uint32_t* block_sums; // [SCAN_BLOCKS]
+  uint32_t* big_list;   // [nH] hosts with segments longer than one wave
+  EvRec* sort_scratch;  // [SORT_BLOCKS * SORT_MAX]
   EvRec* seg;
   uint32_t seg_cap;
   uint32_t n_ranks;
@@ -193,6 +197,8 @@ struct DevSim {
 };
 
 constexpr int SCAN_BLOCKS = 256;
+constexpr int SORT_BLOCKS = 128;   // workgroups of the block-level segment sort
+constexpr int SORT_MAX = 4096;     // longest segment the block sort holds in LDS
 
 }  // namespace sgn
 
@@ -241,7 +247,7 @@ struct sgn_ctx {
     uint64_t launches = 0;
     double ms = 0;
   };
-  KT kt[8];
+  KT kt[16];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<std::pair<int, size_t>> ev_pending;  // (kernel, pool index)
   size_t ev_next = 0;

@@ -129,8 +129,8 @@ class RoutesTiming(C.Structure):
 
 
 class KernelTimes(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 8), ("ms", C.c_double * 8),
-                ("name", C.c_char_p * 8), ("n_kernels", C.c_uint32)]
+    _fields_ = [("launches", C.c_uint64 * 16), ("ms", C.c_double * 16),
+                ("name", C.c_char_p * 16), ("n_kernels", C.c_uint32)]
 
 
 _lib = None
