@@ -127,13 +127,15 @@ struct HostExec {
   uint32_t ro_dst, ro_pay, ro_tag;
   uint32_t ri_src, ri_pay, ri_tag;
   uint64_t ri_eid;
-  uint64_t tbb0, tbl0, tbc0, tbi0, tbb1, tbl1, tbc1, tbi1;
+  uint64_t tbb0, tbl0, tbb1, tbl1;  // balances / last refills (capacity, increment: memory)
   uint32_t cq_head, cq_len;
   uint64_t cq_bytes, cq_ie, cq_dn, cq_cur, cq_prev;
   uint32_t fq_head, fq_len;
   uint64_t dtx, drx, dapp;
-  uint64_t c_sent, c_loss, c_unknown, c_popped, c_codel, c_deliv, c_ldeliv, c_blocked,
-      c_localev, c_bytes, c_maxcodel;
+  // per-round counter increments (a host cannot see 2^32 events in one window)
+  uint32_t c_sent, c_loss, c_unknown, c_popped, c_codel, c_deliv, c_ldeliv, c_blocked,
+      c_localev, c_maxcodel;
+  uint64_t c_bytes;
   uint64_t tseq;
   uint64_t lat_cache;
 
@@ -165,12 +167,8 @@ struct HostExec {
     ri_eid = S.ri_eid[h];
     tbb0 = S.tb_bal[h];
     tbl0 = S.tb_last[h];
-    tbc0 = S.tb_cap[h];
-    tbi0 = S.tb_inc[h];
     tbb1 = S.tb_bal[nH + h];
     tbl1 = S.tb_last[nH + h];
-    tbc1 = S.tb_cap[nH + h];
-    tbi1 = S.tb_inc[nH + h];
     cq_head = S.cq_head[h];
     cq_len = S.cq_len[h];
     cq_bytes = S.cq_bytes[h];
@@ -185,8 +183,8 @@ struct HostExec {
     dapp = S.d_app[h];
     c_sent = c_loss = c_unknown = c_popped = c_codel = c_deliv = c_ldeliv = c_blocked =
         c_localev = c_bytes = 0;
-    c_maxcodel = S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
-    tseq = S.trace_seq[h];
+    c_maxcodel = (uint32_t)S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
+    tseq = S.trace_on ? S.trace_seq[h] : 0;
     lat_cache = INVALID;
   }
 
@@ -241,7 +239,7 @@ struct HostExec {
     c[CNT_LOCAL_EV * n + h] += c_localev;
     c[CNT_BYTES * n + h] += c_bytes;
     c[CNT_MAX_CODEL * n + h] = c_maxcodel;
-    S.trace_seq[h] = tseq;
+    if (S.trace_on) S.trace_seq[h] = tseq;
   }
 
   __device__ uint64_t next_local_time() const {
@@ -269,8 +267,8 @@ struct HostExec {
 
   __device__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
                         uint64_t c) {
-    uint64_t seq = tseq++;
     if (!S.trace_on) return;
+    const uint64_t seq = tseq++;
     uint64_t pos = atomicAdd((unsigned long long*)&C->trace_n, 1ULL);
     if (pos >= S.trace_cap) {
       atomicOr(&C->overflow, OVF_TRACE);
@@ -331,8 +329,7 @@ struct HostExec {
   __device__ bool tb_remove(uint64_t dec, uint64_t* dur) {
     uint64_t& bal = W == 0 ? tbb0 : tbb1;
     uint64_t& last = W == 0 ? tbl0 : tbl1;
-    const uint64_t cap = W == 0 ? tbc0 : tbc1;
-    const uint64_t inc = W == 0 ? tbi0 : tbi1;
+    const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
     const uint64_t interval = 1000000ULL;  // relay/mod.rs:279
     // lazy_refill
     uint64_t span = now - last;
@@ -341,6 +338,7 @@ struct HostExec {
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
       if (b < bal) b = ~0ULL;
+      const uint64_t cap = S.tb_cap[(size_t)W * S.nH + h];
       bal = b > cap ? cap : b;
       uint64_t adv = mul_sat(interval, nref, SIMTIME_MAX);
       last = emu_sat_add(last, adv);
@@ -1468,6 +1466,18 @@ void time_end(sgn_ctx* ctx) {
 
 void time_collect(sgn_ctx* ctx) {
   if (!(ctx->flags & (SGN_CREATE_TIME_KERNELS | SGN_CREATE_TIME_EXECUTE))) return;
+  if (ctx->graph_pending) {
+    // events recorded by the replayed graph's event-record nodes
+    for (auto& p : ctx->graph_timed) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ctx->ev_pool[p.second].first,
+                              ctx->ev_pool[p.second].second) == hipSuccess) {
+        ctx->kt[p.first].ms += ms;
+        ctx->kt[p.first].launches++;
+      }
+    }
+    ctx->graph_pending = false;
+  }
   for (auto& p : ctx->ev_pending) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ctx->ev_pool[p.second].first, ctx->ev_pool[p.second].second) ==
@@ -1481,6 +1491,13 @@ void time_collect(sgn_ctx* ctx) {
 }
 
 void free_sim(sgn_ctx* ctx) {
+  if (ctx->gexec) hipGraphExecDestroy(ctx->gexec);
+  if (ctx->graph) hipGraphDestroy(ctx->graph);
+  ctx->gexec = nullptr;
+  ctx->graph = nullptr;
+  ctx->gbatch = 0;
+  ctx->graph_timed.clear();
+  ctx->graph_pending = false;
   for (void* p : ctx->allocs) hipFree(p);
   ctx->allocs.clear();
   if (ctx->h_ctrl) {
@@ -1770,11 +1787,36 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   if (rc) return rc;
   const uint64_t r_start = ctx->h_ctrl->rounds;
   uint64_t enq = 0;
-  const uint64_t batch = ctx->nranks > 1 ? 1 : 64;
+  // Rounds are enqueued in batches with one host synchronisation per batch (the window
+  // lives on the device; kernels of rounds past the end return at once). On a single
+  // shard a full batch is one hipGraph replay: the round's launches are captured once.
+  const uint64_t batch = 32;
+  const bool graph = ctx->nranks == 1 && ctx->use_graph;
   while (ctx->h_ctrl->active && enq < max_rounds) {
     const uint64_t n = std::min<uint64_t>(batch, max_rounds - enq);
-    for (uint64_t i = 0; i < n; i++)
-      if ((rc = launch_round(ctx))) return rc;
+    if (graph && n == batch) {
+      if (!ctx->gexec) {
+        ctx->ev_pending.clear();
+        ctx->ev_next = 0;
+        SGN_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        for (uint64_t i = 0; i < n && rc == 0; i++) rc = launch_round(ctx);
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc) return rc;
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamEndCapture");
+        ctx->graph = g;
+        SGN_HIP(ctx, hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0));
+        ctx->graph_timed = ctx->ev_pending;
+        ctx->ev_pending.clear();
+        ctx->ev_next = 0;
+        ctx->gbatch = batch;
+      }
+      SGN_HIP(ctx, hipGraphLaunch(ctx->gexec, ctx->stream));
+      ctx->graph_pending = !ctx->graph_timed.empty();
+    } else {
+      for (uint64_t i = 0; i < n; i++)
+        if ((rc = launch_round(ctx))) return rc;
+    }
     enq += n;
     if ((rc = sync_ctrl(ctx))) return rc;
   }

@@ -252,6 +252,14 @@ struct sgn_ctx {
   std::vector<std::pair<int, size_t>> ev_pending;  // (kernel, pool index)
   size_t ev_next = 0;
 
+  // a batch of rounds captured once as a hipGraph and replayed (single shard)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  uint64_t gbatch = 0;
+  std::vector<std::pair<int, size_t>> graph_timed;
+  bool graph_pending = false;
+  bool use_graph = true;
+
   ~sgn_ctx();
 };
 
