@@ -1440,11 +1440,63 @@ int sync_ctrl(sgn_ctx* ctx) {
   return check_overflow(ctx);
 }
 
+// Event-record nodes around the timed kernel nodes of a captured batch (a captured
+// hipEventRecord yields no timing on ROCm 7.2; explicit record nodes do).
+int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
+  const bool all = ctx->flags & SGN_CREATE_TIME_KERNELS;
+  const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
+  ctx->graph_timed.clear();
+  if (!all && !exec) return 0;
+  const void* fn[K_NUM] = {(const void*)k_count, (const void*)k_scan_reduce,
+                           (const void*)k_scan_apply, (const void*)k_scatter,
+                           (const void*)k_execute, (const void*)k_finalize,
+                           (const void*)k_import, (const void*)k_advance,
+                           (const void*)k_segsort_small, (const void*)k_segsort_big};
+  size_t n = 0;
+  SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  SGN_HIP(ctx, hipGraphGetNodes(g, nodes.data(), &n));
+  size_t ev = 0;
+  for (hipGraphNode_t node : nodes) {
+    hipGraphNodeType t;
+    SGN_HIP(ctx, hipGraphNodeGetType(node, &t));
+    if (t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams p;
+    SGN_HIP(ctx, hipGraphKernelNodeGetParams(node, &p));
+    int kid = -1;
+    for (int k = 0; k < K_NUM; k++)
+      if (p.func == fn[k]) kid = k;
+    if (kid < 0 || (!all && kid != K_EXECUTE)) continue;
+    if (ev >= ctx->ev_pool.size()) {
+      hipEvent_t a, b;
+      SGN_HIP(ctx, hipEventCreate(&a));
+      SGN_HIP(ctx, hipEventCreate(&b));
+      ctx->ev_pool.push_back({a, b});
+    }
+    size_t nd = 0, nn = 0;
+    SGN_HIP(ctx, hipGraphNodeGetDependencies(node, nullptr, &nd));
+    std::vector<hipGraphNode_t> deps(nd);
+    if (nd) SGN_HIP(ctx, hipGraphNodeGetDependencies(node, deps.data(), &nd));
+    SGN_HIP(ctx, hipGraphNodeGetDependentNodes(node, nullptr, &nn));
+    std::vector<hipGraphNode_t> outs(nn);
+    if (nn) SGN_HIP(ctx, hipGraphNodeGetDependentNodes(node, outs.data(), &nn));
+    hipGraphNode_t a, b;
+    SGN_HIP(ctx, hipGraphAddEventRecordNode(&a, g, nd ? deps.data() : nullptr, nd, ctx->ev_pool[ev].first));
+    SGN_HIP(ctx, hipGraphAddDependencies(g, &a, &node, 1));
+    SGN_HIP(ctx, hipGraphAddEventRecordNode(&b, g, &node, 1, ctx->ev_pool[ev].second));
+    for (hipGraphNode_t o : outs) SGN_HIP(ctx, hipGraphAddDependencies(g, &b, &o, 1));
+    ctx->graph_timed.push_back({kid, ev});
+    ev++;
+  }
+  return 0;
+}
+
 }  // namespace
 
 namespace sgn {
 
 void time_begin(sgn_ctx* ctx, int kernel) {
+  if (ctx->capturing) return;  // graph mode: event-record nodes are added after capture
   const bool all = ctx->flags & SGN_CREATE_TIME_KERNELS;
   const bool exec = (ctx->flags & SGN_CREATE_TIME_EXECUTE) && kernel == K_EXECUTE;
   if (!all && !exec) return;
@@ -1458,6 +1510,7 @@ void time_begin(sgn_ctx* ctx, int kernel) {
 }
 
 void time_end(sgn_ctx* ctx) {
+  if (ctx->capturing) return;
   if (!(ctx->flags & (SGN_CREATE_TIME_KERNELS | SGN_CREATE_TIME_EXECUTE))) return;
   if (ctx->ev_pending.empty() || ctx->ev_pending.back().second != ctx->ev_next) return;
   hipEventRecord(ctx->ev_pool[ctx->ev_next].second, ctx->stream);
@@ -1798,17 +1851,18 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
       if (!ctx->gexec) {
         ctx->ev_pending.clear();
         ctx->ev_next = 0;
-        SGN_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-        for (uint64_t i = 0; i < n && rc == 0; i++) rc = launch_round(ctx);
+        ctx->capturing = true;
+        hipError_t e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
+        for (uint64_t i = 0; i < n && rc == 0 && e == hipSuccess; i++) rc = launch_round(ctx);
         hipGraph_t g = nullptr;
-        hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        hipError_t e2 = hipStreamEndCapture(ctx->stream, &g);
+        ctx->capturing = false;
         if (rc) return rc;
-        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamEndCapture");
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamBeginCapture");
+        if (e2 != hipSuccess) return hip_fail(ctx, e2, "hipStreamEndCapture");
         ctx->graph = g;
+        if ((rc = add_timing_nodes(ctx, g))) return rc;
         SGN_HIP(ctx, hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0));
-        ctx->graph_timed = ctx->ev_pending;
-        ctx->ev_pending.clear();
-        ctx->ev_next = 0;
         ctx->gbatch = batch;
       }
       SGN_HIP(ctx, hipGraphLaunch(ctx->gexec, ctx->stream));

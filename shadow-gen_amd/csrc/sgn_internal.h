@@ -259,6 +259,7 @@ struct sgn_ctx {
   std::vector<std::pair<int, size_t>> graph_timed;
   bool graph_pending = false;
   bool use_graph = true;
+  bool capturing = false;
 
   ~sgn_ctx();
 };
