@@ -138,6 +138,8 @@ struct HostExec {
   uint64_t c_bytes;
   uint64_t tseq;
   uint64_t lat_cache;
+  CodelEnt cqc[4];  // prefetched head of the CoDel ring (cqc[0] = entry at cq_head)
+  uint32_t cqc_n;
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint64_t kb)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1_keep_base(kb), b1(bucket1) {
@@ -186,6 +188,7 @@ struct HostExec {
     c_maxcodel = (uint32_t)S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
     tseq = S.trace_on ? S.trace_seq[h] : 0;
     lat_cache = INVALID;
+    cqc_n = 0;
   }
 
   __device__ void store() {
@@ -405,7 +408,18 @@ struct HostExec {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    CodelEnt e = *cq_slot(0);
+    if (cqc_n == 0) {
+      // refill the head window: up to four independent ring loads in flight at once
+      cqc_n = min(4u, cq_len);
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++)
+        if (j < cqc_n) cqc[j] = *cq_slot(j);
+    }
+    const CodelEnt e = cqc[0];
+    cqc[0] = cqc[1];
+    cqc[1] = cqc[2];
+    cqc[2] = cqc[3];
+    cqc_n--;
     cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
     cq_len--;
     cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + SGN_UDP_HEADER_BYTES);
@@ -902,16 +916,33 @@ struct HostExec {
       if (st1 < lt || (st1 == lt && se1 < le)) { lt = st1; le = se1; ls = 1; }
       if (st2 < lt || (st2 == lt && se2 < le)) { lt = st2; le = se2; ls = 2; }
       if (pi < s1) {
-        const uint64_t pt = seg[pi].time;
-        if (pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
-          EvRec ev = seg[pi];
-          pi++;
-          now = ev.time;
-          c_popped++;
-          drx = sgn_digest3(drx, ev.time, ev.src, ev.eid);
-          trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid);
-          codel_push(ev);     // Router::route_incoming_packet (router/mod.rs:55-57)
-          relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
+        // packet events are consumed in chunks of up to four: the four segment loads
+        // are independent, so their latency overlaps instead of serialising per event
+        constexpr uint32_t K = 4;
+        EvRec buf[K];
+        const uint32_t nb = min(K, s1 - pi);
+#pragma unroll
+        for (uint32_t j = 0; j < K; j++)
+          if (j < nb) buf[j] = seg[pi + j];
+        if (buf[0].time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+#pragma unroll
+          for (uint32_t j = 0; j < K; j++) {
+            if (j >= nb) break;
+            if (j > 0) {
+              // a pop can only (re)schedule relay_inet_in, at `now`
+              uint64_t t = st0 < st1 ? st0 : st1;
+              t = st2 < t ? st2 : t;
+              if (buf[j].time > t) break;
+            }
+            const EvRec& ev = buf[j];
+            pi++;
+            now = ev.time;
+            c_popped++;
+            drx = sgn_digest3(drx, ev.time, ev.src, ev.eid);
+            trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid);
+            codel_push(ev);     // Router::route_incoming_packet (router/mod.rs:55-57)
+            relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
+          }
           continue;
         }
       }
@@ -1169,7 +1200,7 @@ __global__ __launch_bounds__(256) void k_segsort_big(DevSim S) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_execute(DevSim S) {
+__global__ __launch_bounds__(64) void k_execute(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
   __shared__ uint64_t sh[4];
@@ -1382,7 +1413,7 @@ int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
   const uint32_t grid_ev = 1024;
-  const uint32_t grid_h = (S.nH + 255) / 256;
+  const uint32_t grid_h = (S.nH + 63) / 64;
   time_begin(ctx, K_COUNT);
   hipLaunchKernelGGL(k_count, dim3(grid_ev), dim3(256), 0, st, S);
   time_end(ctx);
@@ -1402,7 +1433,7 @@ int launch_round(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_segsort_big, dim3(SORT_BLOCKS), dim3(256), kSortLds, st, S);
   time_end(ctx);
   time_begin(ctx, K_EXECUTE);
-  hipLaunchKernelGGL(k_execute, dim3(grid_h), dim3(256), 0, st, S);
+  hipLaunchKernelGGL(k_execute, dim3(grid_h), dim3(64), 0, st, S);
   time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
