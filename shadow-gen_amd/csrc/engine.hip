@@ -1118,6 +1118,15 @@ __global__ __launch_bounds__(256) void k_segsort_small(DevSim S) {
   seg_bounds(S, w, &s0, &s1);
   const uint32_t k = s1 - s0;
   if (k <= 1) return;
+  if (k >= HEAVY_T && lane == 0) {
+    // long segments run on dedicated waves of k_execute, dispatched first and packed with
+    // hosts of the same kind so their (longest) event loops stay convergent
+    const uint32_t pos = atomicAdd(&C->heavy_n, 1u);
+    if (pos < S.heavy_cap) {
+      S.heavy_list[pos] = w;
+      S.heavy_tag[w] = (uint32_t)C->rounds + 1;
+    }
+  }
   if (k > 64) {
     if (lane == 0) S.big_list[atomicAdd(&C->big_n, 1u)] = w;
     return;
@@ -1207,13 +1216,30 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   const uint64_t we = C->we;
   const uint32_t b1 = bucket_of(S, we - 1);
   const uint64_t keep_base = C->keep_base;
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  // Workgroups [0, heavy_blocks) take the hosts on heavy_list (long segments), one per
+  // lane; the rest take hosts in HostId order and skip those already on a heavy wave.
+  uint32_t h;
+  bool take;
+  if (blockIdx.x < S.heavy_blocks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = min(C->heavy_n, S.heavy_cap);
+    take = i < n;
+    h = take ? S.heavy_list[i] : 0;
+  } else {
+    h = (blockIdx.x - S.heavy_blocks) * blockDim.x + threadIdx.x;
+    take = h < S.nH;
+    if (take) {
+      S.hist[h] = 0;
+      take = S.heavy_tag[h] != (uint32_t)C->rounds + 1;
+    }
+  }
   uint64_t my_min = INVALID;
   bool executed = false;
-  if (h < S.nH) {
+  uint32_t n_ev = 0;  // diagnostic: events this lane handled (stamps build only)
+  const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  if (take) {
     uint32_t s0, s1;
     seg_bounds(S, h, &s0, &s1);
-    S.hist[h] = 0;
     const uint32_t nH = S.nH;
     const uint64_t t0 = S.slot_t[h], t1 = S.slot_t[nH + h], t2 = S.slot_t[2 * nH + h];
     uint64_t lmin = t0 < t1 ? t0 : t1;
@@ -1226,6 +1252,25 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       my_min = ex.next_local_time();
       ex.store();
       executed = true;
+      n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_unknown + ex.c_deliv + ex.c_localev +
+             ex.c_codel;
+    }
+  }
+  if (S.stamps) {
+    // per-wave diagnostics: shader cycles, total and max events over the wave's lanes
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime();
+    uint32_t sum = n_ev, mx = n_ev;
+    for (int off = 32; off > 0; off >>= 1) {
+      sum += __shfl_xor(sum, off, 64);
+      const uint32_t o = __shfl_xor(mx, off, 64);
+      mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      uint64_t* st = S.stamps + 4 * (size_t)blockIdx.x;
+      st[0] = clk1 - clk0;
+      st[1] = sum;
+      st[2] = mx;
+      st[3] = __popcll(__ballot(n_ev > 0));
     }
   }
   // hosts that ran this round (roofline accounting: their state made a round trip)
@@ -1258,6 +1303,7 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
     S.bucket_min[b1] = C->keep_min;
     C->keep_n = 0;
     C->big_n = 0;
+    C->heavy_n = 0;
     C->keep_min = INVALID;
     shb0 = b0;
     shb1 = b1;
@@ -1413,7 +1459,7 @@ int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
   const uint32_t grid_ev = 1024;
-  const uint32_t grid_h = (S.nH + 63) / 64;
+  const uint32_t grid_h = S.heavy_blocks + (S.nH + 63) / 64;
   time_begin(ctx, K_COUNT);
   hipLaunchKernelGGL(k_count, dim3(grid_ev), dim3(256), 0, st, S);
   time_end(ctx);
@@ -1790,6 +1836,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.cursor = dalloc<uint32_t>(ctx, nH + 1);
   S.block_sums = dalloc<uint32_t>(ctx, SCAN_BLOCKS);
   S.big_list = dalloc<uint32_t>(ctx, nH + 1);
+  S.heavy_cap = ((std::max<uint32_t>(1024, nH / 16) + 63) / 64) * 64;
+  S.heavy_blocks = S.heavy_cap / 64;
+  S.heavy_list = dalloc<uint32_t>(ctx, S.heavy_cap);
+  S.heavy_tag = dalloc<uint32_t>(ctx, nH + 1);
+  if (!S.heavy_list || !S.heavy_tag) return set_error(ctx, SGN_ENOMEM, "device allocation failed (heavy list)");
+  if (getenv("SGN_STAMPS"))
+    S.stamps = dalloc<uint64_t>(ctx, 4 * ((size_t)nH / 64 + 1 + S.heavy_blocks));
   S.sort_scratch = dalloc<EvRec>(ctx, (size_t)SORT_BLOCKS * SORT_MAX);
   SGN_HIP(ctx, hipFuncSetAttribute((const void*)k_segsort_big,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortLds));
@@ -2037,6 +2090,18 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
     out->ms[i] = ctx->kt[i].ms;
     out->name[i] = kKernelNames[i];
   }
+  return 0;
+}
+
+// Diagnostics: per-wave {cycles, events, max lane events, busy lanes} of the last k_execute
+// (allocated when SGN_STAMPS=1 is set in the environment at sgn_sim_init).
+int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!ctx || !ctx->sim_ready) return SGN_EINVAL;
+  const uint64_t waves = (ctx->S.nH + 63) / 64 + ctx->S.heavy_blocks;
+  if (n) *n = ctx->S.stamps ? waves : 0;
+  if (!ctx->S.stamps || !out) return 0;
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SGN_HIP(ctx, hipMemcpy(out, ctx->S.stamps, std::min(cap, waves) * 32, hipMemcpyDeviceToHost));
   return 0;
 }
 

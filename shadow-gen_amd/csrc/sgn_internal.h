@@ -75,7 +75,7 @@ struct Ctrl {
   uint64_t remote_min;    // multi-GPU: min over events exported this round
   uint64_t exec_hosts;    // cumulative host executions (hosts with due events per round)
   uint32_t big_n;         // hosts whose segment needs the block-level sort this round
-  uint32_t pad2;
+  uint32_t heavy_n;       // hosts scheduled on the heavy waves of k_execute this round
   uint64_t pad1[1];
 };
 
@@ -179,6 +179,11 @@ struct DevSim {
   uint32_t* block_sums; // [SCAN_BLOCKS]
   uint32_t* big_list;   // [nH] hosts with segments longer than one wave
   EvRec* sort_scratch;  // [SORT_BLOCKS * SORT_MAX]
+  uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
+  uint32_t* heavy_list; // [heavy_cap] hosts with long segments this round
+  uint32_t* heavy_tag;  // [nH] round number + 1 when the host is on heavy_list
+  uint32_t heavy_cap;   // heavy wave slots (multiple of 64)
+  uint32_t heavy_blocks;
   EvRec* seg;
   uint32_t seg_cap;
   uint32_t n_ranks;
@@ -199,6 +204,7 @@ struct DevSim {
 constexpr int SCAN_BLOCKS = 256;
 constexpr int SORT_BLOCKS = 128;   // workgroups of the block-level segment sort
 constexpr int SORT_MAX = 4096;     // longest segment the block sort holds in LDS
+constexpr uint32_t HEAVY_T = 16;   // due events that make a host "heavy" for one round
 
 }  // namespace sgn
 
