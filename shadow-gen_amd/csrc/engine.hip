@@ -1216,14 +1216,16 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   const uint64_t we = C->we;
   const uint32_t b1 = bucket_of(S, we - 1);
   const uint64_t keep_base = C->keep_base;
-  // Workgroups [0, heavy_blocks) take the hosts on heavy_list (long segments), one per
-  // lane; the rest take hosts in HostId order and skip those already on a heavy wave.
+  // Workgroups [0, heavy_blocks) each take ONE host of heavy_list (long segments) on lane 0:
+  // a heavy host's event loop is the round's critical path, so it gets a wave of its own
+  // (no divergence with other hosts) dispatched before everything else. The rest take
+  // hosts in HostId order and skip those already on a heavy wave.
   uint32_t h;
   bool take;
   if (blockIdx.x < S.heavy_blocks) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = blockIdx.x;
     const uint32_t n = min(C->heavy_n, S.heavy_cap);
-    take = i < n;
+    take = threadIdx.x == 0 && i < n;
     h = take ? S.heavy_list[i] : 0;
   } else {
     h = (blockIdx.x - S.heavy_blocks) * blockDim.x + threadIdx.x;
@@ -1836,8 +1838,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.cursor = dalloc<uint32_t>(ctx, nH + 1);
   S.block_sums = dalloc<uint32_t>(ctx, SCAN_BLOCKS);
   S.big_list = dalloc<uint32_t>(ctx, nH + 1);
-  S.heavy_cap = ((std::max<uint32_t>(1024, nH / 16) + 63) / 64) * 64;
-  S.heavy_blocks = S.heavy_cap / 64;
+  S.heavy_cap = std::min<uint32_t>(2048, std::max<uint32_t>(64, nH / 128));
+  S.heavy_blocks = S.heavy_cap;
   S.heavy_list = dalloc<uint32_t>(ctx, S.heavy_cap);
   S.heavy_tag = dalloc<uint32_t>(ctx, nH + 1);
   if (!S.heavy_list || !S.heavy_tag) return set_error(ctx, SGN_ENOMEM, "device allocation failed (heavy list)");

@@ -182,7 +182,7 @@ struct DevSim {
   uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
   uint32_t* heavy_list; // [heavy_cap] hosts with long segments this round
   uint32_t* heavy_tag;  // [nH] round number + 1 when the host is on heavy_list
-  uint32_t heavy_cap;   // heavy wave slots (multiple of 64)
+  uint32_t heavy_cap;   // heavy waves (one host each)
   uint32_t heavy_blocks;
   EvRec* seg;
   uint32_t seg_cap;
