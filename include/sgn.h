@@ -323,9 +323,11 @@ int sgn_units_parse(int32_t kind, const char* text, uint64_t* value_base);
  * (router/codel_queue.rs:285-298), for checking device f64 rounding against the host. */
 int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out);
 
-/* Diagnostics of the last execute launch, 4 u64 per wave of 64 hosts: {shader cycles,
- * events handled, max events of one host, hosts with events}. Needs SGN_STAMPS=1 in the
- * environment at sgn_sim_init; n = number of waves (0 when disabled). */
+/* Diagnostics of the last execute launch, SGN_STAMP_WORDS u64 per wave: {shader cycles,
+ * events handled, max events of one host, hosts with events, then (diagnostic build
+ * libsgn_diag.so only) lane 0's per-event-kind cycles and counts}. Needs SGN_STAMPS=1 in
+ * the environment at sgn_sim_init; n = number of waves (0 when disabled), cap in waves. */
+#define SGN_STAMP_WORDS 16
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n);
 
 #ifdef __cplusplus

@@ -140,6 +140,11 @@ struct HostExec {
   uint64_t lat_cache;
   CodelEnt cqc[4];  // prefetched head of the CoDel ring (cqc[0] = entry at cq_head)
   uint32_t cqc_n;
+#ifdef SGN_PHASES
+  // diagnostic build only (libsgn_diag.so): shader cycles and counts per event kind
+  uint64_t ph[4];
+  uint32_t pn[4];
+#endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint64_t kb)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1_keep_base(kb), b1(bucket1) {
@@ -189,6 +194,9 @@ struct HostExec {
     tseq = S.trace_on ? S.trace_seq[h] : 0;
     lat_cache = INVALID;
     cqc_n = 0;
+#ifdef SGN_PHASES
+    for (int i = 0; i < 4; i++) ph[i] = 0, pn[i] = 0;
+#endif
   }
 
   __device__ void store() {
@@ -925,6 +933,9 @@ struct HostExec {
         for (uint32_t j = 0; j < K; j++)
           if (j < nb) buf[j] = seg[pi + j];
         if (buf[0].time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+#ifdef SGN_PHASES
+          const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
           for (uint32_t j = 0; j < K; j++) {
             if (j >= nb) break;
@@ -943,12 +954,19 @@ struct HostExec {
             codel_push(ev);     // Router::route_incoming_packet (router/mod.rs:55-57)
             relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
           }
+#ifdef SGN_PHASES
+          ph[0] += __builtin_amdgcn_s_memtime() - pt0;
+          pn[0]++;
+#endif
           continue;
         }
       }
       if (lt >= we) break;
       now = lt;
       c_localev++;
+#ifdef SGN_PHASES
+      const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
       if (ls == 0) {
         st0 = INVALID;
         run_forward_task<0>();
@@ -959,6 +977,10 @@ struct HostExec {
         st2 = INVALID;
         app_task();
       }
+#ifdef SGN_PHASES
+      ph[1 + ls] += __builtin_amdgcn_s_memtime() - pt1;
+      pn[1 + ls]++;
+#endif
     }
   }
 };
@@ -1239,6 +1261,11 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   bool executed = false;
   uint32_t n_ev = 0;  // diagnostic: events this lane handled (stamps build only)
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#ifdef SGN_PHASES
+  uint64_t dph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t dpn[4] = {0, 0, 0, 0};
+  uint32_t dcnt[4] = {0, 0, 0, 0};
+#endif
   if (take) {
     uint32_t s0, s1;
     seg_bounds(S, h, &s0, &s1);
@@ -1249,11 +1276,31 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
     if (s0 == s1 && lmin >= we) {
       my_min = lmin;  // nothing due: the host sleeps through this window
     } else {
+#ifdef SGN_PHASES
+      const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
       HostExec ex(S, h, we, b1, keep_base);
+#ifdef SGN_PHASES
+      const uint64_t q1 = __builtin_amdgcn_s_memtime();
+#endif
       ex.run(s0, s1);
       my_min = ex.next_local_time();
+#ifdef SGN_PHASES
+      const uint64_t q2 = __builtin_amdgcn_s_memtime();
+#endif
       ex.store();
       executed = true;
+#ifdef SGN_PHASES
+      const uint64_t q3 = __builtin_amdgcn_s_memtime();
+      for (int i = 0; i < 4; i++) dph[i] = ex.ph[i], dpn[i] = ex.pn[i];
+      dph[4] = q1 - q0;
+      dph[5] = q3 - q2;
+      dph[6] = q2 - q1;
+      dcnt[0] = ex.c_popped;
+      dcnt[1] = ex.c_sent + ex.c_loss + ex.c_unknown;
+      dcnt[2] = ex.c_deliv;
+      dcnt[3] = ex.c_codel;
+#endif
       n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_unknown + ex.c_deliv + ex.c_localev +
              ex.c_codel;
     }
@@ -1267,12 +1314,21 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       const uint32_t o = __shfl_xor(mx, off, 64);
       mx = o > mx ? o : mx;
     }
+    const uint32_t busy = __popcll(__ballot(n_ev > 0));
     if ((threadIdx.x & 63) == 0) {
-      uint64_t* st = S.stamps + 4 * (size_t)blockIdx.x;
+      uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)blockIdx.x;
       st[0] = clk1 - clk0;
       st[1] = sum;
       st[2] = mx;
-      st[3] = __popcll(__ballot(n_ev > 0));
+      st[3] = busy;
+#ifdef SGN_PHASES
+      // lane 0's breakdown: pop chunks, relay_out / relay_in / app tasks, load, store, run
+      for (int i = 0; i < 7; i++) st[4 + i] = dph[i];
+      st[11] = dpn[0] | ((uint64_t)dpn[1] << 32);
+      st[12] = dpn[2] | ((uint64_t)dpn[3] << 32);
+      st[13] = dcnt[0] | ((uint64_t)dcnt[1] << 32);
+      st[14] = dcnt[2] | ((uint64_t)dcnt[3] << 32);
+#endif
     }
   }
   // hosts that ran this round (roofline accounting: their state made a round trip)
@@ -1844,7 +1900,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.heavy_tag = dalloc<uint32_t>(ctx, nH + 1);
   if (!S.heavy_list || !S.heavy_tag) return set_error(ctx, SGN_ENOMEM, "device allocation failed (heavy list)");
   if (getenv("SGN_STAMPS"))
-    S.stamps = dalloc<uint64_t>(ctx, 4 * ((size_t)nH / 64 + 1 + S.heavy_blocks));
+    S.stamps = dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * ((size_t)nH / 64 + 1 + S.heavy_blocks));
   S.sort_scratch = dalloc<EvRec>(ctx, (size_t)SORT_BLOCKS * SORT_MAX);
   SGN_HIP(ctx, hipFuncSetAttribute((const void*)k_segsort_big,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortLds));
@@ -2103,7 +2159,7 @@ int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (n) *n = ctx->S.stamps ? waves : 0;
   if (!ctx->S.stamps || !out) return 0;
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  SGN_HIP(ctx, hipMemcpy(out, ctx->S.stamps, std::min(cap, waves) * 32, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(out, ctx->S.stamps, std::min(cap, waves) * SGN_STAMP_WORDS * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -12,7 +12,8 @@ import bench
 import sgn
 
 g, used, hosts, cfg, tr = bench.build_workload(int(sys.argv[1]) if len(sys.argv) > 1 else 100_000, 1000)
-ctx = sgn.Context()
+lib = sgn.load(sgn.HERE / "libsgn_diag.so")
+ctx = sgn.Context(lib=lib)
 ctx.routes_build(g, used)
 ctx.hosts_set(hosts)
 ctx.sim_init(cfg, tr)
@@ -22,9 +23,9 @@ ctx.check(ctx.L.sgn_debug_stamps(ctx.h, None, 0, sgn.C.byref(n)))
 W = n.value
 for r in range(3):
     ctx.round()
-    out = np.zeros(4 * W, dtype=np.uint64)
+    out = np.zeros(16 * W, dtype=np.uint64)
     ctx.check(ctx.L.sgn_debug_stamps(ctx.h, sgn.ptr(out, sgn.C.c_uint64), W, sgn.C.byref(n)))
-    s = out.reshape(W, 4).astype(np.int64)
+    s = out.reshape(W, 16).astype(np.int64)
     cyc, ev, mx, busy = s[:, 0], s[:, 1], s[:, 2], s[:, 3]
     order = np.argsort(cyc)[::-1]
     print(f"round {r}: waves={W} cycles max={cyc.max()} p50={np.median(cyc):.0f} p99={np.percentile(cyc, 99):.0f}"
@@ -32,6 +33,11 @@ for r in range(3):
     for i in order[:12]:
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} max_lane={mx[i]:4d} busy_lanes={busy[i]:2d}"
               f"  cyc/event={cyc[i] / max(ev[i], 1):7.1f}")
+        p = s[i, 4:11]
+        n = [s[i, 11] & 0xFFFFFFFF, s[i, 11] >> 32, s[i, 12] & 0xFFFFFFFF, s[i, 12] >> 32]
+        c = [s[i, 13] & 0xFFFFFFFF, s[i, 13] >> 32, s[i, 14] & 0xFFFFFFFF, s[i, 14] >> 32]
+        print(f"      lane0: pop {p[0]}c/{n[0]} chunks, ro {p[1]}c/{n[1]}, ri {p[2]}c/{n[2]}, app {p[3]}c/{n[3]}"
+              f" | load {p[4]} run {p[6]} store {p[5]} | popped {c[0]} sends {c[1]} deliv {c[2]} codel {c[3]}")
     sel = ev > 0
     A = np.stack([ev[sel], mx[sel], np.ones(sel.sum())], 1)
     coef, *_ = np.linalg.lstsq(A, cyc[sel], rcond=None)
