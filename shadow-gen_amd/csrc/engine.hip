@@ -128,7 +128,7 @@ struct HostExec {
   uint32_t ri_src, ri_pay, ri_tag;
   uint64_t ri_eid;
   uint64_t tbb0, tbl0, tbb1, tbl1;  // balances / last refills (capacity, increment: memory)
-  uint32_t cq_head, cq_len;
+  uint32_t cq_head, cq_nr, cq_len;  // head run slot, runs in the ring, packets queued
   uint64_t cq_bytes, cq_ie, cq_dn, cq_cur, cq_prev;
   uint32_t fq_head, fq_len;
   uint64_t dtx, drx, dapp;
@@ -138,8 +138,10 @@ struct HostExec {
   uint64_t c_bytes;
   uint64_t tseq;
   uint64_t lat_cache;
-  CodelEnt cqc[4];  // prefetched head of the CoDel ring (cqc[0] = entry at cq_head)
-  uint32_t cqc_n;
+  // CoDel run cache: the head run being consumed and the tail run being extended live in
+  // registers; their ring slots are stale until store() (or until the tail is closed).
+  CodelEnt hd, tl;
+  bool hd_valid, tl_open;
 #ifdef SGN_PHASES
   // diagnostic build only (libsgn_diag.so): shader cycles and counts per event kind
   uint64_t ph[4];
@@ -177,6 +179,7 @@ struct HostExec {
     tbb1 = S.tb_bal[nH + h];
     tbl1 = S.tb_last[nH + h];
     cq_head = S.cq_head[h];
+    cq_nr = S.cq_nr[h];
     cq_len = S.cq_len[h];
     cq_bytes = S.cq_bytes[h];
     cq_ie = S.cq_ie[h];
@@ -193,7 +196,7 @@ struct HostExec {
     c_maxcodel = (uint32_t)S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
     tseq = S.trace_on ? S.trace_seq[h] : 0;
     lat_cache = INVALID;
-    cqc_n = 0;
+    hd_valid = tl_open = false;
 #ifdef SGN_PHASES
     for (int i = 0; i < 4; i++) ph[i] = 0, pn[i] = 0;
 #endif
@@ -225,7 +228,10 @@ struct HostExec {
     S.tb_last[h] = tbl0;
     S.tb_bal[nH + h] = tbb1;
     S.tb_last[nH + h] = tbl1;
+    if (hd_valid) *cq_slot(0) = hd;
+    if (tl_open) *cq_slot(cq_nr - 1) = tl;
     S.cq_head[h] = cq_head;
+    S.cq_nr[h] = cq_nr;
     S.cq_len[h] = cq_len;
     S.cq_bytes[h] = cq_bytes;
     S.cq_ie[h] = cq_ie;
@@ -340,11 +346,12 @@ struct HostExec {
   __device__ bool tb_remove(uint64_t dec, uint64_t* dur) {
     uint64_t& bal = W == 0 ? tbb0 : tbb1;
     uint64_t& last = W == 0 ? tbl0 : tbl1;
-    const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
     const uint64_t interval = 1000000ULL;  // relay/mod.rs:279
-    // lazy_refill
+    // lazy_refill. The refill increment and capacity stay in memory (they are only read
+    // when a refill is due or a removal fails, not on the per-packet fast path).
     uint64_t span = now - last;
     if (span >= interval) {
+      const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
       uint64_t nref = span / interval;
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
@@ -358,6 +365,7 @@ struct HostExec {
     uint64_t next_refill_span = interval - span;
     if (dec > bal) {
       // compute_conforming_duration (:91-117)
+      const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
       uint64_t req = dec - bal;
       uint64_t n = req / inc + ((req % inc) ? 1 : 0);
       if (n == 0)
@@ -382,21 +390,38 @@ struct HostExec {
     if (idx >= S.codel_cap) idx -= S.codel_cap;
     return S.codel + (size_t)h * S.codel_cap + idx;
   }
-  __device__ void codel_push(const EvRec& ev) {  // :303-317
-    if (cq_len >= S.codel_cap) {
-      overflow(OVF_CODEL);
-      return;
+  // Router::route_incoming_packet (router/mod.rs:55-57) -> CoDelQueue::push (:303-317) for a
+  // run of n packets arriving at `now`: extends the open tail run when it continues it.
+  __device__ void codel_push_run(uint32_t src, uint64_t eid0, uint32_t payload, uint32_t tag,
+                                 uint32_t n) {
+    const auto continues = [&](const CodelEnt& r) {
+      return r.enqueue_ts == now && r.src == src && r.eid + r.count == eid0 &&
+             r.payload == payload && r.tag == tag;
+    };
+    if (tl_open && continues(tl)) {
+      tl.count += n;
+    } else if (!tl_open && hd_valid && cq_nr == 1 && continues(hd)) {
+      hd.count += n;
+    } else {
+      if (tl_open) {
+        *cq_slot(cq_nr - 1) = tl;
+        tl_open = false;
+      }
+      if (cq_nr >= S.codel_cap) {
+        overflow(OVF_CODEL);
+        return;
+      }
+      tl.enqueue_ts = now;
+      tl.eid = eid0;
+      tl.src = src;
+      tl.payload = payload;
+      tl.tag = tag;
+      tl.count = n;
+      tl_open = true;
+      cq_nr++;
     }
-    CodelEnt e;
-    e.enqueue_ts = now;
-    e.eid = ev.eid;
-    e.src = ev.src;
-    e.payload = ev.payload;
-    e.tag = ev.tag;
-    e.pad = 0;
-    *cq_slot(cq_len) = e;
-    cq_len++;
-    cq_bytes += (uint64_t)ev.payload + SGN_UDP_HEADER_BYTES;
+    cq_len += n;
+    cq_bytes += (uint64_t)n * ((uint64_t)payload + SGN_UDP_HEADER_BYTES);
     if (cq_len > c_maxcodel) c_maxcodel = cq_len;
   }
   // process_standing_delay (:231-262)
@@ -410,25 +435,31 @@ struct HostExec {
     cq_ie = emu_sat_add(now, CODEL_INTERVAL);
     return false;
   }
+  // the head run into registers (queue not empty)
+  __device__ __forceinline__ void load_head() {
+    if (hd_valid) return;
+    if (tl_open && cq_nr == 1) {  // the only run is the open tail: take it over
+      hd = tl;
+      tl_open = false;
+    } else {
+      hd = *cq_slot(0);
+    }
+    hd_valid = true;
+  }
   // codel_pop (:204-227)
   __device__ bool codel_pop_raw(Pkt* p, bool* ok_to_drop) {
     if (cq_len == 0) {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    if (cqc_n == 0) {
-      // refill the head window: up to four independent ring loads in flight at once
-      cqc_n = min(4u, cq_len);
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++)
-        if (j < cqc_n) cqc[j] = *cq_slot(j);
+    load_head();
+    const CodelEnt e = hd;
+    hd.eid++;
+    if (--hd.count == 0) {
+      hd_valid = false;
+      cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
+      cq_nr--;
     }
-    const CodelEnt e = cqc[0];
-    cqc[0] = cqc[1];
-    cqc[1] = cqc[2];
-    cqc[2] = cqc[3];
-    cqc_n--;
-    cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
     cq_len--;
     cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + SGN_UDP_HEADER_BYTES);
     *ok_to_drop = codel_standing(sat_sub(now, e.enqueue_ts));
@@ -543,84 +574,6 @@ struct HostExec {
     }
   }
 
-  // push_packet_to_host (core/worker.rs:603-613) into the calendar / exchange slot
-  __device__ void emit(uint32_t dst, uint64_t t, uint32_t payload, uint32_t tag, uint64_t e) {
-    EvRec r;
-    r.time = t;
-    r.eid = e;
-    r.src = gid;
-    r.dst = dst;
-    r.payload = payload;
-    r.tag = tag;
-    if (dst - S.lo < S.nH) {
-      uint32_t b = bucket_of(S, t);
-      uint32_t pos;
-      uint64_t base;
-      if (b == b1) {
-        pos = atomicAdd(&C->keep_n, 1u);
-        base = b1_keep_base;
-        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)t);
-      } else {
-        pos = atomicAdd(&S.bucket_n[b], 1u);
-        base = S.bucket_base[b];
-        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)t);
-      }
-      if (pos >= S.BC) {
-        overflow(OVF_BUCKET);
-        return;
-      }
-      S.pool[base + pos] = r;
-    } else {
-      // owner rank of dst: contiguous ranges
-      uint32_t lo = 0, hi = S.n_ranks;
-      while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
-      }
-      uint32_t pos = atomicAdd(&S.xout_n[lo], 1u);
-      if (pos >= S.xslot) {
-        overflow(OVF_EXCHANGE);
-        return;
-      }
-      S.xout[(size_t)lo * S.xslot + pos] = r;
-    }
-  }
-
-  // ---- Worker::send_packet (core/worker.rs:330-403) ----
-  __device__ void send_packet(const Pkt& p) {
-    if (now >= S.end_time) return;  // is_completed: no draw, nothing recorded
-    const bool boot = now < S.boot_end;
-    uint32_t dst;
-    if (!dns_lookup(p.dst_ip, &dst)) {  // InetDropped, no draw (:347-357)
-      c_unknown++;
-      dtx = sgn_digest3(dtx, now, 0xFFFFFFFFULL | (2ULL << 32), 0);
-      trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
-      return;
-    }
-    const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
-    const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);  // :532-537 (f32), widened :363-365
-    const double reliability = (double)rel32;
-    const double chance = rng_f64();                   // :366
-    if (!boot && chance >= reliability && p.payload > 0) {  // :371
-      c_loss++;
-      dtx = sgn_digest3(dtx, now, (uint64_t)dst | (1ULL << 32), 0);
-      trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
-      return;
-    }
-    const uint64_t delay = S.rlat[ri];  // :376
-    if (S.dynamic && delay < lat_cache) {  // update_lowest_used_latency (:297-308)
-      lat_cache = delay;
-      atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
-    }
-    uint64_t deliver = now + delay;  // :387-390
-    if (deliver < we) deliver = we;
-    const uint64_t e = eid++;  // Event::new_packet: the SOURCE host's counter (event.rs:27)
-    c_sent++;
-    dtx = sgn_digest3(dtx, now, (uint64_t)dst, deliver);
-    trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
-    emit(dst, deliver, p.payload, p.tag, e);
-  }
-
   // interface delivery to the synthetic app (NetworkInterface::push -> socket)
   __device__ void deliver_to_app(const Pkt& p, bool local) {
     if (local) {
@@ -644,61 +597,97 @@ struct HostExec {
     }
   }
 
-  // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) ----
-  template <int W>
-  __device__ bool forward_until_blocked(uint64_t* dur) {
+  // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) for relay_inet_in:
+  //      the router's CoDel queue -> the interface (relay_inet_out uses forward_out) ----
+  __device__ bool forward_in(uint64_t* dur) {
     const bool boot = now < S.boot_end;
-    set_relay_state<W>(RELAY_FORWARDING);
-    const uint32_t src_addr = W == 0 ? my_ip : 0u;  // eth0 / router (0.0.0.0)
+    set_relay_state<1>(RELAY_FORWARDING);
     while (true) {
       Pkt p;
-      const uint32_t next_bit = W == 0 ? F_RO_NEXT : F_RI_NEXT;
-      if (fl & next_bit) {
-        fl &= ~next_bit;
-        if (W == 0) {
-          p.src = gid;
-          p.dst_ip = ro_dst;
-          p.payload = ro_pay;
-          p.tag = ro_tag;
-          p.eid = 0;
-        } else {
-          p.src = ri_src;
-          p.dst_ip = my_ip;
-          p.payload = ri_pay;
-          p.tag = ri_tag;
-          p.eid = ri_eid;
-        }
+      if (fl & F_RI_NEXT) {
+        fl &= ~F_RI_NEXT;
+        p.src = ri_src;
+        p.dst_ip = my_ip;
+        p.payload = ri_pay;
+        p.tag = ri_tag;
+        p.eid = ri_eid;
       } else {
-        bool got = W == 0 ? fifo_pop(&p) : codel_pop(&p);
-        if (!got) {
-          set_relay_state<W>(RELAY_IDLE);
+        if (cq_len > 0) {
+          load_head();
+          if (sat_sub(now, hd.enqueue_ts) < CODEL_TARGET) {
+            // Fast path over the head run: every packet of it has the same standing delay
+            // (< TARGET: CoDelQueue::pop returns it, clearing interval_end and drop mode,
+            // codel_queue.rs:204-262) and wire size, and all removals happen at the same
+            // `now`, so after the first comforming_remove (which applies the lazy refill)
+            // balance / wire more packets conform; the first that does not is cached.
+            const uint32_t n = hd.count;
+            const uint64_t wire = (uint64_t)hd.payload + SGN_UDP_HEADER_BYTES;
+            uint32_t m = n;
+            bool blocked = false;
+            if (!boot) {
+              if (!tb_remove<1>(wire, dur)) {
+                m = 0;
+                blocked = true;
+              } else if (n > 1) {
+                const uint64_t more = tbb1 / wire;
+                if (more >= n - 1) {
+                  tbb1 -= (uint64_t)(n - 1) * wire;
+                } else {
+                  tbb1 -= more * wire;
+                  m = 1 + (uint32_t)more;
+                  blocked = true;
+                  tb_remove<1>(wire, dur);  // fails: same `now`, gives the conforming duration
+                }
+              }
+            }
+            fl &= ~(F_CODEL_IE | F_CODEL_DROP);
+            const uint32_t used = m + (blocked ? 1u : 0u);
+            const CodelEnt r = hd;
+            hd.eid += used;
+            hd.count -= used;
+            cq_len -= used;
+            cq_bytes = sat_sub(cq_bytes, (uint64_t)used * wire);
+            if (hd.count == 0) {
+              hd_valid = false;
+              cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
+              cq_nr--;
+            }
+            p.src = r.src;
+            p.dst_ip = my_ip;
+            p.payload = r.payload;
+            p.tag = r.tag;
+            for (uint32_t k = 0; k < m; k++) {
+              p.eid = r.eid + k;
+              deliver_to_app(p, false);
+            }
+            if (blocked) {
+              fl |= F_RI_NEXT;
+              ri_src = r.src;
+              ri_pay = r.payload;
+              ri_tag = r.tag;
+              ri_eid = r.eid + m;
+              set_relay_state<1>(RELAY_IDLE);
+              return true;
+            }
+            continue;
+          }
+        }
+        if (!codel_pop(&p)) {
+          set_relay_state<1>(RELAY_IDLE);
           return false;
         }
       }
-      const bool is_local = src_addr == p.dst_ip;
-      if (!boot && !is_local) {
-        if (!tb_remove<W>((uint64_t)p.payload + SGN_UDP_HEADER_BYTES, dur)) {
-          fl |= next_bit;
-          if (W == 0) {
-            ro_dst = p.dst_ip;
-            ro_pay = p.payload;
-            ro_tag = p.tag;
-          } else {
-            ri_src = p.src;
-            ri_pay = p.payload;
-            ri_tag = p.tag;
-            ri_eid = p.eid;
-          }
-          set_relay_state<W>(RELAY_IDLE);
-          return true;
-        }
+      // the source address is the router's (0.0.0.0), never this host's: no local bypass
+      if (!boot && !tb_remove<1>((uint64_t)p.payload + SGN_UDP_HEADER_BYTES, dur)) {
+        fl |= F_RI_NEXT;
+        ri_src = p.src;
+        ri_pay = p.payload;
+        ri_tag = p.tag;
+        ri_eid = p.eid;
+        set_relay_state<1>(RELAY_IDLE);
+        return true;
       }
-      if (is_local)
-        deliver_to_app(p, true);
-      else if (W == 0)
-        send_packet(p);  // Router::push -> route_outgoing_packet (router/mod.rs:48-73)
-      else
-        deliver_to_app(p, false);
+      deliver_to_app(p, false);
     }
   }
 
@@ -741,6 +730,9 @@ struct HostExec {
     const uint32_t nsent = (uint32_t)(eid - eid0);
     if (nsent == 0) return;
     c_sent += nsent;
+    // sent packets have consecutive ids (drops take none): one event run record each
+    // RUN_MAX packets
+    const uint32_t nrec = (nsent + RUN_MAX - 1) / RUN_MAX;
     if (S.dynamic && delay < lat_cache) {
       lat_cache = delay;
       atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
@@ -753,11 +745,11 @@ struct HostExec {
       const uint32_t b = bucket_of(S, deliver);
       uint64_t base;
       if (b == b1) {
-        pos = atomicAdd(&C->keep_n, nsent);
+        pos = atomicAdd(&C->keep_n, nrec);
         base = b1_keep_base;
         atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)deliver);
       } else {
-        pos = atomicAdd(&S.bucket_n[b], nsent);
+        pos = atomicAdd(&S.bucket_n[b], nrec);
         base = S.bucket_base[b];
         atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)deliver);
       }
@@ -769,21 +761,22 @@ struct HostExec {
         const uint32_t mid = (lo + hi) >> 1;
         if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
       }
-      pos = atomicAdd(&S.xout_n[lo], nsent);
+      pos = atomicAdd(&S.xout_n[lo], nrec);
       dstp = S.xout + (size_t)lo * S.xslot;
       cap = S.xslot;
     }
-    if (pos + nsent > cap) {
+    if (pos + nrec > cap) {
       overflow(owned ? OVF_BUCKET : OVF_EXCHANGE);
       return;
     }
-    for (uint32_t m = 0; m < nsent; m++) {
+    for (uint32_t m = 0; m < nrec; m++) {
+      const uint32_t k = min(RUN_MAX, nsent - m * RUN_MAX);
       EvRec r;
       r.time = deliver;
-      r.eid = eid0 + m;
+      r.eid = eid0 + (uint64_t)m * RUN_MAX;
       r.src = gid;
       r.dst = dst;
-      r.payload = payload;
+      r.pc = payload | (k << 16);
       r.tag = tag;
       dstp[pos + m] = r;
     }
@@ -880,7 +873,7 @@ struct HostExec {
   __device__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
     uint64_t dur;
-    const bool blocked = W == 0 ? forward_out(&dur) : forward_until_blocked<W>(&dur);
+    const bool blocked = W == 0 ? forward_out(&dur) : forward_in(&dur);
     if (blocked) forward_later<W>(dur);
   }
 
@@ -948,10 +941,17 @@ struct HostExec {
             const EvRec& ev = buf[j];
             pi++;
             now = ev.time;
-            c_popped++;
-            drx = sgn_digest3(drx, ev.time, ev.src, ev.eid);
-            trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid);
-            codel_push(ev);     // Router::route_incoming_packet (router/mod.rs:55-57)
+            // the run's packets pop back to back (nothing sorts between them); each is
+            // routed into CoDel and notifies relay_inet_in, which schedules its task on
+            // the first notification only (Relay::notify, relay/mod.rs:111-136)
+            const uint32_t n = ev_count(ev);
+            c_popped += n;
+            for (uint32_t k = 0; k < n; k++) {
+              drx = sgn_digest3(drx, ev.time, ev.src, ev.eid + k);
+              trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid + k);
+            }
+            // Router::route_incoming_packet (router/mod.rs:55-57)
+            codel_push_run(ev.src, ev.eid, ev_payload(ev), ev.tag, n);
             relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
           }
 #ifdef SGN_PHASES
@@ -1139,25 +1139,28 @@ __global__ __launch_bounds__(256) void k_segsort_small(DevSim S) {
   uint32_t s0, s1;
   seg_bounds(S, w, &s0, &s1);
   const uint32_t k = s1 - s0;
-  if (k <= 1) return;
-  if (k >= HEAVY_T && lane == 0) {
-    // long segments run on dedicated waves of k_execute, dispatched first and packed with
-    // hosts of the same kind so their (longest) event loops stay convergent
+  if (k == 0) return;
+  EvRec r;
+  r.time = ~0ULL;
+  r.src = ~0u;
+  r.eid = ~0ULL;
+  r.pc = 0;
+  if (k <= 64 && (uint32_t)lane < k) r = S.seg[s0 + lane];
+  const uint32_t packets = k <= 64 ? wave_sum_u32(ev_count(r)) : ~0u;
+  if ((k >= HEAVY_T || packets >= HEAVY_P) && lane == 0) {
+    // hosts with many due packets run on dedicated waves of k_execute (one host each),
+    // dispatched first: their event loops are the round's critical path
     const uint32_t pos = atomicAdd(&C->heavy_n, 1u);
     if (pos < S.heavy_cap) {
       S.heavy_list[pos] = w;
       S.heavy_tag[w] = (uint32_t)C->rounds + 1;
     }
   }
+  if (k == 1) return;
   if (k > 64) {
     if (lane == 0) S.big_list[atomicAdd(&C->big_n, 1u)] = w;
     return;
   }
-  EvRec r;
-  r.time = ~0ULL;
-  r.src = ~0u;
-  r.eid = ~0ULL;
-  if ((uint32_t)lane < k) r = S.seg[s0 + lane];
   uint32_t rank = 0;
   for (uint32_t j = 0; j < k; j++) {
     const uint64_t tj = shfl64(r.time, j);
@@ -1262,6 +1265,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   uint32_t n_ev = 0;  // diagnostic: events this lane handled (stamps build only)
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
 #ifdef SGN_PHASES
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
   uint64_t dph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t dpn[4] = {0, 0, 0, 0};
   uint32_t dcnt[4] = {0, 0, 0, 0};
@@ -1328,6 +1332,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       st[12] = dpn[2] | ((uint64_t)dpn[3] << 32);
       st[13] = dcnt[0] | ((uint64_t)dcnt[1] << 32);
       st[14] = dcnt[2] | ((uint64_t)dcnt[3] << 32);
+      st[15] = __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz
 #endif
     }
   }
@@ -1849,6 +1854,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.ri_eid = dalloc<uint64_t>(ctx, nH);
   S.codel = dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
   S.cq_head = dalloc<uint32_t>(ctx, nH);
+  S.cq_nr = dalloc<uint32_t>(ctx, nH);
   S.cq_len = dalloc<uint32_t>(ctx, nH);
   S.cq_bytes = dalloc<uint64_t>(ctx, nH);
   S.cq_ie = dalloc<uint64_t>(ctx, nH);
@@ -1861,7 +1867,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.cnt = dalloc<uint64_t>(ctx, (size_t)NCNT * nH);
   S.trace_seq = dalloc<uint64_t>(ctx, nH);
   if (!S.ro_dst || !S.ro_pay || !S.ro_tag || !S.ri_src || !S.ri_pay || !S.ri_tag || !S.ri_eid ||
-      !S.codel || !S.cq_head || !S.cq_len || !S.cq_bytes || !S.cq_ie || !S.cq_dn || !S.cq_cur ||
+      !S.codel || !S.cq_head || !S.cq_nr || !S.cq_len || !S.cq_bytes || !S.cq_ie || !S.cq_dn || !S.cq_cur ||
       !S.cq_prev || !S.fifo || !S.fq_head || !S.fq_len || !S.cnt || !S.trace_seq)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
 

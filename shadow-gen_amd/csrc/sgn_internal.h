@@ -25,25 +25,35 @@ constexpr uint64_t SIM_START = SGN_SIMULATION_START;
 constexpr uint64_t EMU_MAX = SGN_EMUTIME_MAX;
 constexpr uint64_t INVALID = SGN_EMUTIME_INVALID;
 
-// One in-flight packet event (core/work/event.rs:20-31 + the packet fields the core needs).
+// A run of in-flight packet events (core/work/event.rs:20-31 + the packet fields the core
+// needs): `count` packets from one source to one destination with the same delivery time,
+// payload and tag and CONSECUTIVE source event ids eid, eid+1, ... Shadow queues each of
+// them as its own Event; a run is only a compact encoding of events that are adjacent in
+// Shadow's order anyway (same time and source, consecutive ids: nothing sorts between
+// them), so popping a run = popping its packets one by one. A single packet is a run of 1.
 struct __attribute__((aligned(16))) EvRec {
   uint64_t time;     // delivery time (EmulatedTime)
-  uint64_t eid;      // source host's event id
+  uint64_t eid;      // source host's event id of the first packet
   uint32_t src;      // source HostId
   uint32_t dst;      // destination HostId
-  uint32_t payload;  // UDP payload bytes (wire = payload + 28)
+  uint32_t pc;       // UDP payload bytes (low 16; wire = payload + 28) | packets (high 16, >= 1)
   uint32_t tag;      // opaque app tag
 };
 static_assert(sizeof(EvRec) == 32, "EvRec is two 16-byte halves");
+__host__ __device__ __forceinline__ uint32_t ev_payload(const EvRec& e) { return e.pc & 0xFFFFu; }
+__host__ __device__ __forceinline__ uint32_t ev_count(const EvRec& e) { return e.pc >> 16; }
+constexpr uint32_t RUN_MAX = 0xFFFFu;  // packets per event run
 
-// One entry of the inbound CoDel ring (router/codel_queue.rs:51-54).
+// A run of entries of the inbound CoDel queue (router/codel_queue.rs:51-54): `count`
+// packets enqueued at the same time from one source with consecutive event ids and the
+// same payload and tag (the same encoding as EvRec; CoDel still handles them one by one).
 struct __attribute__((aligned(16))) CodelEnt {
   uint64_t enqueue_ts;
-  uint64_t eid;
+  uint64_t eid;      // first packet's source event id
   uint32_t src;
   uint32_t payload;
   uint32_t tag;
-  uint32_t pad;
+  uint32_t count;    // packets in the run (>= 1)
 };
 static_assert(sizeof(CodelEnt) == 32, "");
 
@@ -157,8 +167,8 @@ struct DevSim {
   uint32_t *ri_src, *ri_pay, *ri_tag;
   uint64_t* ri_eid;
   uint64_t *tb_bal, *tb_last, *tb_cap, *tb_inc;  // [2 * nH]: 0 = inet_out, 1 = inet_in
-  CodelEnt* codel;
-  uint32_t *cq_head, *cq_len;
+  CodelEnt* codel;       // [nH * codel_cap] run ring per host
+  uint32_t *cq_head, *cq_nr, *cq_len;  // head run slot, runs, packets
   uint64_t *cq_bytes, *cq_ie, *cq_dn, *cq_cur, *cq_prev;
   FifoEnt* fifo;
   uint32_t *fq_head, *fq_len;
@@ -204,7 +214,8 @@ struct DevSim {
 constexpr int SCAN_BLOCKS = 256;
 constexpr int SORT_BLOCKS = 128;   // workgroups of the block-level segment sort
 constexpr int SORT_MAX = 4096;     // longest segment the block sort holds in LDS
-constexpr uint32_t HEAVY_T = 16;   // due events that make a host "heavy" for one round
+constexpr uint32_t HEAVY_T = 16;   // due event runs that make a host "heavy" for one round
+constexpr uint32_t HEAVY_P = 48;   // ... or due packets
 
 }  // namespace sgn
 

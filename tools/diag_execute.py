@@ -34,10 +34,10 @@ for r in range(3):
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} max_lane={mx[i]:4d} busy_lanes={busy[i]:2d}"
               f"  cyc/event={cyc[i] / max(ev[i], 1):7.1f}")
         p = s[i, 4:11]
-        n = [s[i, 11] & 0xFFFFFFFF, s[i, 11] >> 32, s[i, 12] & 0xFFFFFFFF, s[i, 12] >> 32]
+        pn = [s[i, 11] & 0xFFFFFFFF, s[i, 11] >> 32, s[i, 12] & 0xFFFFFFFF, s[i, 12] >> 32]
         c = [s[i, 13] & 0xFFFFFFFF, s[i, 13] >> 32, s[i, 14] & 0xFFFFFFFF, s[i, 14] >> 32]
-        print(f"      lane0: pop {p[0]}c/{n[0]} chunks, ro {p[1]}c/{n[1]}, ri {p[2]}c/{n[2]}, app {p[3]}c/{n[3]}"
-              f" | load {p[4]} run {p[6]} store {p[5]} | popped {c[0]} sends {c[1]} deliv {c[2]} codel {c[3]}")
+        print(f"      lane0: pop {p[0]}c/{pn[0]} chunks, ro {p[1]}c/{pn[1]}, ri {p[2]}c/{pn[2]}, app {p[3]}c/{pn[3]}"
+              f" | load {p[4]} run {p[6]} store {p[5]} | {s[i, 15] * 10} ns | popped {c[0]} sends {c[1]} deliv {c[2]} codel {c[3]}")
     sel = ev > 0
     A = np.stack([ev[sel], mx[sel], np.ones(sel.sum())], 1)
     coef, *_ = np.linalg.lstsq(A, cyc[sel], rcond=None)
