@@ -216,6 +216,9 @@ typedef struct sgn_stats {
   uint64_t max_codel_len;      /* high-water mark of any CoDel ring (capacity planning) */
   uint64_t max_pending_events; /* high-water mark of in-flight packet events */
   uint64_t host_executions;    /* sum over rounds of hosts that had an event due */
+  uint64_t sched_heavy_hosts;  /* sum over rounds of hosts run on a wave of their own */
+  uint64_t sched_sorted_segments; /* sum over rounds of per-host segments that needed sorting */
+  uint64_t event_runs;         /* due event runs (records) processed; <= packet_events_popped */
 } sgn_stats;
 int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out);
 
@@ -327,7 +330,7 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out);
  * events handled, max events of one host, hosts with events, then (diagnostic build
  * libsgn_diag.so only) lane 0's per-event-kind cycles and counts}. Needs SGN_STAMPS=1 in
  * the environment at sgn_sim_init; n = number of waves (0 when disabled), cap in waves. */
-#define SGN_STAMP_WORDS 16
+#define SGN_STAMP_WORDS 32
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n);
 
 #ifdef __cplusplus

@@ -117,8 +117,8 @@ struct HostExec {
   const DevSim& S;
   Ctrl* C;
   uint32_t h, gid, my_ip, my_unode;
-  uint64_t now, we, b1_keep_base;
-  uint32_t b1;
+  uint64_t now, we;
+  uint32_t b1, keep_slab;  // the window's last bucket (its new events go to the spare slab)
   // RNG (host/host.rs:234) and counters (host.rs:259-263)
   uint64_t r0, r1, r2, r3;
   uint64_t eid, app_k;
@@ -142,14 +142,12 @@ struct HostExec {
   // registers; their ring slots are stale until store() (or until the tail is closed).
   CodelEnt hd, tl;
   bool hd_valid, tl_open;
-#ifdef SGN_PHASES
-  // diagnostic build only (libsgn_diag.so): shader cycles and counts per event kind
-  uint64_t ph[4];
-  uint32_t pn[4];
-#endif
 
-  __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint64_t kb)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1_keep_base(kb), b1(bucket1) {
+  __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks) {}
+
+  // the host's state into registers (once per round, only for hosts with something due)
+  __device__ void load() {
     const uint32_t nH = S.nH;
     gid = S.lo + h;
     my_ip = S.ip[gid];
@@ -197,9 +195,6 @@ struct HostExec {
     tseq = S.trace_on ? S.trace_seq[h] : 0;
     lat_cache = INVALID;
     hd_valid = tl_open = false;
-#ifdef SGN_PHASES
-    for (int i = 0; i < 4; i++) ph[i] = 0, pn[i] = 0;
-#endif
   }
 
   __device__ void store() {
@@ -743,18 +738,13 @@ struct HostExec {
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
       const uint32_t b = bucket_of(S, deliver);
-      uint64_t base;
-      if (b == b1) {
-        pos = atomicAdd(&C->keep_n, nrec);
-        base = b1_keep_base;
-        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)deliver);
-      } else {
-        pos = atomicAdd(&S.bucket_n[b], nrec);
-        base = S.bucket_base[b];
-        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)deliver);
-      }
-      dstp = S.pool + base;
-      cap = S.BC;
+      const uint32_t slab = b == b1 ? keep_slab : S.bucket_slab[b];
+      const size_t idx = (size_t)slab * S.G + (dst - S.lo) / GROUP;
+      pos = atomicAdd(&S.slab_n[idx], nrec);
+      atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
+                (unsigned long long)deliver);
+      dstp = S.pool + idx * S.CAP;
+      cap = S.CAP;
     } else {
       uint32_t lo = 0, hi = S.n_ranks;
       while (hi - lo > 1) {
@@ -905,10 +895,14 @@ struct HostExec {
     schedule<SLOT_APP>(now + next_delay);
   }
 
-  // ---- Host::execute (host.rs:762-830) over the ordered segment + local slots ----
-  // the segment [s0, s1) arrives ordered by (time, src host, src event id) (k_segsort_*)
-  __device__ void run(uint32_t s0, uint32_t s1) {
-    const EvRec* seg = S.seg;
+  // ---- Host::execute (host.rs:762-830) over the host's due event runs + local slots ----
+  // ev[ord[s0 .. s1)] are the host's runs due before `until` in Shadow's order, (time, src
+  // host, src event id) (core/work/event.rs:84-155), in LDS; local events run while their
+  // time < until. A window is executed as consecutive sub-windows (one per calendar
+  // bucket): nothing created inside a window is due in it (packet deliveries are >= the
+  // window end, worker.rs:386-390), so this is the same sequence of events.
+  __device__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
+                      uint64_t until) {
     uint32_t pi = s0;
     while (true) {
       // earliest local event by (time, event id)
@@ -917,56 +911,30 @@ struct HostExec {
       if (st1 < lt || (st1 == lt && se1 < le)) { lt = st1; le = se1; ls = 1; }
       if (st2 < lt || (st2 == lt && se2 < le)) { lt = st2; le = se2; ls = 2; }
       if (pi < s1) {
-        // packet events are consumed in chunks of up to four: the four segment loads
-        // are independent, so their latency overlaps instead of serialising per event
-        constexpr uint32_t K = 4;
-        EvRec buf[K];
-        const uint32_t nb = min(K, s1 - pi);
-#pragma unroll
-        for (uint32_t j = 0; j < K; j++)
-          if (j < nb) buf[j] = seg[pi + j];
-        if (buf[0].time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
-#ifdef SGN_PHASES
-          const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-#endif
-#pragma unroll
-          for (uint32_t j = 0; j < K; j++) {
-            if (j >= nb) break;
-            if (j > 0) {
-              // a pop can only (re)schedule relay_inet_in, at `now`
-              uint64_t t = st0 < st1 ? st0 : st1;
-              t = st2 < t ? st2 : t;
-              if (buf[j].time > t) break;
-            }
-            const EvRec& ev = buf[j];
-            pi++;
-            now = ev.time;
-            // the run's packets pop back to back (nothing sorts between them); each is
-            // routed into CoDel and notifies relay_inet_in, which schedules its task on
-            // the first notification only (Relay::notify, relay/mod.rs:111-136)
-            const uint32_t n = ev_count(ev);
-            c_popped += n;
-            for (uint32_t k = 0; k < n; k++) {
-              drx = sgn_digest3(drx, ev.time, ev.src, ev.eid + k);
-              trace(SGN_TRACE_POP, ev.src, 0, ev.time, 0, ev.eid + k);
-            }
-            // Router::route_incoming_packet (router/mod.rs:55-57)
-            codel_push_run(ev.src, ev.eid, ev_payload(ev), ev.tag, n);
-            relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
+        const EvRec& e = ev[ord[pi]];
+        if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+          pi++;
+          now = e.time;
+          // the run's packets pop back to back (nothing sorts between them); each is
+          // routed into CoDel and notifies relay_inet_in, which schedules its task on
+          // the first notification only (Relay::notify, relay/mod.rs:111-136)
+          const uint32_t n = ev_count(e);
+          const uint32_t src = e.src;
+          const uint64_t eid0 = e.eid;
+          c_popped += n;
+          for (uint32_t k = 0; k < n; k++) {
+            drx = sgn_digest3(drx, now, src, eid0 + k);
+            trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
           }
-#ifdef SGN_PHASES
-          ph[0] += __builtin_amdgcn_s_memtime() - pt0;
-          pn[0]++;
-#endif
+          // Router::route_incoming_packet (router/mod.rs:55-57)
+          codel_push_run(src, eid0, ev_payload(e), e.tag, n);
+          relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
           continue;
         }
       }
-      if (lt >= we) break;
+      if (lt >= until) break;
       now = lt;
       c_localev++;
-#ifdef SGN_PHASES
-      const uint64_t pt1 = __builtin_amdgcn_s_memtime();
-#endif
       if (ls == 0) {
         st0 = INVALID;
         run_forward_task<0>();
@@ -977,10 +945,6 @@ struct HostExec {
         st2 = INVALID;
         app_task();
       }
-#ifdef SGN_PHASES
-      ph[1 + ls] += __builtin_amdgcn_s_memtime() - pt1;
-      pn[1 + ls]++;
-#endif
     }
   }
 };
@@ -988,327 +952,153 @@ struct HostExec {
 // ------------------------------------------------------------------------------------
 // Round kernels
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void due_buckets(const DevSim& S, const Ctrl* C, uint32_t* b0,
-                                            uint32_t* b1, uint32_t* n0, uint32_t* n1) {
-  *b0 = bucket_of(S, C->ws);
-  *b1 = bucket_of(S, C->we - 1);
-  *n0 = S.bucket_n[*b0];
-  *n1 = *b1 != *b0 ? S.bucket_n[*b1] : 0;
-}
-
-__global__ __launch_bounds__(256) void k_count(DevSim S) {
-  const Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint64_t we = C->we;
-  uint32_t b0, b1, n0, n1;
-  due_buckets(S, C, &b0, &b1, &n0, &n1);
-  n0 = min(n0, S.BC);
-  n1 = min(n1, S.BC);
-  const uint32_t total = n0 + n1;
-  const uint64_t base0 = S.bucket_base[b0], base1 = S.bucket_base[b1];
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += gridDim.x * blockDim.x) {
-    const EvRec* e = i < n0 ? &S.pool[base0 + i] : &S.pool[base1 + (i - n0)];
-    const uint64_t t = e->time;
-    if (t < we) atomicAdd(&S.hist[e->dst - S.lo], 1u);
-  }
-}
-
-// per-block sums of hist over SCAN_BLOCKS tiles
-__global__ __launch_bounds__(256) void k_scan_reduce(DevSim S) {
-  const Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint32_t nH = S.nH;
-  const uint32_t tile = (nH + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
-  const uint32_t beg = blockIdx.x * tile;
-  const uint32_t end = min(nH, beg + tile);
-  uint32_t s = 0;
-  for (uint32_t i = beg + threadIdx.x; i < end; i += blockDim.x) s += S.hist[i];
-  __shared__ uint32_t sh[4];
-  s = wave_sum_u32(s);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) S.block_sums[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
-}
-
-__global__ __launch_bounds__(256) void k_scan_apply(DevSim S) {
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint32_t nH = S.nH;
-  const uint32_t tile = (nH + SCAN_BLOCKS - 1) / SCAN_BLOCKS;
-  const uint32_t beg = blockIdx.x * tile;
-  const uint32_t end = min(nH, beg + tile);
-  __shared__ uint32_t sh[8];
-  // prefix of earlier tiles
-  uint32_t p = 0;
-  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += blockDim.x) p += S.block_sums[i];
-  p = wave_sum_u32(p);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = p;
-  __syncthreads();
-  uint32_t carry = sh[0] + sh[1] + sh[2] + sh[3];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint32_t c0 = beg; c0 < end; c0 += blockDim.x) {
-    const uint32_t i = c0 + threadIdx.x;
-    const uint32_t v = i < end ? S.hist[i] : 0;
-    // inclusive wave scan
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      uint32_t y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) sh[w] = x;
-    __syncthreads();
-    uint32_t wpre = 0;
-    for (int k = 0; k < w; k++) wpre += sh[k];
-    const uint32_t total = sh[0] + sh[1] + sh[2] + sh[3];
-    const uint32_t excl = carry + wpre + x - v;
-    if (i < end) {
-      S.seg_start[i] = excl;
-      S.cursor[i] = excl;
-    }
-    carry += total;
-    __syncthreads();
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    // grand total (every tile's sum) closes the offsets
-    uint32_t tot = 0;
-    for (int i = 0; i < SCAN_BLOCKS; i++) tot += S.block_sums[i];
-    S.seg_start[nH] = tot;
-    if (tot > S.seg_cap) {
-      if ((atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0) C->overflow_info = tot;
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void k_scatter(DevSim S) {
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint64_t we = C->we;
-  uint32_t b0, b1, n0, n1;
-  due_buckets(S, C, &b0, &b1, &n0, &n1);
-  n0 = min(n0, S.BC);
-  n1 = min(n1, S.BC);
-  const uint32_t total = n0 + n1;
-  const uint64_t base0 = S.bucket_base[b0], base1 = S.bucket_base[b1];
-  const uint64_t keep_base = C->keep_base;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += gridDim.x * blockDim.x) {
-    const EvRec e = i < n0 ? S.pool[base0 + i] : S.pool[base1 + (i - n0)];
-    if (e.time < we) {
-      const uint32_t pos = atomicAdd(&S.cursor[e.dst - S.lo], 1u);
-      if (pos < S.seg_cap) S.seg[pos] = e;
-    } else {
-      const uint32_t pos = atomicAdd(&C->keep_n, 1u);
-      atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)e.time);
-      if (pos < S.BC)
-        S.pool[keep_base + pos] = e;
-      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-        C->overflow_info = e.dst;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Segmented sort: each host's due events into Shadow's event order, (time, src host, src
-// event id) (core/work/event.rs:84-155). Keys are unique (a source never reuses an id).
-// ------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   const uint32_t lo = __shfl((uint32_t)v, src, 64);
   const uint32_t hi = __shfl((uint32_t)(v >> 32), src, 64);
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ void seg_bounds(const DevSim& S, uint32_t h, uint32_t* s0,
-                                           uint32_t* s1) {
-  // clamp: an oversubscribed round is flagged OVF_SEG by k_scan_apply and never faults
-  *s0 = min(S.seg_start[h], S.seg_cap);
-  *s1 = min(S.seg_start[h + 1], S.seg_cap);
+// exclusive position of this lane among the lanes where m has a bit set
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  const uint32_t lane = threadIdx.x & 63;
+  return (uint32_t)__popcll(lane ? (m & ((~0ULL) >> (64 - lane))) : 0ULL);
 }
 
-// One wave per host: segments of up to 64 events are rank-sorted in registers, each lane
-// counting (via wave-wide broadcasts) how many keys precede its own. Longer segments are
-// queued for k_segsort_big.
-__global__ __launch_bounds__(256) void k_segsort_small(DevSim S) {
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (w >= S.nH) return;
-  uint32_t s0, s1;
-  seg_bounds(S, w, &s0, &s1);
-  const uint32_t k = s1 - s0;
-  if (k == 0) return;
-  EvRec r;
-  r.time = ~0ULL;
-  r.src = ~0u;
-  r.eid = ~0ULL;
-  r.pc = 0;
-  if (k <= 64 && (uint32_t)lane < k) r = S.seg[s0 + lane];
-  const uint32_t packets = k <= 64 ? wave_sum_u32(ev_count(r)) : ~0u;
-  if ((k >= HEAVY_T || packets >= HEAVY_P) && lane == 0) {
-    // hosts with many due packets run on dedicated waves of k_execute (one host each),
-    // dispatched first: their event loops are the round's critical path
-    const uint32_t pos = atomicAdd(&C->heavy_n, 1u);
-    if (pos < S.heavy_cap) {
-      S.heavy_list[pos] = w;
-      S.heavy_tag[w] = (uint32_t)C->rounds + 1;
-    }
-  }
-  if (k == 1) return;
-  if (k > 64) {
-    if (lane == 0) S.big_list[atomicAdd(&C->big_n, 1u)] = w;
-    return;
-  }
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < k; j++) {
-    const uint64_t tj = shfl64(r.time, j);
-    const uint32_t sj = __shfl(r.src, j, 64);
-    const uint64_t ej = shfl64(r.eid, j);
-    rank += (tj < r.time || (tj == r.time && (sj < r.src || (sj == r.src && ej < r.eid)))) ? 1 : 0;
-  }
-  if ((uint32_t)lane < k) S.seg[s0 + rank] = r;
-}
-
-// One workgroup per long segment: bitonic sort of an index permutation over keys held in
-// LDS, then a gather through a per-workgroup scratch slab.
-__global__ __launch_bounds__(256) void k_segsort_big(DevSim S) {
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  const uint32_t nbig = C->big_n;
-  if (blockIdx.x >= nbig) return;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint64_t* kt = (uint64_t*)smem;
-  uint64_t* ke = kt + SORT_MAX;
-  uint32_t* ks = (uint32_t*)(ke + SORT_MAX);
-  uint32_t* ix = ks + SORT_MAX;
-  EvRec* scratch = S.sort_scratch + (size_t)blockIdx.x * SORT_MAX;
-  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-    const uint32_t h = S.big_list[b];
-    uint32_t s0, s1;
-    seg_bounds(S, h, &s0, &s1);
-    const uint32_t k = s1 - s0;
-    if (k > (uint32_t)SORT_MAX) {
-      if (threadIdx.x == 0 && (atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0)
-        C->overflow_info = S.lo + h;
-      continue;
-    }
-    uint32_t P = 64;
-    while (P < k) P <<= 1;
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-      if (i < k) {
-        const EvRec& e = S.seg[s0 + i];
-        kt[i] = e.time;
-        ks[i] = e.src;
-        ke[i] = e.eid;
-      } else {
-        kt[i] = ~0ULL;
-        ks[i] = ~0u;
-        ke[i] = ~0ULL;
-      }
-      ix[i] = i;
-    }
-    __syncthreads();
-    for (uint32_t size = 2; size <= P; size <<= 1) {
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
-          const uint32_t a = 2 * stride * (i / stride) + (i % stride);
-          const uint32_t bb = a + stride;
-          const uint32_t xa = ix[a], xb = ix[bb];
-          const bool b_less = kt[xb] < kt[xa] ||
-                              (kt[xb] == kt[xa] && (ks[xb] < ks[xa] || (ks[xb] == ks[xa] && ke[xb] < ke[xa])));
-          const bool asc = (a & size) == 0;
-          if (b_less == asc) {
-            ix[a] = xb;
-            ix[bb] = xa;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) scratch[i] = S.seg[s0 + ix[i]];
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) S.seg[s0 + i] = scratch[i];
-    __syncthreads();
-  }
-}
-
+// One wave per host group (GROUP consecutive hosts), lane = host. A round is:
+//  1. gather: the group's slabs of the window's buckets are read; runs due in the window go
+//     to LDS, the last bucket's later runs move to the spare slab (Ctrl::keep_slab);
+//  2. order: counting sort of the due runs by destination lane (LDS atomics + wave scan),
+//     then a rank sort inside each destination's segment by (time, src host, src event
+//     id) — Shadow's EventQueue order (core/work/event.rs:84-155; keys are unique);
+//  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
+//     segment and local slots, emitting new runs into the calendar / exchange slots;
+//  4. the wave's minimum next local event time goes to Ctrl::round_min.
 __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
-  __shared__ uint64_t sh[4];
-  const uint64_t we = C->we;
-  const uint32_t b1 = bucket_of(S, we - 1);
-  const uint64_t keep_base = C->keep_base;
-  // Workgroups [0, heavy_blocks) each take ONE host of heavy_list (long segments) on lane 0:
-  // a heavy host's event loop is the round's critical path, so it gets a wave of its own
-  // (no divergence with other hosts) dispatched before everything else. The rest take
-  // hosts in HostId order and skip those already on a heavy wave.
-  uint32_t h;
-  bool take;
-  if (blockIdx.x < S.heavy_blocks) {
-    const uint32_t i = blockIdx.x;
-    const uint32_t n = min(C->heavy_n, S.heavy_cap);
-    take = threadIdx.x == 0 && i < n;
-    h = take ? S.heavy_list[i] : 0;
-  } else {
-    h = (blockIdx.x - S.heavy_blocks) * blockDim.x + threadIdx.x;
-    take = h < S.nH;
-    if (take) {
-      S.hist[h] = 0;
-      take = S.heavy_tag[h] != (uint32_t)C->rounds + 1;
-    }
-  }
-  uint64_t my_min = INVALID;
-  bool executed = false;
-  uint32_t n_ev = 0;  // diagnostic: events this lane handled (stamps build only)
+  __shared__ EvRec lev[LDS_CAP];
+  __shared__ uint16_t lb[LDS_CAP];  // due runs grouped by destination lane (unordered)
+  __shared__ uint16_t lc[LDS_CAP];  // ... ordered inside each destination segment
+  __shared__ uint32_t lcnt[GROUP], lstart[GROUP], lcur[GROUP];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t g = blockIdx.x;
+  const uint32_t h = g * GROUP + lane;  // local host index
+  const bool valid = h < S.nH;
+  const uint64_t ws = C->ws, we = C->we;
+  const uint32_t bs = bucket_of(S, ws), be = bucket_of(S, we - 1);
+  const uint32_t nbk = (be + S.NB - bs) % S.NB + 1;  // buckets overlapping the window
+  const uint32_t ks = C->keep_slab;
+  const uint32_t gbase = S.lo + g * GROUP;  // HostId of lane 0
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
-#ifdef SGN_PHASES
-  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t dph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t dpn[4] = {0, 0, 0, 0};
-  uint32_t dcnt[4] = {0, 0, 0, 0};
-#endif
-  if (take) {
-    uint32_t s0, s1;
-    seg_bounds(S, h, &s0, &s1);
+  const size_t ik = (size_t)ks * S.G + g;
+  EvRec* pk = S.pool + ik * S.CAP;
+
+  uint64_t lmin = INVALID;
+  if (valid) {
     const uint32_t nH = S.nH;
     const uint64_t t0 = S.slot_t[h], t1 = S.slot_t[nH + h], t2 = S.slot_t[2 * nH + h];
-    uint64_t lmin = t0 < t1 ? t0 : t1;
+    lmin = t0 < t1 ? t0 : t1;
     lmin = t2 < lmin ? t2 : lmin;
-    if (s0 == s1 && lmin >= we) {
-      my_min = lmin;  // nothing due: the host sleeps through this window
-    } else {
-#ifdef SGN_PHASES
-      const uint64_t q0 = __builtin_amdgcn_s_memtime();
-#endif
-      HostExec ex(S, h, we, b1, keep_base);
-#ifdef SGN_PHASES
-      const uint64_t q1 = __builtin_amdgcn_s_memtime();
-#endif
-      ex.run(s0, s1);
-      my_min = ex.next_local_time();
-#ifdef SGN_PHASES
-      const uint64_t q2 = __builtin_amdgcn_s_memtime();
-#endif
-      ex.store();
-      executed = true;
-#ifdef SGN_PHASES
-      const uint64_t q3 = __builtin_amdgcn_s_memtime();
-      for (int i = 0; i < 4; i++) dph[i] = ex.ph[i], dpn[i] = ex.pn[i];
-      dph[4] = q1 - q0;
-      dph[5] = q3 - q2;
-      dph[6] = q2 - q1;
-      dcnt[0] = ex.c_popped;
-      dcnt[1] = ex.c_sent + ex.c_loss + ex.c_unknown;
-      dcnt[2] = ex.c_deliv;
-      dcnt[3] = ex.c_codel;
-#endif
-      n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_unknown + ex.c_deliv + ex.c_localev +
-             ex.c_codel;
-    }
   }
+  HostExec ex(S, h, we, be, ks);
+  bool loaded = false;
+  uint32_t N_all = 0, sorted = 0;
+  uint64_t kmin = INVALID;
+
+  for (uint32_t bi = 0; bi < nbk; bi++) {
+    const uint32_t b = (bs + bi) % S.NB;
+    const bool last = bi == nbk - 1;
+    const uint64_t sub_end = last ? we : SIM_START + ((ws - SIM_START) / S.BW + bi + 1) * S.BW;
+    // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
+    //      runs at >= we, which join this round's new runs for it in the spare slab) ----
+    const size_t ib = (size_t)S.bucket_slab[b] * S.G + g;
+    const uint32_t n = min(S.slab_n[ib], S.CAP);
+    const EvRec* pb = S.pool + ib * S.CAP;
+    lcnt[lane] = 0;
+    uint32_t N = 0;
+    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      EvRec r;
+      if (j < n) r = pb[j];
+      const bool due = j < n && (!last || r.time < we);
+      const bool keep = j < n && !due;
+      const uint64_t dm = __ballot(due), km = __ballot(keep);
+      if (due) lev[N + lanes_below(dm)] = r;
+      N += (uint32_t)__popcll(dm);
+      if (km) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&S.slab_n[ik], (uint32_t)__popcll(km));
+        base = __shfl(base, 0, 64) + lanes_below(km);
+        if (keep) {
+          if (base < S.CAP)
+            pk[base] = r;
+          else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+            C->overflow_info = r.dst;
+          kmin = r.time < kmin ? r.time : kmin;
+        }
+      }
+    }
+    if (lane == 0) {
+      S.slab_n[ib] = 0;  // consumed (or moved); nobody appends to it this round
+      if (n > C->max_bucket) atomicMax((unsigned long long*)&C->max_bucket, (unsigned long long)n);
+    }
+    N_all += N;
+    __syncthreads();
+    // ---- 2. order: counting sort by destination lane, then rank sort by Shadow's key ----
+    for (uint32_t j = lane; j < N; j += 64) atomicAdd(&lcnt[lev[j].dst - gbase], 1u);
+    __syncthreads();
+    const uint32_t cnt = lcnt[lane];
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, 64);
+      if ((int)lane >= off) incl += y;
+    }
+    const uint32_t start = incl - cnt;
+    lstart[lane] = start;
+    lcur[lane] = start;
+    __syncthreads();
+    for (uint32_t j = lane; j < N; j += 64) {
+      const uint32_t pos = atomicAdd(&lcur[lev[j].dst - gbase], 1u);
+      lb[pos] = (uint16_t)j;
+    }
+    __syncthreads();
+    for (uint32_t q = lane; q < N; q += 64) {
+      const uint32_t idx = lb[q];
+      const EvRec& r = lev[idx];
+      const uint32_t d = r.dst - gbase;
+      const uint32_t a = lstart[d], k = lcnt[d];
+      uint32_t rank = 0;
+      for (uint32_t t = a; k > 1 && t < a + k; t++) {
+        const EvRec& o = lev[lb[t]];
+        rank += (o.time < r.time ||
+                 (o.time == r.time && (o.src < r.src || (o.src == r.src && o.eid < r.eid))))
+                    ? 1u : 0u;
+      }
+      lc[a + rank] = (uint16_t)idx;
+    }
+    sorted += cnt > 1 ? 1u : 0u;
+    __syncthreads();
+    // ---- 3. execute the sub-window [.., sub_end) ----
+    if (valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end)) {
+      if (!loaded) {
+        ex.load();
+        loaded = true;
+      }
+      ex.run(lev, lc, start, start + cnt, sub_end);
+    }
+    __syncthreads();  // LDS is reused by the next bucket
+  }
+
+  uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
+  uint32_t n_ev = 0;
+  if (loaded) {
+    my_min = ex.next_local_time();
+    ex.store();
+    n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_unknown + ex.c_deliv + ex.c_localev +
+           ex.c_codel;
+  }
+  kmin = wave_min_u64(kmin);
   if (S.stamps) {
     // per-wave diagnostics: shader cycles, total and max events over the wave's lanes
     const uint64_t clk1 = __builtin_amdgcn_s_memtime();
@@ -1319,30 +1109,27 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       mx = o > mx ? o : mx;
     }
     const uint32_t busy = __popcll(__ballot(n_ev > 0));
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) {
       uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)blockIdx.x;
       st[0] = clk1 - clk0;
       st[1] = sum;
       st[2] = mx;
       st[3] = busy;
-#ifdef SGN_PHASES
-      // lane 0's breakdown: pop chunks, relay_out / relay_in / app tasks, load, store, run
-      for (int i = 0; i < 7; i++) st[4 + i] = dph[i];
-      st[11] = dpn[0] | ((uint64_t)dpn[1] << 32);
-      st[12] = dpn[2] | ((uint64_t)dpn[3] << 32);
-      st[13] = dcnt[0] | ((uint64_t)dcnt[1] << 32);
-      st[14] = dcnt[2] | ((uint64_t)dcnt[3] << 32);
-      st[15] = __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz
-#endif
+      st[4] = N_all;
     }
   }
-  // hosts that ran this round (roofline accounting: their state made a round trip)
-  const uint64_t ex_mask = __ballot(executed);
-  if ((threadIdx.x & 63) == 0 && ex_mask)
-    atomicAdd((unsigned long long*)&C->exec_hosts, (unsigned long long)__popcll(ex_mask));
-  const uint64_t m = block_min_u64(my_min, sh);
-  if (threadIdx.x == 0 && m != INVALID)
-    atomicMin((unsigned long long*)&C->round_min, (unsigned long long)m);
+  // ---- 4. hosts that ran (roofline accounting) and the group's next event ----
+  const uint64_t ex_mask = __ballot(loaded);
+  const uint32_t n_sorted = wave_sum_u32(sorted);
+  const uint64_t m = wave_min_u64(my_min);
+  if (lane == 0) {
+    if (kmin != INVALID) atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)kmin);
+    if (ex_mask)
+      atomicAdd((unsigned long long*)&C->exec_hosts, (unsigned long long)__popcll(ex_mask));
+    if (N_all) atomicAdd((unsigned long long*)&C->tot_runs, (unsigned long long)N_all);
+    if (n_sorted) atomicAdd((unsigned long long*)&C->tot_sorted, (unsigned long long)n_sorted);
+    if (m != INVALID) atomicMin((unsigned long long*)&C->round_min, (unsigned long long)m);
+  }
 }
 
 // Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
@@ -1351,55 +1138,27 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
   __shared__ uint64_t sh[16];
-  __shared__ uint32_t shb0, shb1;
   if (threadIdx.x == 0) {
     const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
-    if (b0 != b1) {
-      S.bucket_n[b0] = 0;
-      S.bucket_min[b0] = INVALID;
-    }
-    const uint64_t old = S.bucket_base[b1];
-    S.bucket_base[b1] = C->keep_base;
-    C->keep_base = old;
-    const uint32_t kn = C->keep_n;
-    S.bucket_n[b1] = kn;
+    for (uint32_t b = b0; b != b1; b = (b + 1) % S.NB) S.bucket_min[b] = INVALID;  // consumed
+    // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
+    const uint32_t old = S.bucket_slab[b1];
+    S.bucket_slab[b1] = C->keep_slab;
+    C->keep_slab = old;
     S.bucket_min[b1] = C->keep_min;
-    C->keep_n = 0;
-    C->big_n = 0;
-    C->heavy_n = 0;
     C->keep_min = INVALID;
-    shb0 = b0;
-    shb1 = b1;
   }
   __syncthreads();
   uint64_t m = INVALID;
-  uint32_t mx = 0;
   for (uint32_t b = threadIdx.x; b < S.NB; b += blockDim.x) {
-    const uint32_t n = S.bucket_n[b];
-    if (n > 0) {
-      const uint64_t bm = S.bucket_min[b];
-      m = bm < m ? bm : m;
-    }
-    mx = n > mx ? n : mx;
+    const uint64_t bm = S.bucket_min[b];
+    m = bm < m ? bm : m;
   }
   m = wave_min_u64(m);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint32_t o = __shfl_xor(mx, off, 64);
-    mx = o > mx ? o : mx;
-  }
-  __shared__ uint32_t shx[16];
-  if ((threadIdx.x & 63) == 0) {
-    sh[threadIdx.x >> 6] = m;
-    shx[threadIdx.x >> 6] = mx;
-  }
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x >> 6); i++) {
-      m = sh[i] < m ? sh[i] : m;
-      mx = shx[i] > mx ? shx[i] : mx;
-    }
-    if (mx > C->max_bucket) C->max_bucket = mx;
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) m = sh[i] < m ? sh[i] : m;
     m = C->round_min < m ? C->round_min : m;
     C->round_min = m;  // local minimum (reduced across shards when advance == 0)
     if (advance) {
@@ -1419,8 +1178,6 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
       C->rounds++;
     }
   }
-  (void)shb0;
-  (void)shb1;
 }
 
 // Multi-shard: window advance from the all-reduced {min_next, min_used}.
@@ -1444,31 +1201,26 @@ __global__ void k_advance(DevSim S, const uint64_t* red) {
   C->rounds++;
 }
 
-// Multi-shard: file received events into the local calendar.
+// Multi-shard: file received runs into the local calendar (after k_execute, so runs for
+// the window's last bucket go to the spare slab like local sends).
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
   const uint32_t b1 = bucket_of(S, C->we - 1);
-  const uint64_t keep_base = C->keep_base;
+  const uint32_t ks = C->keep_slab;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
     const uint32_t n = min(S.xin_n[r], S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
       const EvRec e = S.xin[(size_t)r * S.xslot + i];
       const uint32_t b = bucket_of(S, e.time);
-      uint32_t pos;
-      uint64_t base;
-      if (b == b1) {
-        pos = atomicAdd(&C->keep_n, 1u);
-        base = keep_base;
-        atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)e.time);
-      } else {
-        pos = atomicAdd(&S.bucket_n[b], 1u);
-        base = S.bucket_base[b];
-        atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)e.time);
-      }
-      if (pos < S.BC)
-        S.pool[base + pos] = e;
+      const uint32_t slab = b == b1 ? ks : S.bucket_slab[b];
+      const size_t idx = (size_t)slab * S.G + (e.dst - S.lo) / GROUP;
+      const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+      atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
+                (unsigned long long)e.time);
+      if (pos < S.CAP)
+        S.pool[idx * S.CAP + pos] = e;
       else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
         C->overflow_info = e.dst;
     }
@@ -1504,12 +1256,8 @@ T* dalloc(sgn_ctx* ctx, size_t n) {
   return (T*)dev_alloc(ctx, n * sizeof(T));
 }
 
-enum { K_COUNT = 0, K_SCAN_R, K_SCAN_A, K_SCATTER, K_EXECUTE, K_FINALIZE, K_IMPORT, K_ADVANCE,
-       K_SORT_S, K_SORT_B, K_NUM };
-const char* kKernelNames[K_NUM] = {"k_count", "k_scan_reduce", "k_scan_apply", "k_scatter",
-                                   "k_execute", "k_finalize", "k_import", "k_advance",
-                                   "k_segsort_small", "k_segsort_big"};
-constexpr size_t kSortLds = (size_t)SORT_MAX * 24;
+enum { K_EXECUTE = 0, K_FINALIZE, K_IMPORT, K_ADVANCE, K_NUM };
+const char* kKernelNames[K_NUM] = {"k_execute", "k_finalize", "k_import", "k_advance"};
 
 int launch_round(sgn_ctx* ctx);
 
@@ -1521,28 +1269,8 @@ namespace {
 int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
-  const uint32_t grid_ev = 1024;
-  const uint32_t grid_h = S.heavy_blocks + (S.nH + 63) / 64;
-  time_begin(ctx, K_COUNT);
-  hipLaunchKernelGGL(k_count, dim3(grid_ev), dim3(256), 0, st, S);
-  time_end(ctx);
-  time_begin(ctx, K_SCAN_R);
-  hipLaunchKernelGGL(k_scan_reduce, dim3(SCAN_BLOCKS), dim3(256), 0, st, S);
-  time_end(ctx);
-  time_begin(ctx, K_SCAN_A);
-  hipLaunchKernelGGL(k_scan_apply, dim3(SCAN_BLOCKS), dim3(256), 0, st, S);
-  time_end(ctx);
-  time_begin(ctx, K_SCATTER);
-  hipLaunchKernelGGL(k_scatter, dim3(grid_ev), dim3(256), 0, st, S);
-  time_end(ctx);
-  time_begin(ctx, K_SORT_S);
-  hipLaunchKernelGGL(k_segsort_small, dim3((S.nH + 3) / 4), dim3(256), 0, st, S);
-  time_end(ctx);
-  time_begin(ctx, K_SORT_B);
-  hipLaunchKernelGGL(k_segsort_big, dim3(SORT_BLOCKS), dim3(256), kSortLds, st, S);
-  time_end(ctx);
   time_begin(ctx, K_EXECUTE);
-  hipLaunchKernelGGL(k_execute, dim3(grid_h), dim3(64), 0, st, S);
+  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(GROUP), 0, st, S);
   time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
@@ -1587,11 +1315,8 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
   ctx->graph_timed.clear();
   if (!all && !exec) return 0;
-  const void* fn[K_NUM] = {(const void*)k_count, (const void*)k_scan_reduce,
-                           (const void*)k_scan_apply, (const void*)k_scatter,
-                           (const void*)k_execute, (const void*)k_finalize,
-                           (const void*)k_import, (const void*)k_advance,
-                           (const void*)k_segsort_small, (const void*)k_segsort_big};
+  const void* fn[K_NUM] = {(const void*)k_execute, (const void*)k_finalize,
+                           (const void*)k_import, (const void*)k_advance};
   size_t n = 0;
   SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
   std::vector<hipGraphNode_t> nodes(n);
@@ -1872,47 +1597,28 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
 
   // ---- calendar: bucket width >= any window length, horizon > max latency ----
-  uint64_t rmax = S.dynamic ? std::max(max_lat, cfg->runahead_ns)
-                            : std::max(min_possible, cfg->runahead_ns);
-  uint64_t BW = std::max<uint64_t>(1, rmax);
+  // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least
+  // one bucket, and in dynamic mode possibly many (executed bucket by bucket).
+  uint64_t BW = std::max<uint64_t>(1, std::max(min_possible, cfg->runahead_ns));
   uint64_t NB = max_lat / BW + 4;
   if (NB > (1u << 20)) return set_error(ctx, SGN_EINVAL, "calendar would need > 2^20 buckets");
+  const uint64_t G = (nH + GROUP - 1) / GROUP;
   uint64_t cap = cfg->event_capacity ? cfg->event_capacity : (1ULL << 22);
-  uint64_t BC = cap / (NB + 1);
-  if (BC < 256) BC = 256;
-  if (BC > 0x7FFFFFFFULL) BC = 0x7FFFFFFFULL;
+  uint64_t CAP = cap / ((NB + 1) * G);
+  CAP = std::max<uint64_t>(64, std::min<uint64_t>(CAP_MAX, CAP));
   S.NB = (uint32_t)NB;
-  S.BC = (uint32_t)BC;
+  S.G = (uint32_t)G;
+  S.CAP = (uint32_t)CAP;
   S.BW = BW;
-  S.pool = dalloc<EvRec>(ctx, (NB + 1) * BC);
-  std::vector<uint64_t> bbase(NB);
-  for (uint64_t b = 0; b < NB; b++) bbase[b] = b * BC;
-  if (!S.pool) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event pool)");
-  if ((rc = up64(bbase, &S.bucket_base))) return rc;
-  S.bucket_n = dalloc<uint32_t>(ctx, NB);
+  S.pool = dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
+  S.slab_n = dalloc<uint32_t>(ctx, (NB + 1) * G);
+  if (!S.pool || !S.slab_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event calendar)");
+  std::vector<uint32_t> bslab(NB);
+  for (uint64_t b = 0; b < NB; b++) bslab[b] = (uint32_t)b;
+  if ((rc = up32(bslab, &S.bucket_slab))) return rc;
   std::vector<uint64_t> bmin(NB, INVALID);
   if ((rc = up64(bmin, &S.bucket_min))) return rc;
-  uint64_t segcap = std::min<uint64_t>(2 * BC, 0xFFFFFFF0ULL);
-  S.seg_cap = (uint32_t)segcap;
-  S.seg = dalloc<EvRec>(ctx, segcap);
-  S.hist = dalloc<uint32_t>(ctx, nH + 1);
-  S.seg_start = dalloc<uint32_t>(ctx, nH + 1);
-  S.cursor = dalloc<uint32_t>(ctx, nH + 1);
-  S.block_sums = dalloc<uint32_t>(ctx, SCAN_BLOCKS);
-  S.big_list = dalloc<uint32_t>(ctx, nH + 1);
-  S.heavy_cap = std::min<uint32_t>(2048, std::max<uint32_t>(64, nH / 128));
-  S.heavy_blocks = S.heavy_cap;
-  S.heavy_list = dalloc<uint32_t>(ctx, S.heavy_cap);
-  S.heavy_tag = dalloc<uint32_t>(ctx, nH + 1);
-  if (!S.heavy_list || !S.heavy_tag) return set_error(ctx, SGN_ENOMEM, "device allocation failed (heavy list)");
-  if (getenv("SGN_STAMPS"))
-    S.stamps = dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * ((size_t)nH / 64 + 1 + S.heavy_blocks));
-  S.sort_scratch = dalloc<EvRec>(ctx, (size_t)SORT_BLOCKS * SORT_MAX);
-  SGN_HIP(ctx, hipFuncSetAttribute((const void*)k_segsort_big,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortLds));
-  if (!S.bucket_n || !S.seg || !S.hist || !S.seg_start || !S.cursor || !S.block_sums ||
-      !S.big_list || !S.sort_scratch)
-    return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar)");
+  if (getenv("SGN_STAMPS")) S.stamps = dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
   if (ctx->trace_cap) {
     S.trace = dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
     if (!S.trace) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
@@ -1945,7 +1651,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.active = 1;
   c.round_min = INVALID;
   c.min_used = INVALID;
-  c.keep_base = NB * BC;
+  c.keep_slab = (uint32_t)NB;
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
   c.remote_min = INVALID;
@@ -2057,6 +1763,9 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   s.max_codel_len = mc;
   s.max_pending_events = ctx->h_ctrl->max_bucket;
   s.host_executions = ctx->h_ctrl->exec_hosts;
+  s.sched_heavy_hosts = 0;
+  s.sched_sorted_segments = ctx->h_ctrl->tot_sorted;
+  s.event_runs = ctx->h_ctrl->tot_runs;
   *out = s;
   return rc;
 }
@@ -2111,18 +1820,19 @@ int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
     SGN_HIP(ctx, hipMemcpy(&v, ctx->S.slot_t + (size_t)s * nH + h, 8, hipMemcpyDeviceToHost));
     m = std::min(m, v);
   }
-  // pending packet events for this host anywhere in the calendar
-  const uint64_t total = (uint64_t)(ctx->S.NB + 1) * ctx->S.BC;
-  std::vector<uint32_t> bn(ctx->S.NB);
-  std::vector<uint64_t> bb(ctx->S.NB);
-  SGN_HIP(ctx, hipMemcpy(bn.data(), ctx->S.bucket_n, bn.size() * 4, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(bb.data(), ctx->S.bucket_base, bb.size() * 8, hipMemcpyDeviceToHost));
-  (void)total;
-  for (uint32_t b = 0; b < ctx->S.NB; b++) {
-    const uint32_t n = std::min(bn[b], ctx->S.BC);
+  // pending packet events for this host: its group's slab in every bucket
+  const DevSim& S = ctx->S;
+  const uint32_t g = h / GROUP;
+  std::vector<uint32_t> bs(S.NB);
+  SGN_HIP(ctx, hipMemcpy(bs.data(), S.bucket_slab, bs.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t b = 0; b < S.NB; b++) {
+    const size_t idx = (size_t)bs[b] * S.G + g;
+    uint32_t n = 0;
+    SGN_HIP(ctx, hipMemcpy(&n, S.slab_n + idx, 4, hipMemcpyDeviceToHost));
+    n = std::min(n, S.CAP);
     if (!n) continue;
     std::vector<EvRec> ev(n);
-    SGN_HIP(ctx, hipMemcpy(ev.data(), ctx->S.pool + bb[b], n * sizeof(EvRec), hipMemcpyDeviceToHost));
+    SGN_HIP(ctx, hipMemcpy(ev.data(), S.pool + idx * S.CAP, n * sizeof(EvRec), hipMemcpyDeviceToHost));
     for (const EvRec& e : ev)
       if (e.dst == host) m = std::min(m, e.time);
   }
@@ -2161,7 +1871,7 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
 // (allocated when SGN_STAMPS=1 is set in the environment at sgn_sim_init).
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (!ctx || !ctx->sim_ready) return SGN_EINVAL;
-  const uint64_t waves = (ctx->S.nH + 63) / 64 + ctx->S.heavy_blocks;
+  const uint64_t waves = ctx->S.G;
   if (n) *n = ctx->S.stamps ? waves : 0;
   if (!ctx->S.stamps || !out) return 0;
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -74,19 +74,17 @@ struct Ctrl {
   uint64_t overflow_info;
   uint64_t round_min;     // atomicMin: next local event over owned hosts
   uint64_t min_used;      // Runahead::min_used_latency (atomicMin), INVALID = None
-  uint64_t keep_base;     // spare slab (event offset into the pool)
-  uint32_t keep_n;        // events placed in the spare slab this round
+  uint32_t keep_slab;     // spare slab: receives the window's last bucket this round
   uint32_t pad0;
-  uint64_t keep_min;
+  uint64_t keep_min;      // min time placed in the spare slab this round
   uint64_t last_min_next; // min_next_event_time of the last finished round
   uint64_t rounds;
-  uint64_t max_bucket;    // high-water mark of any bucket fill
+  uint64_t max_bucket;    // high-water mark of any (bucket, host group) slab fill
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
   uint64_t exec_hosts;    // cumulative host executions (hosts with due events per round)
-  uint32_t big_n;         // hosts whose segment needs the block-level sort this round
-  uint32_t heavy_n;       // hosts scheduled on the heavy waves of k_execute this round
-  uint64_t pad1[1];
+  uint64_t tot_runs;      // cumulative due event runs (records) handled
+  uint64_t tot_sorted;    // cumulative host segments that needed ordering (>= 2 runs)
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -143,7 +141,8 @@ struct DevSim {
   uint32_t trace_on;
   // traffic
   uint32_t tkind, payload_len, unknown_permille, req_payload;
-  uint32_t n_servers, pad0;
+  uint32_t n_servers;
+  uint32_t diag_mode;  // diagnostic build only (SGN_DIAG_MODE): 1 = light waves skip
   uint64_t flow_seed, period, period_jitter;
   uint64_t file_bytes[3];
   const uint32_t* servers;
@@ -175,27 +174,19 @@ struct DevSim {
   uint64_t *d_tx, *d_rx, *d_app;
   uint64_t* cnt;
   uint64_t* trace_seq;
-  // calendar
-  EvRec* pool;
-  uint64_t* bucket_base;
-  uint32_t* bucket_n;
-  uint64_t* bucket_min;
-  uint32_t NB, BC;
+  // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host
+  // group (GROUP consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
+  // ids are indirect (bucket_slab) so the partially consumed last bucket of a window can
+  // swap with the spare slab set (Ctrl::keep_slab) instead of being copied.
+  EvRec* pool;            // [(NB + 1) * G * CAP]
+  uint32_t* slab_n;       // [(NB + 1) * G] fill of slab (s, g)
+  uint32_t* bucket_slab;  // [NB] slab id of bucket b
+  uint64_t* bucket_min;   // [NB] earliest event in bucket b (INVALID = empty)
+  uint32_t NB, G;
+  uint32_t CAP;
+  uint32_t pad2;
   uint64_t BW;
-  // window scratch
-  uint32_t* hist;       // [nH]
-  uint32_t* seg_start;  // [nH + 1]
-  uint32_t* cursor;     // [nH]
-  uint32_t* block_sums; // [SCAN_BLOCKS]
-  uint32_t* big_list;   // [nH] hosts with segments longer than one wave
-  EvRec* sort_scratch;  // [SORT_BLOCKS * SORT_MAX]
   uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
-  uint32_t* heavy_list; // [heavy_cap] hosts with long segments this round
-  uint32_t* heavy_tag;  // [nH] round number + 1 when the host is on heavy_list
-  uint32_t heavy_cap;   // heavy waves (one host each)
-  uint32_t heavy_blocks;
-  EvRec* seg;
-  uint32_t seg_cap;
   uint32_t n_ranks;
   Ctrl* ctrl;
   // trace
@@ -211,11 +202,9 @@ struct DevSim {
   const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
 
-constexpr int SCAN_BLOCKS = 256;
-constexpr int SORT_BLOCKS = 128;   // workgroups of the block-level segment sort
-constexpr int SORT_MAX = 4096;     // longest segment the block sort holds in LDS
-constexpr uint32_t HEAVY_T = 16;   // due event runs that make a host "heavy" for one round
-constexpr uint32_t HEAVY_P = 48;   // ... or due packets
+constexpr uint32_t GROUP = 64;      // hosts per group = lanes of one k_execute wave
+constexpr uint32_t CAP_MAX = 1024;  // event runs per (bucket, group) slab
+constexpr uint32_t LDS_CAP = CAP_MAX;  // one bucket's runs of one group are ordered in LDS
 
 }  // namespace sgn
 

@@ -20,6 +20,7 @@ EMUTIME_INVALID = 0xFFFFFFFFFFFFFFFF
 EMUTIME_MAX = 0xFFFFFFFFFFFFFFFE
 TRAFFIC_PERIODIC = 1
 TRAFFIC_TGEN = 2
+STAMP_WORDS = 32  # include/sgn.h SGN_STAMP_WORDS
 CREATE_TIME_KERNELS = 1
 
 u32p = C.POINTER(C.c_uint32)
@@ -87,7 +88,8 @@ class Stats(C.Structure):
         "rounds", "packets_sent", "packets_loss_dropped", "packets_unknown_dst",
         "packet_events_popped", "codel_dropped", "delivered", "local_delivered",
         "app_blocked", "local_events", "bytes_delivered", "min_used_latency_ns",
-        "max_codel_len", "max_pending_events", "host_executions")]
+        "max_codel_len", "max_pending_events", "host_executions",
+        "sched_heavy_hosts", "sched_sorted_segments", "event_runs")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
