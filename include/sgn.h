@@ -152,7 +152,8 @@ typedef struct sgn_sim_config {
   uint32_t out_fifo_cap;        /* synthetic socket send-queue entries per host (>= 1) */
   uint32_t codel_cap;           /* device CoDel ring slots per host (reference: unlimited;
                                    exceeding it is SGN_EOVERFLOW, never a silent drop) */
-  uint32_t reserved0;
+  uint32_t hosts_per_wave;      /* hosts served by one 64-lane execute wave: a power of two
+                                   in [1, 64]; 0 = default (64). Performance only. */
   uint64_t event_capacity;      /* in-flight packet-event slots per shard (0 = auto) */
 } sgn_sim_config;
 

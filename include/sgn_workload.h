@@ -95,13 +95,63 @@ SGN_HD uint64_t sgn_digest3(uint64_t h, uint64_t a, uint64_t b, uint64_t c) {
   return h ^ (h >> 32);
 }
 
-/* What each digest covers (identical on every implementation):
- *  tx : per send_packet call past the is_completed check, (now, dst_host|outcome<<32,
- *       deliver_time_or_0), outcome 0 sent / 1 loss-dropped / 2 unknown destination
- *       (dst_host = 0xFFFFFFFF for unknown).
- *  rx : per packet event popped, (event_time, src_host, src_event_id).
+/* Run-encoded digests. Each digest is taken over the host's records in order, but a maximal
+ * run of records that differ only by a counter is folded in as ONE step (a bijective
+ * re-encoding of the same sequence: any change of a value, of the order or of a run length
+ * still changes the digest w.h.p.), so a train of n packets costs O(1) digest work:
+ *  tx : per send_packet call past the is_completed check, record (now, dst_host |
+ *       outcome << 32, deliver_time_or_0); outcome 0 sent / 1 loss-dropped / 2 unknown
+ *       destination (dst_host = 0xFFFFFFFF). A run = n identical records:
+ *       digest3(h, now, dst | outcome << 32 | n << 34, deliver_or_0).
+ *  rx : per packet event popped, (event_time, src_host, src_event_id). A run = n records
+ *       with the same time and source and consecutive ids e0, e0+1, ...:
+ *       digest3(h, time, src | n << 32, e0).
  *  app: per interface delivery (now, src_host, src_event_id) and per CoDel drop
- *       (now, src_host | 1<<63, src_event_id).                                          */
+ *       (now, src_host | 1<<63, src_event_id), runs as for rx (n in bits 32..61); a local
+ *       (loopback) delivery is a run of its own: digest3(h, now, src | 1<<62 | 1<<32,
+ *       payload).
+ * Runs never span two values of `now`; every implementation flushes its pending runs at
+ * least whenever `now` changes and at the end of each Host::execute.                     */
+typedef struct sgn_drun {
+  uint64_t a, b, c; /* run key (a, b) and c = next id (seq runs) or the common value */
+  uint32_t n;       /* records in the pending run (0 = none) */
+} sgn_drun;
+
+SGN_HD void sgn_drun_flush_seq(uint64_t* h, sgn_drun* r) {
+  if (r->n) *h = sgn_digest3(*h, r->a, r->b | ((uint64_t)r->n << 32), r->c - r->n);
+  r->n = 0;
+}
+SGN_HD void sgn_drun_flush_same(uint64_t* h, sgn_drun* r) {
+  if (r->n) *h = sgn_digest3(*h, r->a, r->b | ((uint64_t)r->n << 34), r->c);
+  r->n = 0;
+}
+/* n records (a, b, c0), (a, b, c0+1), ... (rx, app) */
+SGN_HD void sgn_drun_add_seq(uint64_t* h, sgn_drun* r, uint64_t a, uint64_t b, uint64_t c0,
+                             uint32_t n) {
+  if (r->n && r->a == a && r->b == b && r->c == c0) {
+    r->n += n;
+    r->c += n;
+    return;
+  }
+  sgn_drun_flush_seq(h, r);
+  r->a = a;
+  r->b = b;
+  r->c = c0 + n;
+  r->n = n;
+}
+/* n identical records (a, b, c) (tx) */
+SGN_HD void sgn_drun_add_same(uint64_t* h, sgn_drun* r, uint64_t a, uint64_t b, uint64_t c,
+                              uint32_t n) {
+  if (r->n && r->a == a && r->b == b && r->c == c) {
+    r->n += n;
+    return;
+  }
+  sgn_drun_flush_same(h, r);
+  r->a = a;
+  r->b = b;
+  r->c = c;
+  r->n = n;
+}
 #define SGN_DIGEST_SEED 0x5eed5eed5eed5eedULL
 
 #endif /* SGN_WORKLOAD_H */

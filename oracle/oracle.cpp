@@ -893,6 +893,7 @@ struct Host {
   uint64_t app_k = 0;
   bool is_server = false;
   uint64_t d_tx = SGN_DIGEST_SEED, d_rx = SGN_DIGEST_SEED, d_app = SGN_DIGEST_SEED;
+  sgn_drun r_tx = {0, 0, 0, 0}, r_rx = {0, 0, 0, 0}, r_app = {0, 0, 0, 0};  // pending runs
   uint64_t n_sent = 0, n_popped = 0, n_delivered = 0, n_codel_dropped = 0;
   uint64_t trace_seq = 0;
 };
@@ -982,13 +983,15 @@ struct ora_sim {
   void deliver_to_app(Host& h, const Pkt& p, bool local) {
     if (local) {
       st.local_delivered++;
-      h.d_app = sgn_digest3(h.d_app, now, (uint64_t)p.src_host | (1ULL << 62), p.payload);
+      sgn_drun_flush_seq(&h.d_app, &h.r_app);  // a local delivery is a run of its own
+      h.d_app = sgn_digest3(h.d_app, now, (uint64_t)p.src_host | (1ULL << 62) | (1ULL << 32),
+                            p.payload);
       return;
     }
     st.delivered++;
     st.bytes_delivered += p.payload;
     h.n_delivered++;
-    h.d_app = sgn_digest3(h.d_app, now, p.src_host, p.src_eid);
+    sgn_drun_add_seq(&h.d_app, &h.r_app, now, p.src_host, p.src_eid, 1);
     trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, now, 0, p.src_eid);
     if (traffic.kind == SGN_TRAFFIC_TGEN && h.is_server && (p.tag & SGN_TAG_REQ)) {
       uint64_t size = traffic.file_bytes[p.tag & 3u];
@@ -1011,7 +1014,7 @@ struct ora_sim {
     auto it = dns.find(p.dst_ip);  // resolve_ip_to_host_id (:347, dns.rs:174)
     if (it == dns.end()) {
       st.packets_unknown_dst++;
-      h.d_tx = sgn_digest3(h.d_tx, now, 0xFFFFFFFFULL | (2ULL << 32), 0);
+      sgn_drun_add_same(&h.d_tx, &h.r_tx, now, 0xFFFFFFFFULL | (2ULL << 32), 0, 1);
       trace_rec(h, SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
       return;
     }
@@ -1023,7 +1026,7 @@ struct ora_sim {
     double chance = h.rng.next_f64();  // :366
     if (!bootstrapping && chance >= reliability && p.payload > 0) {  // :371
       st.packets_loss_dropped++;
-      h.d_tx = sgn_digest3(h.d_tx, now, (uint64_t)dst | (1ULL << 32), 0);
+      sgn_drun_add_same(&h.d_tx, &h.r_tx, now, (uint64_t)dst | (1ULL << 32), 0, 1);
       trace_rec(h, SGN_TRACE_SEND, dst, 1, now, 0, 0);
       return;
     }
@@ -1052,7 +1055,7 @@ struct ora_sim {
     ev.task = -1;
     p.src_eid = ev.eid;
     ev.pkt = p;
-    h.d_tx = sgn_digest3(h.d_tx, now, (uint64_t)dst, deliver);
+    sgn_drun_add_same(&h.d_tx, &h.r_tx, now, (uint64_t)dst, deliver, 1);
     trace_rec(h, SGN_TRACE_SEND, dst, 0, now, deliver, ev.eid);
     if (owned(dst)) {
       Host& d = hosts[dst];
@@ -1086,7 +1089,7 @@ struct ora_sim {
     for (const Pkt& d : h.codel.dropped) {
       st.codel_dropped++;
       h.n_codel_dropped++;
-      h.d_app = sgn_digest3(h.d_app, now, (uint64_t)d.src_host | (1ULL << 63), d.src_eid);
+      sgn_drun_add_seq(&h.d_app, &h.r_app, now, (uint64_t)d.src_host | (1ULL << 63), d.src_eid, 1);
       trace_rec(h, SGN_TRACE_CODEL_DROP, d.src_host, 0, now, 0, d.src_eid);
     }
     h.codel.dropped.clear();
@@ -1183,7 +1186,7 @@ struct ora_sim {
       if (ev.kind == EV_PACKET) {
         st.packet_events_popped++;
         h.n_popped++;
-        h.d_rx = sgn_digest3(h.d_rx, ev.time, ev.src_host, ev.eid);
+        sgn_drun_add_seq(&h.d_rx, &h.r_rx, ev.time, ev.src_host, ev.eid, 1);
         trace_rec(h, SGN_TRACE_POP, ev.src_host, 0, ev.time, 0, ev.eid);
         h.codel.push(ev.pkt, now);            // Router::route_incoming_packet (router/mod.rs:55)
         relay_notify(h, TASK_RELAY_IN);       // notify_router_has_packets (host.rs:958)
@@ -1196,6 +1199,10 @@ struct ora_sim {
           run_forward_task(h, ev.task);
       }
     }
+    // digests are run-encoded (sgn_workload.h): close the pending runs
+    sgn_drun_flush_same(&h.d_tx, &h.r_tx);
+    sgn_drun_flush_seq(&h.d_rx, &h.r_rx);
+    sgn_drun_flush_seq(&h.d_app, &h.r_app);
   }
 
   uint64_t local_min_next() const {

@@ -28,6 +28,21 @@
 #include "sgn_internal.h"
 #include "sgn_workload.h"
 
+// Diagnostic build (libsgn_diag.so, -DSGN_DIAG): per-lane counts of the work kinds that
+// carry dependent global-memory round trips, reported through sgn_debug_stamps.
+#ifdef SGN_DIAG
+#define DG(i) (dg[i]++)
+#define DGT_BEGIN(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define DGT_END(i, v) (dgt[i] += (uint32_t)(__builtin_amdgcn_s_memtime() - (v)))
+#else
+#define DG(i) ((void)0)
+#define DGT_BEGIN(v) ((void)0)
+#define DGT_END(i, v) ((void)0)
+#endif
+enum { DG_RO = 0, DG_RI, DG_APP, DG_BATCH, DG_HDLOAD, DG_FQLOAD, DG_TBREF, DG_POPRUN, DG_N };
+// diagnostic timers: cycles while this lane was inside ...
+enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD, DGT_N };
+
 namespace sgn {
 
 enum : uint32_t { RELAY_IDLE = 0, RELAY_PENDING = 1, RELAY_FORWARDING = 2 };
@@ -57,8 +72,14 @@ __device__ __forceinline__ bool ev_less(const EvRec& a, const EvRec& b) {
   return a.eid < b.eid;
 }
 
+// a / b for a divisor below 2^32: u32 division when the dividend fits too
+__device__ __forceinline__ uint64_t div_small(uint64_t a, uint64_t b) {
+  if (((a | b) >> 32) == 0) return (uint32_t)a / (uint32_t)b;
+  return a / b;
+}
+
 __device__ __forceinline__ uint32_t bucket_of(const DevSim& S, uint64_t t) {
-  return (uint32_t)(((t - SIM_START) / S.BW) % (uint64_t)S.NB);
+  return (uint32_t)S.bw_div.div(t - SIM_START) & (S.NB - 1);
 }
 
 // CoDel control law (router/codel_queue.rs:285-298)
@@ -142,9 +163,17 @@ struct HostExec {
   // registers; their ring slots are stale until store() (or until the tail is closed).
   CodelEnt hd, tl;
   bool hd_valid, tl_open;
+  // pending runs of the run-encoded digests (sgn_workload.h), closed at the end of run():
+  // this lane's three sgn_drun {tx, rx, app} in LDS (registers are the scarce resource)
+  sgn_drun* dr;
+#ifdef SGN_DIAG
+  uint32_t dg[DG_N];
+  uint32_t dgt[DGT_N];
+#endif
 
-  __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks) {}
+  __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
+                      sgn_drun* runs)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), dr(runs) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ void load() {
@@ -152,93 +181,98 @@ struct HostExec {
     gid = S.lo + h;
     my_ip = S.ip[gid];
     my_unode = S.unode[gid];
-    r0 = S.rng0[h];
-    r1 = S.rng1[h];
-    r2 = S.rng2[h];
-    r3 = S.rng3[h];
-    eid = S.eid[h];
-    app_k = S.app_k[h];
-    st0 = S.slot_t[h];
-    st1 = S.slot_t[nH + h];
-    st2 = S.slot_t[2 * nH + h];
-    se0 = S.slot_e[h];
-    se1 = S.slot_e[nH + h];
-    se2 = S.slot_e[2 * nH + h];
-    fl = S.flags[h];
-    ro_dst = S.ro_dst[h];
-    ro_pay = S.ro_pay[h];
-    ro_tag = S.ro_tag[h];
-    ri_src = S.ri_src[h];
-    ri_pay = S.ri_pay[h];
-    ri_tag = S.ri_tag[h];
-    ri_eid = S.ri_eid[h];
-    tbb0 = S.tb_bal[h];
-    tbl0 = S.tb_last[h];
-    tbb1 = S.tb_bal[nH + h];
-    tbl1 = S.tb_last[nH + h];
-    cq_head = S.cq_head[h];
-    cq_nr = S.cq_nr[h];
-    cq_len = S.cq_len[h];
-    cq_bytes = S.cq_bytes[h];
-    cq_ie = S.cq_ie[h];
-    cq_dn = S.cq_dn[h];
-    cq_cur = S.cq_cur[h];
-    cq_prev = S.cq_prev[h];
-    fq_head = S.fq_head[h];
-    fq_len = S.fq_len[h];
-    dtx = S.d_tx[h];
-    drx = S.d_rx[h];
-    dapp = S.d_app[h];
+    r0 = S.f64(H_RNG0)[h];
+    r1 = S.f64(H_RNG1)[h];
+    r2 = S.f64(H_RNG2)[h];
+    r3 = S.f64(H_RNG3)[h];
+    eid = S.f64(H_EID)[h];
+    app_k = S.f64(H_APPK)[h];
+    st0 = S.f64(H_SLOT_T)[h];
+    st1 = S.f64(H_SLOT_T)[nH + h];
+    st2 = S.f64(H_SLOT_T)[2 * nH + h];
+    se0 = S.f64(H_SLOT_E)[h];
+    se1 = S.f64(H_SLOT_E)[nH + h];
+    se2 = S.f64(H_SLOT_E)[2 * nH + h];
+    fl = S.f32(H_FLAGS)[h];
+    ro_dst = S.f32(H_RO_DST)[h];
+    ro_pay = S.f32(H_RO_PAY)[h];
+    ro_tag = S.f32(H_RO_TAG)[h];
+    ri_src = S.f32(H_RI_SRC)[h];
+    ri_pay = S.f32(H_RI_PAY)[h];
+    ri_tag = S.f32(H_RI_TAG)[h];
+    ri_eid = S.f64(H_RI_EID)[h];
+    tbb0 = S.f64(H_TB_BAL)[h];
+    tbl0 = S.f64(H_TB_LAST)[h];
+    tbb1 = S.f64(H_TB_BAL)[nH + h];
+    tbl1 = S.f64(H_TB_LAST)[nH + h];
+    cq_head = S.f32(H_CQ_HEAD)[h];
+    cq_nr = S.f32(H_CQ_NR)[h];
+    cq_len = S.f32(H_CQ_LEN)[h];
+    cq_bytes = S.f64(H_CQ_BYTES)[h];
+    cq_ie = S.f64(H_CQ_IE)[h];
+    cq_dn = S.f64(H_CQ_DN)[h];
+    cq_cur = S.f64(H_CQ_CUR)[h];
+    cq_prev = S.f64(H_CQ_PREV)[h];
+    fq_head = S.f32(H_FQ_HEAD)[h];
+    fq_len = S.f32(H_FQ_LEN)[h];
+    dtx = S.f64(H_D_TX)[h];
+    drx = S.f64(H_D_RX)[h];
+    dapp = S.f64(H_D_APP)[h];
     c_sent = c_loss = c_unknown = c_popped = c_codel = c_deliv = c_ldeliv = c_blocked =
         c_localev = c_bytes = 0;
-    c_maxcodel = (uint32_t)S.cnt[CNT_MAX_CODEL * (size_t)nH + h];
-    tseq = S.trace_on ? S.trace_seq[h] : 0;
+    c_maxcodel = (uint32_t)S.f64(H_CNT)[CNT_MAX_CODEL * (size_t)nH + h];
+    tseq = S.trace_on ? S.f64(H_TSEQ)[h] : 0;
     lat_cache = INVALID;
     hd_valid = tl_open = false;
+    dr[0].n = dr[1].n = dr[2].n = 0;
+#ifdef SGN_DIAG
+    for (int i = 0; i < DG_N; i++) dg[i] = 0;
+    for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
+#endif
   }
 
   __device__ void store() {
     const uint32_t nH = S.nH;
-    S.rng0[h] = r0;
-    S.rng1[h] = r1;
-    S.rng2[h] = r2;
-    S.rng3[h] = r3;
-    S.eid[h] = eid;
-    S.app_k[h] = app_k;
-    S.slot_t[h] = st0;
-    S.slot_t[nH + h] = st1;
-    S.slot_t[2 * nH + h] = st2;
-    S.slot_e[h] = se0;
-    S.slot_e[nH + h] = se1;
-    S.slot_e[2 * nH + h] = se2;
-    S.flags[h] = fl;
-    S.ro_dst[h] = ro_dst;
-    S.ro_pay[h] = ro_pay;
-    S.ro_tag[h] = ro_tag;
-    S.ri_src[h] = ri_src;
-    S.ri_pay[h] = ri_pay;
-    S.ri_tag[h] = ri_tag;
-    S.ri_eid[h] = ri_eid;
-    S.tb_bal[h] = tbb0;
-    S.tb_last[h] = tbl0;
-    S.tb_bal[nH + h] = tbb1;
-    S.tb_last[nH + h] = tbl1;
+    S.f64(H_RNG0)[h] = r0;
+    S.f64(H_RNG1)[h] = r1;
+    S.f64(H_RNG2)[h] = r2;
+    S.f64(H_RNG3)[h] = r3;
+    S.f64(H_EID)[h] = eid;
+    S.f64(H_APPK)[h] = app_k;
+    S.f64(H_SLOT_T)[h] = st0;
+    S.f64(H_SLOT_T)[nH + h] = st1;
+    S.f64(H_SLOT_T)[2 * nH + h] = st2;
+    S.f64(H_SLOT_E)[h] = se0;
+    S.f64(H_SLOT_E)[nH + h] = se1;
+    S.f64(H_SLOT_E)[2 * nH + h] = se2;
+    S.f32(H_FLAGS)[h] = fl;
+    S.f32(H_RO_DST)[h] = ro_dst;
+    S.f32(H_RO_PAY)[h] = ro_pay;
+    S.f32(H_RO_TAG)[h] = ro_tag;
+    S.f32(H_RI_SRC)[h] = ri_src;
+    S.f32(H_RI_PAY)[h] = ri_pay;
+    S.f32(H_RI_TAG)[h] = ri_tag;
+    S.f64(H_RI_EID)[h] = ri_eid;
+    S.f64(H_TB_BAL)[h] = tbb0;
+    S.f64(H_TB_LAST)[h] = tbl0;
+    S.f64(H_TB_BAL)[nH + h] = tbb1;
+    S.f64(H_TB_LAST)[nH + h] = tbl1;
     if (hd_valid) *cq_slot(0) = hd;
     if (tl_open) *cq_slot(cq_nr - 1) = tl;
-    S.cq_head[h] = cq_head;
-    S.cq_nr[h] = cq_nr;
-    S.cq_len[h] = cq_len;
-    S.cq_bytes[h] = cq_bytes;
-    S.cq_ie[h] = cq_ie;
-    S.cq_dn[h] = cq_dn;
-    S.cq_cur[h] = cq_cur;
-    S.cq_prev[h] = cq_prev;
-    S.fq_head[h] = fq_head;
-    S.fq_len[h] = fq_len;
-    S.d_tx[h] = dtx;
-    S.d_rx[h] = drx;
-    S.d_app[h] = dapp;
-    uint64_t* c = S.cnt;
+    S.f32(H_CQ_HEAD)[h] = cq_head;
+    S.f32(H_CQ_NR)[h] = cq_nr;
+    S.f32(H_CQ_LEN)[h] = cq_len;
+    S.f64(H_CQ_BYTES)[h] = cq_bytes;
+    S.f64(H_CQ_IE)[h] = cq_ie;
+    S.f64(H_CQ_DN)[h] = cq_dn;
+    S.f64(H_CQ_CUR)[h] = cq_cur;
+    S.f64(H_CQ_PREV)[h] = cq_prev;
+    S.f32(H_FQ_HEAD)[h] = fq_head;
+    S.f32(H_FQ_LEN)[h] = fq_len;
+    S.f64(H_D_TX)[h] = dtx;
+    S.f64(H_D_RX)[h] = drx;
+    S.f64(H_D_APP)[h] = dapp;
+    uint64_t* c = S.f64(H_CNT);
     const size_t n = nH;
     c[CNT_SENT * n + h] += c_sent;
     c[CNT_LOSS * n + h] += c_loss;
@@ -251,7 +285,7 @@ struct HostExec {
     c[CNT_LOCAL_EV * n + h] += c_localev;
     c[CNT_BYTES * n + h] += c_bytes;
     c[CNT_MAX_CODEL * n + h] = c_maxcodel;
-    if (S.trace_on) S.trace_seq[h] = tseq;
+    if (S.trace_on) S.f64(H_TSEQ)[h] = tseq;
   }
 
   __device__ uint64_t next_local_time() const {
@@ -346,12 +380,13 @@ struct HostExec {
     // when a refill is due or a removal fails, not on the per-packet fast path).
     uint64_t span = now - last;
     if (span >= interval) {
-      const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
+      DG(DG_TBREF);
+      const uint64_t inc = S.f64(H_TB_INC)[(size_t)W * S.nH + h];
       uint64_t nref = span / interval;
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
       if (b < bal) b = ~0ULL;
-      const uint64_t cap = S.tb_cap[(size_t)W * S.nH + h];
+      const uint64_t cap = S.f64(H_TB_CAP)[(size_t)W * S.nH + h];
       bal = b > cap ? cap : b;
       uint64_t adv = mul_sat(interval, nref, SIMTIME_MAX);
       last = emu_sat_add(last, adv);
@@ -360,9 +395,16 @@ struct HostExec {
     uint64_t next_refill_span = interval - span;
     if (dec > bal) {
       // compute_conforming_duration (:91-117)
-      const uint64_t inc = S.tb_inc[(size_t)W * S.nH + h];
+      const uint64_t inc = S.f64(H_TB_INC)[(size_t)W * S.nH + h];
       uint64_t req = dec - bal;
-      uint64_t n = req / inc + ((req % inc) ? 1 : 0);
+      uint64_t n;
+      if (((req | inc) >> 32) == 0) {  // u32 division: the u64 routine is long
+        const uint32_t r32 = (uint32_t)req, i32 = (uint32_t)inc;
+        const uint32_t q = r32 / i32;
+        n = q + (r32 - q * i32 ? 1 : 0);
+      } else {
+        n = req / inc + ((req % inc) ? 1 : 0);
+      }
       if (n == 0)
         *dur = 0;
       else if (n == 1)
@@ -437,6 +479,7 @@ struct HostExec {
       hd = tl;
       tl_open = false;
     } else {
+      DG(DG_HDLOAD);
       hd = *cq_slot(0);
     }
     hd_valid = true;
@@ -467,7 +510,7 @@ struct HostExec {
   }
   __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
     c_codel++;
-    dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 63), p.eid);
+    sgn_drun_add_seq(&dapp, dr + 2, now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
   __device__ bool codel_was_dropping_recently() const {  // :273-281
@@ -569,27 +612,33 @@ struct HostExec {
     }
   }
 
-  // interface delivery to the synthetic app (NetworkInterface::push -> socket)
-  __device__ void deliver_to_app(const Pkt& p, bool local) {
-    if (local) {
-      c_ldeliv++;
-      dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 62), p.payload);
-      return;
-    }
-    c_deliv++;
-    c_bytes += p.payload;
-    dapp = sgn_digest3(dapp, now, p.src, p.eid);
-    trace(SGN_TRACE_DELIVER, p.src, 0, now, 0, p.eid);
-    if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (p.tag & SGN_TAG_REQ)) {
-      const uint64_t size = S.file_bytes[p.tag & 3u];
+  // interface delivery to the synthetic app (NetworkInterface::push -> socket) of m packets
+  // from src with consecutive event ids e0.. at `now` (one run-encoded app digest step)
+  __device__ void deliver_run(uint32_t src, uint64_t e0, uint32_t m, uint32_t payload,
+                              uint32_t tag) {
+    c_deliv += m;
+    c_bytes += (uint64_t)m * payload;
+    sgn_drun_add_seq(&dapp, dr + 2, now, src, e0, m);
+    if (S.trace_on)
+      for (uint32_t k = 0; k < m; k++) trace(SGN_TRACE_DELIVER, src, 0, now, 0, e0 + k);
+    if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
+      const uint64_t size = S.file_bytes[tag & 3u];
       const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
       if (n == 0) return;
       const uint32_t last = (uint32_t)(size - (n - 1) * SGN_TGEN_MSS);
-      if (fifo_push(S.ip[p.src], SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
-        relay_notify<0>();
-      else
-        c_blocked++;
+      const uint32_t dip = S.ip[src];
+      for (uint32_t k = 0; k < m; k++) {
+        if (fifo_push(dip, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
+          relay_notify<0>();
+        else
+          c_blocked++;
+      }
     }
+  }
+  __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
+    c_ldeliv++;
+    sgn_drun_flush_seq(&dapp, dr + 2);
+    dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
   }
 
   // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) for relay_inet_in:
@@ -624,7 +673,7 @@ struct HostExec {
                 m = 0;
                 blocked = true;
               } else if (n > 1) {
-                const uint64_t more = tbb1 / wire;
+                const uint64_t more = div_small(tbb1, wire);
                 if (more >= n - 1) {
                   tbb1 -= (uint64_t)(n - 1) * wire;
                 } else {
@@ -647,14 +696,7 @@ struct HostExec {
               cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
               cq_nr--;
             }
-            p.src = r.src;
-            p.dst_ip = my_ip;
-            p.payload = r.payload;
-            p.tag = r.tag;
-            for (uint32_t k = 0; k < m; k++) {
-              p.eid = r.eid + k;
-              deliver_to_app(p, false);
-            }
+            if (m) deliver_run(r.src, r.eid, m, r.payload, r.tag);
             if (blocked) {
               fl |= F_RI_NEXT;
               ri_src = r.src;
@@ -682,46 +724,61 @@ struct HostExec {
         set_relay_state<1>(RELAY_IDLE);
         return true;
       }
-      deliver_to_app(p, false);
+      deliver_run(p.src, p.eid, 1, p.payload, p.tag);
     }
   }
 
   // A run of n identical datagrams pushed to the router at the same `now`: n consecutive
   // Worker::send_packet calls (core/worker.rs:330-403). The DNS lookup, route entry,
   // reliability and delivery time are the same for all of them, so they are computed
-  // once; the per-packet loss draws and digests stay sequential (same RNG stream, same
-  // order). Sent packets take consecutive source event ids and share one delivery time,
-  // so their events are reserved with one atomic and written as one contiguous run.
+  // once; the per-packet loss draws stay sequential (same RNG stream, same order) and the
+  // digest takes runs of equal outcomes. Sent packets take consecutive source event ids and
+  // share one delivery time, so their events are reserved with one atomic and written as
+  // one contiguous run.
   __device__ void send_batch(uint32_t dst_ip, uint32_t payload, uint32_t tag, uint32_t n) {
+    DGT_BEGIN(t0);
+    send_batch_(dst_ip, payload, tag, n);
+    DGT_END(DGT_SEND, t0);
+  }
+  __device__ void send_batch_(uint32_t dst_ip, uint32_t payload, uint32_t tag, uint32_t n) {
     if (n == 0 || now >= S.end_time) return;
+    DG(DG_BATCH);
     const bool boot = now < S.boot_end;
     uint32_t dst;
     if (!dns_lookup(dst_ip, &dst)) {
-      for (uint32_t j = 0; j < n; j++) {
-        c_unknown++;
-        dtx = sgn_digest3(dtx, now, 0xFFFFFFFFULL | (2ULL << 32), 0);
-        trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
-      }
+      c_unknown += n;
+      sgn_drun_add_same(&dtx, dr + 0, now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
+      if (S.trace_on)
+        for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
       return;
     }
     const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
-    const double reliability = (double)__fsub_rn(1.0f, S.rloss[ri]);
+    const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
     const uint64_t delay = S.rlat[ri];
     uint64_t deliver = now + delay;
     if (deliver < we) deliver = we;
     const uint64_t eid0 = eid;
+    // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53:
+    // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an exact
+    // integer T and the test is (x >> 11) >= T, bit for bit the same decision
+    const uint64_t T = (uint64_t)((double)rel32 * 9007199254740992.0);
+    const bool can_drop = !boot && payload > 0;
+    uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
     for (uint32_t j = 0; j < n; j++) {
-      const double chance = rng_f64();
-      if (!boot && chance >= reliability && payload > 0) {
+      const uint64_t x = rng_next() >> 11;
+      if (can_drop && x >= T) {
         c_loss++;
-        dtx = sgn_digest3(dtx, now, (uint64_t)dst | (1ULL << 32), 0);
-        trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+        if (run) sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst, deliver, run);
+        run = 0;
+        sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst | (1ULL << 32), 0, 1);
+        if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
       } else {
         const uint64_t e = eid++;
-        dtx = sgn_digest3(dtx, now, (uint64_t)dst, deliver);
-        trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+        run++;
+        if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
       }
     }
+    if (run) sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst, deliver, run);
     const uint32_t nsent = (uint32_t)(eid - eid0);
     if (nsent == 0) return;
     c_sent += nsent;
@@ -739,7 +796,7 @@ struct HostExec {
     if (owned) {
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : S.bucket_slab[b];
-      const size_t idx = (size_t)slab * S.G + (dst - S.lo) / GROUP;
+      const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
       atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
                 (unsigned long long)deliver);
@@ -798,11 +855,12 @@ struct HostExec {
       p.tag = ro_tag;
       p.eid = 0;
       if (is_local)
-        deliver_to_app(p, true);
+        deliver_local(p);
       else
         send_batch(ro_dst, ro_pay, ro_tag, 1);
     }
     while (fq_len > 0) {
+      DG(DG_FQLOAD);
       FifoEnt* s = fq_slot(0);
       const FifoEnt e = *s;
       const uint32_t run = e.count == 1 ? 1u : e.count - 1;
@@ -816,7 +874,7 @@ struct HostExec {
           n_ok = 0;
           blocked = true;
         } else if (run > 1) {
-          const uint64_t more = tbb0 / wire;
+          const uint64_t more = div_small(tbb0, wire);
           if (more >= run - 1) {
             tbb0 -= (uint64_t)(run - 1) * wire;
           } else {
@@ -834,7 +892,7 @@ struct HostExec {
         p.payload = payload;
         p.tag = e.tag;
         p.eid = 0;
-        for (uint32_t j = 0; j < n_ok; j++) deliver_to_app(p, true);
+        for (uint32_t j = 0; j < n_ok; j++) deliver_local(p);
       } else {
         send_batch(e.dst_ip, payload, e.tag, n_ok);
       }
@@ -863,7 +921,9 @@ struct HostExec {
   __device__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
     uint64_t dur;
+    DGT_BEGIN(t0);
     const bool blocked = W == 0 ? forward_out(&dur) : forward_in(&dur);
+    DGT_END(W == 0 ? DGT_FWDOUT : DGT_FWDIN, t0);
     if (blocked) forward_later<W>(dur);
   }
 
@@ -914,6 +974,8 @@ struct HostExec {
         const EvRec& e = ev[ord[pi]];
         if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           pi++;
+          DG(DG_POPRUN);
+          DGT_BEGIN(t0);
           now = e.time;
           // the run's packets pop back to back (nothing sorts between them); each is
           // routed into CoDel and notifies relay_inet_in, which schedules its task on
@@ -922,13 +984,13 @@ struct HostExec {
           const uint32_t src = e.src;
           const uint64_t eid0 = e.eid;
           c_popped += n;
-          for (uint32_t k = 0; k < n; k++) {
-            drx = sgn_digest3(drx, now, src, eid0 + k);
-            trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
-          }
+          sgn_drun_add_seq(&drx, dr + 1, now, src, eid0, n);
+          if (S.trace_on)
+            for (uint32_t k = 0; k < n; k++) trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
           // Router::route_incoming_packet (router/mod.rs:55-57)
           codel_push_run(src, eid0, ev_payload(e), e.tag, n);
           relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
+          DGT_END(DGT_POP, t0);
           continue;
         }
       }
@@ -937,15 +999,24 @@ struct HostExec {
       c_localev++;
       if (ls == 0) {
         st0 = INVALID;
+        DG(DG_RO);
         run_forward_task<0>();
       } else if (ls == 1) {
         st1 = INVALID;
+        DG(DG_RI);
         run_forward_task<1>();
       } else {
         st2 = INVALID;
+        DG(DG_APP);
+        DGT_BEGIN(t0);
         app_task();
+        DGT_END(DGT_APP, t0);
       }
     }
+    // the sub-window is done: close the digests' pending runs (sgn_workload.h)
+    sgn_drun_flush_same(&dtx, dr + 0);
+    sgn_drun_flush_seq(&drx, dr + 1);
+    sgn_drun_flush_seq(&dapp, dr + 2);
   }
 };
 
@@ -976,19 +1047,23 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
-  __shared__ EvRec lev[LDS_CAP];
-  __shared__ uint16_t lb[LDS_CAP];  // due runs grouped by destination lane (unordered)
-  __shared__ uint16_t lc[LDS_CAP];  // ... ordered inside each destination segment
-  __shared__ uint32_t lcnt[GROUP], lstart[GROUP], lcur[GROUP];
+  // dynamic LDS sized by the slab capacity S.CAP (a bucket's runs of one group fit a slab)
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  EvRec* lev = (EvRec*)lds_dyn;                 // due runs of the bucket
+  uint16_t* lb = (uint16_t*)(lev + S.CAP);      // grouped by destination lane (unordered)
+  uint16_t* lc = lb + S.CAP;                    // ... ordered inside each destination segment
+  __shared__ uint32_t lcnt[64], lstart[64], lcur[64];
+  __shared__ sgn_drun ldr[3 * 64];  // the lanes' pending digest runs
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x;
-  const uint32_t h = g * GROUP + lane;  // local host index
-  const bool valid = h < S.nH;
+  const uint32_t gsz = 1u << S.gsh;
+  const uint32_t h = (g << S.gsh) + lane;  // local host index
+  const bool valid = lane < gsz && h < S.nH;
   const uint64_t ws = C->ws, we = C->we;
   const uint32_t bs = bucket_of(S, ws), be = bucket_of(S, we - 1);
-  const uint32_t nbk = (be + S.NB - bs) % S.NB + 1;  // buckets overlapping the window
+  const uint32_t nbk = ((be + S.NB - bs) & (S.NB - 1)) + 1;  // buckets overlapping the window
   const uint32_t ks = C->keep_slab;
-  const uint32_t gbase = S.lo + g * GROUP;  // HostId of lane 0
+  const uint32_t gbase = S.lo + (g << S.gsh);  // HostId of lane 0
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
   const size_t ik = (size_t)ks * S.G + g;
   EvRec* pk = S.pool + ik * S.CAP;
@@ -996,19 +1071,21 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   uint64_t lmin = INVALID;
   if (valid) {
     const uint32_t nH = S.nH;
-    const uint64_t t0 = S.slot_t[h], t1 = S.slot_t[nH + h], t2 = S.slot_t[2 * nH + h];
+    const uint64_t t0 = S.f64(H_SLOT_T)[h], t1 = S.f64(H_SLOT_T)[nH + h], t2 = S.f64(H_SLOT_T)[2 * nH + h];
     lmin = t0 < t1 ? t0 : t1;
     lmin = t2 < lmin ? t2 : lmin;
   }
-  HostExec ex(S, h, we, be, ks);
+  HostExec ex(S, h, we, be, ks, ldr + 3 * lane);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
 
+  uint64_t t_gather = 0, t_exec = 0;
   for (uint32_t bi = 0; bi < nbk; bi++) {
-    const uint32_t b = (bs + bi) % S.NB;
+    const uint64_t c0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t b = (bs + bi) & (S.NB - 1);
     const bool last = bi == nbk - 1;
-    const uint64_t sub_end = last ? we : SIM_START + ((ws - SIM_START) / S.BW + bi + 1) * S.BW;
+    const uint64_t sub_end = last ? we : SIM_START + (S.bw_div.div(ws - SIM_START) + bi + 1) * S.BW;
     // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
     const size_t ib = (size_t)S.bucket_slab[b] * S.G + g;
@@ -1080,14 +1157,26 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
     sorted += cnt > 1 ? 1u : 0u;
     __syncthreads();
     // ---- 3. execute the sub-window [.., sub_end) ----
+    const uint64_t c1 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
     if (valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end)) {
       if (!loaded) {
+#ifdef SGN_DIAG
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
         ex.load();
+        ex.dgt[DGT_LOAD] += (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
+#else
+        ex.load();
+#endif
         loaded = true;
       }
       ex.run(lev, lc, start, start + cnt, sub_end);
     }
     __syncthreads();  // LDS is reused by the next bucket
+    if (S.stamps) {
+      const uint64_t c2 = __builtin_amdgcn_s_memtime();
+      t_gather += c1 - c0;
+      t_exec += c2 - c1;
+    }
   }
 
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
@@ -1109,26 +1198,46 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       mx = o > mx ? o : mx;
     }
     const uint32_t busy = __popcll(__ballot(n_ev > 0));
+    uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)blockIdx.x;
     if (lane == 0) {
-      uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)blockIdx.x;
       st[0] = clk1 - clk0;
       st[1] = sum;
       st[2] = mx;
       st[3] = busy;
       st[4] = N_all;
+      st[5] = t_gather;
+      st[6] = t_exec;
     }
+#ifdef SGN_DIAG
+    // the busiest lane's work counts (words 8..15) and the wave's sums (16..23)
+    const uint64_t bm = __ballot(loaded && n_ev == mx);
+    const int bl = bm ? __ffsll((long long)bm) - 1 : 0;
+    for (int i = 0; i < DG_N; i++) {
+      const uint32_t v = loaded ? ex.dg[i] : 0u;
+      const uint32_t vb = __shfl(v, bl, 64);
+      const uint32_t vs = wave_sum_u32(v);
+      if (lane == 0) {
+        st[8 + i] = vb;
+        st[16 + i] = vs;
+      }
+    }
+    for (int i = 0; i < DGT_N; i++) {
+      const uint32_t v = loaded ? ex.dgt[i] : 0u;
+      const uint32_t vb = __shfl(v, bl, 64);
+      if (lane == 0) st[24 + i] = vb;
+    }
+#endif
   }
   // ---- 4. hosts that ran (roofline accounting) and the group's next event ----
   const uint64_t ex_mask = __ballot(loaded);
   const uint32_t n_sorted = wave_sum_u32(sorted);
   const uint64_t m = wave_min_u64(my_min);
   if (lane == 0) {
-    if (kmin != INVALID) atomicMin((unsigned long long*)&C->keep_min, (unsigned long long)kmin);
-    if (ex_mask)
-      atomicAdd((unsigned long long*)&C->exec_hosts, (unsigned long long)__popcll(ex_mask));
-    if (N_all) atomicAdd((unsigned long long*)&C->tot_runs, (unsigned long long)N_all);
-    if (n_sorted) atomicAdd((unsigned long long*)&C->tot_sorted, (unsigned long long)n_sorted);
-    if (m != INVALID) atomicMin((unsigned long long*)&C->round_min, (unsigned long long)m);
+    S.w_keep[g] = kmin;
+    S.w_next[g] = m;
+    if (ex_mask) S.w_cnt[g] += (uint64_t)__popcll(ex_mask);
+    if (N_all) S.w_cnt[S.G + g] += N_all;
+    if (n_sorted) S.w_cnt[2 * (size_t)S.G + g] += n_sorted;
   }
 }
 
@@ -1138,14 +1247,23 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
   __shared__ uint64_t sh[16];
+  // the waves' minima: events kept in the spare slab, and next local events
+  uint64_t kk = INVALID, wn = INVALID;
+  for (uint32_t g = threadIdx.x; g < S.G; g += blockDim.x) {
+    const uint64_t a = S.w_keep[g], b = S.w_next[g];
+    kk = a < kk ? a : kk;
+    wn = b < wn ? b : wn;
+  }
+  kk = block_min_u64(kk, sh);
+  wn = block_min_u64(wn, sh);
   if (threadIdx.x == 0) {
     const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
-    for (uint32_t b = b0; b != b1; b = (b + 1) % S.NB) S.bucket_min[b] = INVALID;  // consumed
+    for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1)) S.bucket_min[b] = INVALID;  // consumed
     // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
     const uint32_t old = S.bucket_slab[b1];
     S.bucket_slab[b1] = C->keep_slab;
     C->keep_slab = old;
-    S.bucket_min[b1] = C->keep_min;
+    S.bucket_min[b1] = C->keep_min < kk ? C->keep_min : kk;
     C->keep_min = INVALID;
   }
   __syncthreads();
@@ -1154,11 +1272,9 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
     const uint64_t bm = S.bucket_min[b];
     m = bm < m ? bm : m;
   }
-  m = wave_min_u64(m);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
-  __syncthreads();
+  m = block_min_u64(m, sh);
   if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x >> 6); i++) m = sh[i] < m ? sh[i] : m;
+    m = wn < m ? wn : m;
     m = C->round_min < m ? C->round_min : m;
     C->round_min = m;  // local minimum (reduced across shards when advance == 0)
     if (advance) {
@@ -1215,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
       const EvRec e = S.xin[(size_t)r * S.xslot + i];
       const uint32_t b = bucket_of(S, e.time);
       const uint32_t slab = b == b1 ? ks : S.bucket_slab[b];
-      const size_t idx = (size_t)slab * S.G + (e.dst - S.lo) / GROUP;
+      const size_t idx = (size_t)slab * S.G + ((e.dst - S.lo) >> S.gsh);
       const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
       atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
                 (unsigned long long)e.time);
@@ -1261,6 +1377,9 @@ const char* kKernelNames[K_NUM] = {"k_execute", "k_finalize", "k_import", "k_adv
 
 int launch_round(sgn_ctx* ctx);
 
+// dynamic LDS of k_execute: CAP event runs + two u16 index arrays
+inline size_t exec_lds_bytes(uint32_t cap) { return (size_t)cap * (sizeof(EvRec) + 4); }
+
 }  // namespace
 
 
@@ -1270,7 +1389,7 @@ int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
   time_begin(ctx, K_EXECUTE);
-  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(GROUP), 0, st, S);
+  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(64), exec_lds_bytes(S.CAP), st, S);
   time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
@@ -1562,39 +1681,26 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     return 0;
   };
   int rc = 0;
-  if ((rc = up64(r0, &S.rng0)) || (rc = up64(r1, &S.rng1)) || (rc = up64(r2, &S.rng2)) ||
-      (rc = up64(r3, &S.rng3)) || (rc = up64(eid, &S.eid)) || (rc = up64(app_k, &S.app_k)) ||
-      (rc = up64(slot_t, &S.slot_t)) || (rc = up64(slot_e, &S.slot_e)) ||
-      (rc = up32(flags, &S.flags)) || (rc = up64(tb_bal, &S.tb_bal)) ||
-      (rc = up64(tb_last, &S.tb_last)) || (rc = up64(tb_cap, &S.tb_cap)) ||
-      (rc = up64(tb_inc, &S.tb_inc)) || (rc = up64(dig, &S.d_tx)) || (rc = up64(dig, &S.d_rx)) ||
-      (rc = up64(dig, &S.d_app)))
-    return rc;
-  S.ro_dst = dalloc<uint32_t>(ctx, nH);
-  S.ro_pay = dalloc<uint32_t>(ctx, nH);
-  S.ro_tag = dalloc<uint32_t>(ctx, nH);
-  S.ri_src = dalloc<uint32_t>(ctx, nH);
-  S.ri_pay = dalloc<uint32_t>(ctx, nH);
-  S.ri_tag = dalloc<uint32_t>(ctx, nH);
-  S.ri_eid = dalloc<uint64_t>(ctx, nH);
+  // the per-host state: one block of u64 fields and one of u32 fields, field f of host h at
+  // [f * nH + h] (few base pointers keep the round kernel's scalar registers free)
+  S.hs64 = dalloc<uint64_t>(ctx, (size_t)H64_N * nH);
+  S.hs32 = dalloc<uint32_t>(ctx, (size_t)H32_N * nH);
   S.codel = dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
-  S.cq_head = dalloc<uint32_t>(ctx, nH);
-  S.cq_nr = dalloc<uint32_t>(ctx, nH);
-  S.cq_len = dalloc<uint32_t>(ctx, nH);
-  S.cq_bytes = dalloc<uint64_t>(ctx, nH);
-  S.cq_ie = dalloc<uint64_t>(ctx, nH);
-  S.cq_dn = dalloc<uint64_t>(ctx, nH);
-  S.cq_cur = dalloc<uint64_t>(ctx, nH);
-  S.cq_prev = dalloc<uint64_t>(ctx, nH);
   S.fifo = dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
-  S.fq_head = dalloc<uint32_t>(ctx, nH);
-  S.fq_len = dalloc<uint32_t>(ctx, nH);
-  S.cnt = dalloc<uint64_t>(ctx, (size_t)NCNT * nH);
-  S.trace_seq = dalloc<uint64_t>(ctx, nH);
-  if (!S.ro_dst || !S.ro_pay || !S.ro_tag || !S.ri_src || !S.ri_pay || !S.ri_tag || !S.ri_eid ||
-      !S.codel || !S.cq_head || !S.cq_nr || !S.cq_len || !S.cq_bytes || !S.cq_ie || !S.cq_dn || !S.cq_cur ||
-      !S.cq_prev || !S.fifo || !S.fq_head || !S.fq_len || !S.cnt || !S.trace_seq)
+  if (!S.hs64 || !S.hs32 || !S.codel || !S.fifo)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
+  auto put64 = [&](uint32_t f, const std::vector<uint64_t>& v) -> int {
+    SGN_HIP(ctx, hipMemcpy(S.f64(f), v.data(), v.size() * 8, hipMemcpyHostToDevice));
+    return 0;
+  };
+  if ((rc = put64(H_RNG0, r0)) || (rc = put64(H_RNG1, r1)) || (rc = put64(H_RNG2, r2)) ||
+      (rc = put64(H_RNG3, r3)) || (rc = put64(H_EID, eid)) || (rc = put64(H_APPK, app_k)) ||
+      (rc = put64(H_SLOT_T, slot_t)) || (rc = put64(H_SLOT_E, slot_e)) ||
+      (rc = put64(H_TB_BAL, tb_bal)) || (rc = put64(H_TB_LAST, tb_last)) ||
+      (rc = put64(H_TB_CAP, tb_cap)) || (rc = put64(H_TB_INC, tb_inc)) ||
+      (rc = put64(H_D_TX, dig)) || (rc = put64(H_D_RX, dig)) || (rc = put64(H_D_APP, dig)))
+    return rc;
+  SGN_HIP(ctx, hipMemcpy(S.f32(H_FLAGS), flags.data(), (size_t)nH * 4, hipMemcpyHostToDevice));
 
   // ---- calendar: bucket width >= any window length, horizon > max latency ----
   // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least
@@ -1602,15 +1708,28 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   uint64_t BW = std::max<uint64_t>(1, std::max(min_possible, cfg->runahead_ns));
   uint64_t NB = max_lat / BW + 4;
   if (NB > (1u << 20)) return set_error(ctx, SGN_EINVAL, "calendar would need > 2^20 buckets");
-  const uint64_t G = (nH + GROUP - 1) / GROUP;
+  while (NB & (NB - 1)) NB += NB & (~NB + 1);  // round up to a power of two
+  // hosts per k_execute wave: fewer than 64 spreads the (divergent, per-lane serial) host
+  // work of a round over more waves; sgn_sim_config.hosts_per_wave (0 = default 64)
+  uint32_t gsz = cfg->hosts_per_wave ? cfg->hosts_per_wave : 64;
+  if (const char* e = getenv("SGN_HOSTS_PER_WAVE")) gsz = (uint32_t)atoi(e);
+  if (gsz == 0 || gsz > GROUP_MAX || (gsz & (gsz - 1)))
+    return set_error(ctx, SGN_EINVAL, "hosts_per_wave must be a power of two in [1, 64]");
+  S.gsh = (uint32_t)__builtin_ctz(gsz);
+  const uint64_t G = (nH + gsz - 1) / gsz;
   uint64_t cap = cfg->event_capacity ? cfg->event_capacity : (1ULL << 22);
   uint64_t CAP = cap / ((NB + 1) * G);
-  CAP = std::max<uint64_t>(64, std::min<uint64_t>(CAP_MAX, CAP));
+  CAP = std::max<uint64_t>(CAP_MIN, std::min<uint64_t>(CAP_MAX, CAP));
   S.NB = (uint32_t)NB;
   S.G = (uint32_t)G;
   S.CAP = (uint32_t)CAP;
   S.BW = BW;
+  S.bw_div.init(BW);
   S.pool = dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
+  S.w_next = dalloc<uint64_t>(ctx, G);
+  S.w_keep = dalloc<uint64_t>(ctx, G);
+  S.w_cnt = dalloc<uint64_t>(ctx, 3 * G);
+  if (!S.w_next || !S.w_keep || !S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
   S.slab_n = dalloc<uint32_t>(ctx, (NB + 1) * G);
   if (!S.pool || !S.slab_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event calendar)");
   std::vector<uint32_t> bslab(NB);
@@ -1738,7 +1857,7 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   int rc = sync_ctrl(ctx);
   const uint32_t nH = ctx->S.nH;
   std::vector<uint64_t> cnt((size_t)NCNT * nH);
-  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.cnt, cnt.size() * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.f64(H_CNT), cnt.size() * 8, hipMemcpyDeviceToHost));
   sgn_stats s{};
   auto sum = [&](int k) {
     uint64_t t = 0;
@@ -1762,10 +1881,18 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   for (uint32_t h = 0; h < nH; h++) mc = std::max(mc, cnt[(size_t)CNT_MAX_CODEL * nH + h]);
   s.max_codel_len = mc;
   s.max_pending_events = ctx->h_ctrl->max_bucket;
-  s.host_executions = ctx->h_ctrl->exec_hosts;
+  {
+    const size_t G = ctx->S.G;
+    std::vector<uint64_t> wc(3 * G);
+    SGN_HIP(ctx, hipMemcpy(wc.data(), ctx->S.w_cnt, wc.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t acc[3] = {0, 0, 0};
+    for (int k = 0; k < 3; k++)
+      for (size_t g = 0; g < G; g++) acc[k] += wc[k * G + g];
+    s.host_executions = acc[0];
+    s.event_runs = acc[1];
+    s.sched_sorted_segments = acc[2];
+  }
   s.sched_heavy_hosts = 0;
-  s.sched_sorted_segments = ctx->h_ctrl->tot_sorted;
-  s.event_runs = ctx->h_ctrl->tot_runs;
   *out = s;
   return rc;
 }
@@ -1779,15 +1906,15 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
   if (n == 0) return rc;
   std::vector<uint64_t> tx(n), rx(n), ap(n), a(n), b(n), c(n), d(n), e(n);
   std::vector<uint64_t> cnt((size_t)NCNT * nH);
-  SGN_HIP(ctx, hipMemcpy(tx.data(), ctx->S.d_tx + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(rx.data(), ctx->S.d_rx + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(ap.data(), ctx->S.d_app + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(a.data(), ctx->S.rng0 + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(b.data(), ctx->S.rng1 + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(c.data(), ctx->S.rng2 + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(d.data(), ctx->S.rng3 + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(e.data(), ctx->S.eid + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.cnt, cnt.size() * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(tx.data(), ctx->S.f64(H_D_TX) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(rx.data(), ctx->S.f64(H_D_RX) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(ap.data(), ctx->S.f64(H_D_APP) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(a.data(), ctx->S.f64(H_RNG0) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(b.data(), ctx->S.f64(H_RNG1) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(c.data(), ctx->S.f64(H_RNG2) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(d.data(), ctx->S.f64(H_RNG3) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(e.data(), ctx->S.f64(H_EID) + off, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.f64(H_CNT), cnt.size() * 8, hipMemcpyDeviceToHost));
   for (uint32_t i = 0; i < n; i++) {
     sgn_host_digest& o = out[i];
     o.tx = tx[i];
@@ -1817,12 +1944,12 @@ int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
   uint64_t m = INVALID;
   for (int s = 0; s < NSLOT; s++) {
     uint64_t v;
-    SGN_HIP(ctx, hipMemcpy(&v, ctx->S.slot_t + (size_t)s * nH + h, 8, hipMemcpyDeviceToHost));
+    SGN_HIP(ctx, hipMemcpy(&v, ctx->S.f64(H_SLOT_T) + (size_t)s * nH + h, 8, hipMemcpyDeviceToHost));
     m = std::min(m, v);
   }
   // pending packet events for this host: its group's slab in every bucket
   const DevSim& S = ctx->S;
-  const uint32_t g = h / GROUP;
+  const uint32_t g = h >> S.gsh;
   std::vector<uint32_t> bs(S.NB);
   SGN_HIP(ctx, hipMemcpy(bs.data(), S.bucket_slab, bs.size() * 4, hipMemcpyDeviceToHost));
   for (uint32_t b = 0; b < S.NB; b++) {

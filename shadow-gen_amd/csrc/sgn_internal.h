@@ -82,9 +82,6 @@ struct Ctrl {
   uint64_t max_bucket;    // high-water mark of any (bucket, host group) slab fill
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
-  uint64_t exec_hosts;    // cumulative host executions (hosts with due events per round)
-  uint64_t tot_runs;      // cumulative due event runs (records) handled
-  uint64_t tot_sorted;    // cumulative host segments that needed ordering (>= 2 runs)
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -115,6 +112,28 @@ enum {
   NCNT
 };
 
+// per-host u64 fields (DevSim::f64); multi-slot fields take consecutive field indices
+enum : uint32_t {
+  H_RNG0 = 0, H_RNG1, H_RNG2, H_RNG3,  // Xoshiro256++ state (host/host.rs:234)
+  H_EID,                               // next event id (host.rs:259,662-666)
+  H_APPK,                              // synthetic app counter
+  H_SLOT_T, H_SLOT_E = H_SLOT_T + 3,   // local event slots: time / event id [3]
+  H_RI_EID = H_SLOT_E + 3,             // relay_inet_in cached packet's event id
+  H_TB_BAL, H_TB_LAST = H_TB_BAL + 2,  // token buckets [2]: 0 = inet_out, 1 = inet_in
+  H_TB_CAP = H_TB_LAST + 2, H_TB_INC = H_TB_CAP + 2,
+  H_CQ_BYTES = H_TB_INC + 2, H_CQ_IE, H_CQ_DN, H_CQ_CUR, H_CQ_PREV,  // CoDel state
+  H_D_TX, H_D_RX, H_D_APP,             // digests
+  H_TSEQ,                              // trace sequence
+  H_CNT,                               // counters [NCNT]
+  H64_N = H_CNT + NCNT
+};
+// per-host u32 fields (DevSim::f32)
+enum : uint32_t {
+  H_FLAGS = 0, H_RO_DST, H_RO_PAY, H_RO_TAG, H_RI_SRC, H_RI_PAY, H_RI_TAG,
+  H_CQ_HEAD, H_CQ_NR, H_CQ_LEN, H_FQ_HEAD, H_FQ_LEN,
+  H32_N
+};
+
 // host flag bits
 enum : uint32_t {
   F_RO_STATE = 0x3u,         // relay_inet_out state (Idle/Pending/Forwarding)
@@ -129,6 +148,48 @@ enum : uint32_t {
 };
 
 enum { SLOT_RO = 0, SLOT_RI = 1, SLOT_APP = 2, NSLOT = 3 };
+
+// Division by a run-time invariant u64 d > 0 as a multiply-high and shifts (the libdivide
+// "round up / add indicator" scheme): exact for every u64 x. GPU u64 division is a long
+// software routine; the round kernel divides every event time by the bucket width.
+struct UDiv64 {
+  uint64_t m;      // magic multiplier (0: d is a power of two)
+  uint32_t shift;
+  uint32_t add;    // 1: use the add-indicator form
+  __host__ void init(uint64_t d) {
+    const uint32_t l = 63u - (uint32_t)__builtin_clzll(d);
+    if ((d & (d - 1)) == 0) {
+      m = 0;
+      shift = l;
+      add = 0;
+      return;
+    }
+    const unsigned __int128 num = (unsigned __int128)1 << (64 + l);
+    uint64_t pm = (uint64_t)(num / d);
+    const uint64_t rem = (uint64_t)(num % d);
+    const uint64_t e = d - rem;
+    if (e < (1ULL << l)) {
+      add = 0;
+    } else {
+      pm += pm;
+      const uint64_t r2 = rem + rem;
+      if (r2 >= d || r2 < rem) pm += 1;
+      add = 1;
+    }
+    m = pm + 1;
+    shift = l;
+  }
+  __host__ __device__ __forceinline__ uint64_t div(uint64_t x) const {
+    if (m == 0) return x >> shift;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t q = __umul64hi(m, x);
+#else
+    const uint64_t q = (uint64_t)(((unsigned __int128)m * x) >> 64);
+#endif
+    if (add) return (((x - q) >> 1) + q) >> shift;
+    return q >> shift;
+  }
+};
 
 // Everything the round kernels need, passed by value as a kernel argument.
 struct DevSim {
@@ -155,37 +216,32 @@ struct DevSim {
   const uint32_t* dns_val;
   uint32_t dns_mask;
   uint32_t pad1;
-  // host state, SoA [nH] (slots/buckets: [k * nH + h])
-  uint64_t *rng0, *rng1, *rng2, *rng3;
-  uint64_t* eid;
-  uint64_t* app_k;
-  uint64_t* slot_t;
-  uint64_t* slot_e;
-  uint32_t* flags;
-  uint32_t *ro_dst, *ro_pay, *ro_tag;
-  uint32_t *ri_src, *ri_pay, *ri_tag;
-  uint64_t* ri_eid;
-  uint64_t *tb_bal, *tb_last, *tb_cap, *tb_inc;  // [2 * nH]: 0 = inet_out, 1 = inet_in
+  // host state, SoA: field f of local host h at hs64[f * nH + h] / hs32[f * nH + h]
+  uint64_t* hs64;        // [H64_N * nH]
+  uint32_t* hs32;        // [H32_N * nH]
   CodelEnt* codel;       // [nH * codel_cap] run ring per host
-  uint32_t *cq_head, *cq_nr, *cq_len;  // head run slot, runs, packets
-  uint64_t *cq_bytes, *cq_ie, *cq_dn, *cq_cur, *cq_prev;
-  FifoEnt* fifo;
-  uint32_t *fq_head, *fq_len;
-  uint64_t *d_tx, *d_rx, *d_app;
-  uint64_t* cnt;
-  uint64_t* trace_seq;
+  FifoEnt* fifo;         // [nH * fifo_cap] send queue per host
+  __host__ __device__ __forceinline__ uint64_t* f64(uint32_t f) const { return hs64 + (size_t)f * nH; }
+  __host__ __device__ __forceinline__ uint32_t* f32(uint32_t f) const { return hs32 + (size_t)f * nH; }
   // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host
-  // group (GROUP consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
+  // group (2^gsh consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
   // ids are indirect (bucket_slab) so the partially consumed last bucket of a window can
   // swap with the spare slab set (Ctrl::keep_slab) instead of being copied.
   EvRec* pool;            // [(NB + 1) * G * CAP]
   uint32_t* slab_n;       // [(NB + 1) * G] fill of slab (s, g)
   uint32_t* bucket_slab;  // [NB] slab id of bucket b
   uint64_t* bucket_min;   // [NB] earliest event in bucket b (INVALID = empty)
-  uint32_t NB, G;
+  uint32_t NB, G;         // NB: a power of two (bucket index = (t / BW) & (NB - 1))
   uint32_t CAP;
-  uint32_t pad2;
+  uint32_t gsh;           // log2(hosts per group); a group is served by one 64-lane wave
+  // per-wave results of k_execute (plain stores, reduced by k_finalize: no same-address
+  // atomics across thousands of waves): next local event, min time kept in the spare slab,
+  // and cumulative {host executions, due runs, sorted segments}
+  uint64_t* w_next;       // [G]
+  uint64_t* w_keep;       // [G]
+  uint64_t* w_cnt;        // [3 * G]
   uint64_t BW;
+  UDiv64 bw_div;          // division by BW
   uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
   uint32_t n_ranks;
   Ctrl* ctrl;
@@ -202,9 +258,10 @@ struct DevSim {
   const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
 
-constexpr uint32_t GROUP = 64;      // hosts per group = lanes of one k_execute wave
-constexpr uint32_t CAP_MAX = 1024;  // event runs per (bucket, group) slab
-constexpr uint32_t LDS_CAP = CAP_MAX;  // one bucket's runs of one group are ordered in LDS
+constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute wave
+// event runs per (bucket, group) slab: one bucket's due runs of a group are ordered in LDS
+// (k_execute's dynamic LDS = CAP * 36 B), so CAP also sets k_execute's occupancy
+constexpr uint32_t CAP_MIN = 64, CAP_MAX = 1024;
 
 }  // namespace sgn
 

@@ -13,7 +13,8 @@ import pathlib
 import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = HERE / "libsgn.so"
+# SGN_LIB overrides the library file (diagnostic builds such as libsgn_diag.so)
+LIB_PATH = pathlib.Path(os.environ["SGN_LIB"]) if os.environ.get("SGN_LIB") else HERE / "libsgn.so"
 
 SIMULATION_START = 946684800 * 1_000_000_000
 EMUTIME_INVALID = 0xFFFFFFFFFFFFFFFF
@@ -60,7 +61,7 @@ class SimConfig(C.Structure):
         ("use_dynamic_runahead", C.c_int32),
         ("out_fifo_cap", C.c_uint32),
         ("codel_cap", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("hosts_per_wave", C.c_uint32),
         ("event_capacity", C.c_uint64),
     ]
 

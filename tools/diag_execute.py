@@ -27,12 +27,20 @@ for r in range(3):
     ctx.check(ctx.L.sgn_debug_stamps(ctx.h, sgn.ptr(out, sgn.C.c_uint64), W, sgn.C.byref(n)))
     s = out.reshape(W, sgn.STAMP_WORDS).astype(np.int64)
     cyc, ev, mx, busy, runs = s[:, 0], s[:, 1], s[:, 2], s[:, 3], s[:, 4]
+    tg, tx = s[:, 5], s[:, 6]
     order = np.argsort(cyc)[::-1]
     print(f"round {r}: waves={W} cycles max={cyc.max()} p50={np.median(cyc):.0f} p99={np.percentile(cyc, 99):.0f}"
           f" events total={ev.sum()} runs total={runs.sum()} max-lane={mx.max()}")
     for i in order[:12]:
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} runs={runs[i]:4d} max_lane={mx[i]:4d}"
-              f" busy_lanes={busy[i]:2d}  cyc/event={cyc[i] / max(ev[i], 1):7.1f}")
+              f" busy_lanes={busy[i]:2d}  cyc/event={cyc[i] / max(ev[i], 1):7.1f} gather={tg[i]} exec={tx[i]}")
+        if s[i, 8:24].any():
+            names = ["ro", "ri", "app", "batch", "hdload", "fqload", "tbref", "poprun"]
+            print("      busiest lane: " + " ".join(f"{n}={s[i, 8 + k]}" for k, n in enumerate(names)))
+            print("      wave sums:    " + " ".join(f"{n}={s[i, 16 + k]}" for k, n in enumerate(names)))
+            tn = ["send", "fwdout", "fwdin", "pop", "app", "load"]
+            print("      busiest lane cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
+    print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
     sel = ev > 0
     A = np.stack([ev[sel], mx[sel], runs[sel], np.ones(sel.sum())], 1)
     coef, *_ = np.linalg.lstsq(A, cyc[sel], rcond=None)
