@@ -134,6 +134,14 @@ struct Pkt {
 // ------------------------------------------------------------------------------------
 // Per-host executor: the host's whole state lives in registers for the round.
 // ------------------------------------------------------------------------------------
+// A lane's LDS slot: the pending digest runs and the digests themselves (touched once per
+// run), and the CoDel queue's cached head and open tail runs.
+struct LaneLDS {
+  sgn_drun run[3];   // tx, rx, app (sgn_workload.h)
+  uint64_t dig[3];   // tx, rx, app digests
+  CodelEnt hd, tl;   // head run being consumed / tail run being extended
+};
+
 struct HostExec {
   const DevSim& S;
   Ctrl* C;
@@ -142,7 +150,7 @@ struct HostExec {
   uint32_t b1, keep_slab;  // the window's last bucket (its new events go to the spare slab)
   // RNG (host/host.rs:234) and counters (host.rs:259-263)
   uint64_t r0, r1, r2, r3;
-  uint64_t eid, app_k;
+  uint64_t eid;
   uint64_t st0, st1, st2, se0, se1, se2;  // local event slots: relay out, relay in, app
   uint32_t fl;
   uint32_t ro_dst, ro_pay, ro_tag;
@@ -150,30 +158,25 @@ struct HostExec {
   uint64_t ri_eid;
   uint64_t tbb0, tbl0, tbb1, tbl1;  // balances / last refills (capacity, increment: memory)
   uint32_t cq_head, cq_nr, cq_len;  // head run slot, runs in the ring, packets queued
-  uint64_t cq_bytes, cq_ie, cq_dn, cq_cur, cq_prev;
+  uint64_t cq_bytes;  // (CoDel drop-state fields: memory, slow path only)
   uint32_t fq_head, fq_len;
-  uint64_t dtx, drx, dapp;
   // per-round counter increments (a host cannot see 2^32 events in one window)
-  uint32_t c_sent, c_loss, c_unknown, c_popped, c_codel, c_deliv, c_ldeliv, c_blocked,
-      c_localev, c_maxcodel;
+  uint32_t c_sent, c_loss, c_popped, c_deliv, c_localev, c_maxcodel;
   uint64_t c_bytes;
-  uint64_t tseq;
-  uint64_t lat_cache;
   // CoDel run cache: the head run being consumed and the tail run being extended live in
   // registers; their ring slots are stale until store() (or until the tail is closed).
-  CodelEnt hd, tl;
   bool hd_valid, tl_open;
-  // pending runs of the run-encoded digests (sgn_workload.h), closed at the end of run():
-  // this lane's three sgn_drun {tx, rx, app} in LDS (registers are the scarce resource)
-  sgn_drun* dr;
+  // state touched O(1) times per run lives in this lane's LDS slot (registers are the
+  // scarce resource: they set how many waves are resident)
+  LaneLDS* L;
 #ifdef SGN_DIAG
   uint32_t dg[DG_N];
   uint32_t dgt[DGT_N];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      sgn_drun* runs)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), dr(runs) {}
+                      LaneLDS* l)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ void load() {
@@ -186,7 +189,6 @@ struct HostExec {
     r2 = S.f64(H_RNG2)[h];
     r3 = S.f64(H_RNG3)[h];
     eid = S.f64(H_EID)[h];
-    app_k = S.f64(H_APPK)[h];
     st0 = S.f64(H_SLOT_T)[h];
     st1 = S.f64(H_SLOT_T)[nH + h];
     st2 = S.f64(H_SLOT_T)[2 * nH + h];
@@ -209,22 +211,15 @@ struct HostExec {
     cq_nr = S.f32(H_CQ_NR)[h];
     cq_len = S.f32(H_CQ_LEN)[h];
     cq_bytes = S.f64(H_CQ_BYTES)[h];
-    cq_ie = S.f64(H_CQ_IE)[h];
-    cq_dn = S.f64(H_CQ_DN)[h];
-    cq_cur = S.f64(H_CQ_CUR)[h];
-    cq_prev = S.f64(H_CQ_PREV)[h];
     fq_head = S.f32(H_FQ_HEAD)[h];
     fq_len = S.f32(H_FQ_LEN)[h];
-    dtx = S.f64(H_D_TX)[h];
-    drx = S.f64(H_D_RX)[h];
-    dapp = S.f64(H_D_APP)[h];
-    c_sent = c_loss = c_unknown = c_popped = c_codel = c_deliv = c_ldeliv = c_blocked =
-        c_localev = c_bytes = 0;
+    L->dig[0] = S.f64(H_D_TX)[h];
+    L->dig[1] = S.f64(H_D_RX)[h];
+    L->dig[2] = S.f64(H_D_APP)[h];
+    c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
     c_maxcodel = (uint32_t)S.f64(H_CNT)[CNT_MAX_CODEL * (size_t)nH + h];
-    tseq = S.trace_on ? S.f64(H_TSEQ)[h] : 0;
-    lat_cache = INVALID;
     hd_valid = tl_open = false;
-    dr[0].n = dr[1].n = dr[2].n = 0;
+    L->run[0].n = L->run[1].n = L->run[2].n = 0;
 #ifdef SGN_DIAG
     for (int i = 0; i < DG_N; i++) dg[i] = 0;
     for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
@@ -238,7 +233,6 @@ struct HostExec {
     S.f64(H_RNG2)[h] = r2;
     S.f64(H_RNG3)[h] = r3;
     S.f64(H_EID)[h] = eid;
-    S.f64(H_APPK)[h] = app_k;
     S.f64(H_SLOT_T)[h] = st0;
     S.f64(H_SLOT_T)[nH + h] = st1;
     S.f64(H_SLOT_T)[2 * nH + h] = st2;
@@ -257,36 +251,30 @@ struct HostExec {
     S.f64(H_TB_LAST)[h] = tbl0;
     S.f64(H_TB_BAL)[nH + h] = tbb1;
     S.f64(H_TB_LAST)[nH + h] = tbl1;
-    if (hd_valid) *cq_slot(0) = hd;
-    if (tl_open) *cq_slot(cq_nr - 1) = tl;
+    if (hd_valid) *cq_slot(0) = L->hd;
+    if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
     S.f32(H_CQ_HEAD)[h] = cq_head;
     S.f32(H_CQ_NR)[h] = cq_nr;
     S.f32(H_CQ_LEN)[h] = cq_len;
     S.f64(H_CQ_BYTES)[h] = cq_bytes;
-    S.f64(H_CQ_IE)[h] = cq_ie;
-    S.f64(H_CQ_DN)[h] = cq_dn;
-    S.f64(H_CQ_CUR)[h] = cq_cur;
-    S.f64(H_CQ_PREV)[h] = cq_prev;
     S.f32(H_FQ_HEAD)[h] = fq_head;
     S.f32(H_FQ_LEN)[h] = fq_len;
-    S.f64(H_D_TX)[h] = dtx;
-    S.f64(H_D_RX)[h] = drx;
-    S.f64(H_D_APP)[h] = dapp;
+    S.f64(H_D_TX)[h] = L->dig[0];
+    S.f64(H_D_RX)[h] = L->dig[1];
+    S.f64(H_D_APP)[h] = L->dig[2];
     uint64_t* c = S.f64(H_CNT);
     const size_t n = nH;
     c[CNT_SENT * n + h] += c_sent;
     c[CNT_LOSS * n + h] += c_loss;
-    c[CNT_UNKNOWN * n + h] += c_unknown;
     c[CNT_POPPED * n + h] += c_popped;
-    c[CNT_CODEL * n + h] += c_codel;
     c[CNT_DELIV * n + h] += c_deliv;
-    c[CNT_LOCAL_DELIV * n + h] += c_ldeliv;
-    c[CNT_BLOCKED * n + h] += c_blocked;
     c[CNT_LOCAL_EV * n + h] += c_localev;
     c[CNT_BYTES * n + h] += c_bytes;
     c[CNT_MAX_CODEL * n + h] = c_maxcodel;
-    if (S.trace_on) S.f64(H_TSEQ)[h] = tseq;
   }
+
+  // rare counters go straight to memory (registers are kept for the per-packet ones)
+  __device__ __forceinline__ void cnt_add(int k, uint32_t v) { S.f64(H_CNT)[(size_t)k * S.nH + h] += v; }
 
   __device__ uint64_t next_local_time() const {
     uint64_t m = st0;
@@ -314,7 +302,7 @@ struct HostExec {
   __device__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
                         uint64_t c) {
     if (!S.trace_on) return;
-    const uint64_t seq = tseq++;
+    const uint64_t seq = S.f64(H_TSEQ)[h]++;
     uint64_t pos = atomicAdd((unsigned long long*)&C->trace_n, 1ULL);
     if (pos >= S.trace_cap) {
       atomicOr(&C->overflow, OVF_TRACE);
@@ -435,25 +423,25 @@ struct HostExec {
       return r.enqueue_ts == now && r.src == src && r.eid + r.count == eid0 &&
              r.payload == payload && r.tag == tag;
     };
-    if (tl_open && continues(tl)) {
-      tl.count += n;
-    } else if (!tl_open && hd_valid && cq_nr == 1 && continues(hd)) {
-      hd.count += n;
+    if (tl_open && continues(L->tl)) {
+      L->tl.count += n;
+    } else if (!tl_open && hd_valid && cq_nr == 1 && continues(L->hd)) {
+      L->hd.count += n;
     } else {
       if (tl_open) {
-        *cq_slot(cq_nr - 1) = tl;
+        *cq_slot(cq_nr - 1) = L->tl;
         tl_open = false;
       }
       if (cq_nr >= S.codel_cap) {
         overflow(OVF_CODEL);
         return;
       }
-      tl.enqueue_ts = now;
-      tl.eid = eid0;
-      tl.src = src;
-      tl.payload = payload;
-      tl.tag = tag;
-      tl.count = n;
+      L->tl.enqueue_ts = now;
+      L->tl.eid = eid0;
+      L->tl.src = src;
+      L->tl.payload = payload;
+      L->tl.tag = tag;
+      L->tl.count = n;
       tl_open = true;
       cq_nr++;
     }
@@ -467,20 +455,20 @@ struct HostExec {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    if (fl & F_CODEL_IE) return now >= cq_ie;
+    if (fl & F_CODEL_IE) return now >= S.f64(H_CQ_IE)[h];
     fl |= F_CODEL_IE;
-    cq_ie = emu_sat_add(now, CODEL_INTERVAL);
+    S.f64(H_CQ_IE)[h] = emu_sat_add(now, CODEL_INTERVAL);
     return false;
   }
   // the head run into registers (queue not empty)
   __device__ __forceinline__ void load_head() {
     if (hd_valid) return;
     if (tl_open && cq_nr == 1) {  // the only run is the open tail: take it over
-      hd = tl;
+      L->hd = L->tl;
       tl_open = false;
     } else {
       DG(DG_HDLOAD);
-      hd = *cq_slot(0);
+      L->hd = *cq_slot(0);
     }
     hd_valid = true;
   }
@@ -491,9 +479,9 @@ struct HostExec {
       return false;
     }
     load_head();
-    const CodelEnt e = hd;
-    hd.eid++;
-    if (--hd.count == 0) {
+    const CodelEnt e = L->hd;
+    L->hd.eid++;
+    if (--L->hd.count == 0) {
       hd_valid = false;
       cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
       cq_nr--;
@@ -509,13 +497,13 @@ struct HostExec {
     return true;
   }
   __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
-    c_codel++;
-    sgn_drun_add_seq(&dapp, dr + 2, now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
+    cnt_add(CNT_CODEL, 1);
+    sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
   __device__ bool codel_was_dropping_recently() const {  // :273-281
     if (!(fl & F_CODEL_DN)) return false;
-    return sat_sub(now, cq_dn) < CODEL_INTERVAL * 16;
+    return sat_sub(now, S.f64(H_CQ_DN)[h]) < CODEL_INTERVAL * 16;
   }
   // CoDelQueue::pop (:125-201)
   __device__ bool codel_pop(Pkt* out) {
@@ -537,24 +525,24 @@ struct HostExec {
       bool nok;
       bool has_n = codel_pop_raw(&n, &nok);
       fl |= F_CODEL_DROP;
-      uint64_t delta = sat_sub(cq_cur, cq_prev);
-      cq_cur = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      uint64_t delta = sat_sub(S.f64(H_CQ_CUR)[h], S.f64(H_CQ_PREV)[h]);
+      S.f64(H_CQ_CUR)[h] = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
       fl |= F_CODEL_DN;
-      cq_dn = codel_law(now, cq_cur);
-      cq_prev = cq_cur;
+      S.f64(H_CQ_DN)[h] = codel_law(now, S.f64(H_CQ_CUR)[h]);
+      S.f64(H_CQ_PREV)[h] = S.f64(H_CQ_CUR)[h];
       if (has_n) *out = n;
       return has_n;
     }
     // drop_from_drop_mode (:172-201)
     bool has_item = true;
     Pkt item = p;
-    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= cq_dn) {
+    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= S.f64(H_CQ_DN)[h]) {
       codel_drop(item);
-      cq_cur++;
+      S.f64(H_CQ_CUR)[h]++;
       bool iok = false;
       has_item = codel_pop_raw(&item, &iok);
       if (has_item && iok)
-        cq_dn = codel_law(cq_dn, cq_cur);
+        S.f64(H_CQ_DN)[h] = codel_law(S.f64(H_CQ_DN)[h], S.f64(H_CQ_CUR)[h]);
       else
         fl &= ~F_CODEL_DROP;
     }
@@ -618,7 +606,7 @@ struct HostExec {
                               uint32_t tag) {
     c_deliv += m;
     c_bytes += (uint64_t)m * payload;
-    sgn_drun_add_seq(&dapp, dr + 2, now, src, e0, m);
+    sgn_drun_add_seq(&L->dig[2], &L->run[2], now, src, e0, m);
     if (S.trace_on)
       for (uint32_t k = 0; k < m; k++) trace(SGN_TRACE_DELIVER, src, 0, now, 0, e0 + k);
     if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
@@ -631,14 +619,14 @@ struct HostExec {
         if (fifo_push(dip, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
           relay_notify<0>();
         else
-          c_blocked++;
+          cnt_add(CNT_BLOCKED, 1);
       }
     }
   }
   __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
-    c_ldeliv++;
-    sgn_drun_flush_seq(&dapp, dr + 2);
-    dapp = sgn_digest3(dapp, now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
+    cnt_add(CNT_LOCAL_DELIV, 1);
+    sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
+    L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
   }
 
   // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) for relay_inet_in:
@@ -658,14 +646,14 @@ struct HostExec {
       } else {
         if (cq_len > 0) {
           load_head();
-          if (sat_sub(now, hd.enqueue_ts) < CODEL_TARGET) {
+          if (sat_sub(now, L->hd.enqueue_ts) < CODEL_TARGET) {
             // Fast path over the head run: every packet of it has the same standing delay
             // (< TARGET: CoDelQueue::pop returns it, clearing interval_end and drop mode,
             // codel_queue.rs:204-262) and wire size, and all removals happen at the same
             // `now`, so after the first comforming_remove (which applies the lazy refill)
             // balance / wire more packets conform; the first that does not is cached.
-            const uint32_t n = hd.count;
-            const uint64_t wire = (uint64_t)hd.payload + SGN_UDP_HEADER_BYTES;
+            const uint32_t n = L->hd.count;
+            const uint64_t wire = (uint64_t)L->hd.payload + SGN_UDP_HEADER_BYTES;
             uint32_t m = n;
             bool blocked = false;
             if (!boot) {
@@ -686,12 +674,12 @@ struct HostExec {
             }
             fl &= ~(F_CODEL_IE | F_CODEL_DROP);
             const uint32_t used = m + (blocked ? 1u : 0u);
-            const CodelEnt r = hd;
-            hd.eid += used;
-            hd.count -= used;
+            const CodelEnt r = L->hd;
+            L->hd.eid += used;
+            L->hd.count -= used;
             cq_len -= used;
             cq_bytes = sat_sub(cq_bytes, (uint64_t)used * wire);
-            if (hd.count == 0) {
+            if (L->hd.count == 0) {
               hd_valid = false;
               cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
               cq_nr--;
@@ -746,8 +734,8 @@ struct HostExec {
     const bool boot = now < S.boot_end;
     uint32_t dst;
     if (!dns_lookup(dst_ip, &dst)) {
-      c_unknown += n;
-      sgn_drun_add_same(&dtx, dr + 0, now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
+      cnt_add(CNT_UNKNOWN, n);
+      sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (S.trace_on)
         for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
       return;
@@ -768,9 +756,9 @@ struct HostExec {
       const uint64_t x = rng_next() >> 11;
       if (can_drop && x >= T) {
         c_loss++;
-        if (run) sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst, deliver, run);
+        if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
         run = 0;
-        sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst | (1ULL << 32), 0, 1);
+        sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
         if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
       } else {
         const uint64_t e = eid++;
@@ -778,15 +766,14 @@ struct HostExec {
         if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
       }
     }
-    if (run) sgn_drun_add_same(&dtx, dr + 0, now, (uint64_t)dst, deliver, run);
+    if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
     const uint32_t nsent = (uint32_t)(eid - eid0);
     if (nsent == 0) return;
     c_sent += nsent;
     // sent packets have consecutive ids (drops take none): one event run record each
     // RUN_MAX packets
     const uint32_t nrec = (nsent + RUN_MAX - 1) / RUN_MAX;
-    if (S.dynamic && delay < lat_cache) {
-      lat_cache = delay;
+    if (S.dynamic) {  // Worker::update_lowest_used_latency (no return value: fire and forget)
       atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
     }
     EvRec* dstp;
@@ -928,7 +915,7 @@ struct HostExec {
   }
 
   __device__ void app_task() {
-    const uint64_t k = app_k++;
+    const uint64_t k = S.f64(H_APPK)[h]++;
     uint32_t dst_ip, payload, tag;
     uint64_t next_delay;
     if (S.tkind == SGN_TRAFFIC_PERIODIC) {
@@ -951,7 +938,7 @@ struct HostExec {
     if (fifo_push(dst_ip, payload, payload, 1, tag))
       relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
     else
-      c_blocked++;
+      cnt_add(CNT_BLOCKED, 1);
     schedule<SLOT_APP>(now + next_delay);
   }
 
@@ -984,7 +971,7 @@ struct HostExec {
           const uint32_t src = e.src;
           const uint64_t eid0 = e.eid;
           c_popped += n;
-          sgn_drun_add_seq(&drx, dr + 1, now, src, eid0, n);
+          sgn_drun_add_seq(&L->dig[1], &L->run[1], now, src, eid0, n);
           if (S.trace_on)
             for (uint32_t k = 0; k < n; k++) trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
           // Router::route_incoming_packet (router/mod.rs:55-57)
@@ -1014,9 +1001,9 @@ struct HostExec {
       }
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
-    sgn_drun_flush_same(&dtx, dr + 0);
-    sgn_drun_flush_seq(&drx, dr + 1);
-    sgn_drun_flush_seq(&dapp, dr + 2);
+    sgn_drun_flush_same(&L->dig[0], &L->run[0]);
+    sgn_drun_flush_seq(&L->dig[1], &L->run[1]);
+    sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
   }
 };
 
@@ -1044,7 +1031,10 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 //  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
 //     segment and local slots, emitting new runs into the calendar / exchange slots;
 //  4. the wave's minimum next local event time goes to Ctrl::round_min.
-__global__ __launch_bounds__(64) void k_execute(DevSim S) {
+__global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg) {
+  // the simulation constants are read from device memory where they are used (a by-value
+  // kernel argument would pin ~90 scalar registers for the whole kernel)
+  const DevSim& S = *Sg;
   Ctrl* C = S.ctrl;
   if (!C->active) return;
   // dynamic LDS sized by the slab capacity S.CAP (a bucket's runs of one group fit a slab)
@@ -1053,7 +1043,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   uint16_t* lb = (uint16_t*)(lev + S.CAP);      // grouped by destination lane (unordered)
   uint16_t* lc = lb + S.CAP;                    // ... ordered inside each destination segment
   __shared__ uint32_t lcnt[64], lstart[64], lcur[64];
-  __shared__ sgn_drun ldr[3 * 64];  // the lanes' pending digest runs
+  __shared__ LaneLDS lslot[64];  // the lanes' LDS slots
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x;
   const uint32_t gsz = 1u << S.gsh;
@@ -1065,6 +1055,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   const uint32_t ks = C->keep_slab;
   const uint32_t gbase = S.lo + (g << S.gsh);  // HostId of lane 0
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt0 = S.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const size_t ik = (size_t)ks * S.G + g;
   EvRec* pk = S.pool + ik * S.CAP;
 
@@ -1075,7 +1066,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
     lmin = t0 < t1 ? t0 : t1;
     lmin = t2 < lmin ? t2 : lmin;
   }
-  HostExec ex(S, h, we, be, ks, ldr + 3 * lane);
+  HostExec ex(S, h, we, be, ks, lslot + lane);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -1184,8 +1175,7 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
   if (loaded) {
     my_min = ex.next_local_time();
     ex.store();
-    n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_unknown + ex.c_deliv + ex.c_localev +
-           ex.c_codel;
+    n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_deliv + ex.c_localev;
   }
   kmin = wave_min_u64(kmin);
   if (S.stamps) {
@@ -1207,6 +1197,8 @@ __global__ __launch_bounds__(64) void k_execute(DevSim S) {
       st[4] = N_all;
       st[5] = t_gather;
       st[6] = t_exec;
+      st[7] = rt0;  // 100 MHz constant clock: wave start / end across the chip
+      st[30] = __builtin_amdgcn_s_memrealtime();
     }
 #ifdef SGN_DIAG
     // the busiest lane's work counts (words 8..15) and the wave's sums (16..23)
@@ -1389,7 +1381,7 @@ int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
   time_begin(ctx, K_EXECUTE);
-  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(64), exec_lds_bytes(S.CAP), st, S);
+  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(64), exec_lds_bytes(S.CAP), st, (const DevSim*)ctx->d_S);
   time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
@@ -1779,6 +1771,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
+  ctx->d_S = dalloc<DevSim>(ctx, 1);
+  if (!ctx->d_S) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+  SGN_HIP(ctx, hipMemcpy(ctx->d_S, &S, sizeof(S), hipMemcpyHostToDevice));
   SGN_HIP(ctx, hipDeviceSynchronize());
   ctx->S = S;
   ctx->sim_ready = true;

@@ -295,6 +295,7 @@ struct sgn_ctx {
   // simulation
   bool sim_ready = false;
   sgn::DevSim S{};
+  void* d_S = nullptr;  // device copy of S (the execute kernel reads it through a pointer)
   std::vector<void*> allocs;
   sgn::Ctrl* h_ctrl = nullptr;  // pinned mirror for reads
   uint64_t trace_cap = 0;

@@ -41,6 +41,14 @@ for r in range(3):
             tn = ["send", "fwdout", "fwdin", "pop", "app", "load"]
             print("      busiest lane cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
+    r0, r1 = s[:, 7], s[:, 30]
+    t0 = r0.min()
+    st_us, en_us = (r0 - t0) / 100.0, (r1 - t0) / 100.0
+    clk = cyc / np.maximum((r1 - r0) / 100.0, 1e-3)  # cycles per us = MHz
+    print(f"   wave start us: p0={st_us.min():.1f} p50={np.median(st_us):.1f} p99={np.percentile(st_us, 99):.1f} max={st_us.max():.1f}"
+          f" | end us: p50={np.median(en_us):.1f} max={en_us.max():.1f} | clock MHz p50={np.median(clk):.0f}")
+    late = np.argsort(en_us)[::-1][:5]
+    print("   last to finish: " + ", ".join(f"w{i} start={st_us[i]:.1f} end={en_us[i]:.1f} cyc={cyc[i]}" for i in late))
     sel = ev > 0
     A = np.stack([ev[sel], mx[sel], runs[sel], np.ones(sel.sum())], 1)
     coef, *_ = np.linalg.lstsq(A, cyc[sel], rcond=None)
