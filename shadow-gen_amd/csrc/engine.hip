@@ -166,6 +166,9 @@ struct HostExec {
   // CoDel run cache: the head run being consumed and the tail run being extended live in
   // registers; their ring slots are stale until store() (or until the tail is closed).
   bool hd_valid, tl_open;
+  // XOR of the returned values of the calendar's atomicMins: returning atomics are
+  // performed at the coherence point before the wave's arrival count (fused round edge)
+  uint64_t sink;
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
@@ -219,6 +222,7 @@ struct HostExec {
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
     c_maxcodel = (uint32_t)S.f64(H_CNT)[CNT_MAX_CODEL * (size_t)nH + h];
     hd_valid = tl_open = false;
+    sink = 0;
     L->run[0].n = L->run[1].n = L->run[2].n = 0;
 #ifdef SGN_DIAG
     for (int i = 0; i < DG_N; i++) dg[i] = 0;
@@ -271,6 +275,7 @@ struct HostExec {
     c[CNT_LOCAL_EV * n + h] += c_localev;
     c[CNT_BYTES * n + h] += c_bytes;
     c[CNT_MAX_CODEL * n + h] = c_maxcodel;
+    if (sink == 0x9e3779b97f4a7c15ULL) C->overflow_info = 0;  // keeps the atomics returning
   }
 
   // rare counters go straight to memory (registers are kept for the per-packet ones)
@@ -774,7 +779,7 @@ struct HostExec {
     // RUN_MAX packets
     const uint32_t nrec = (nsent + RUN_MAX - 1) / RUN_MAX;
     if (S.dynamic) {  // Worker::update_lowest_used_latency (no return value: fire and forget)
-      atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
+      sink ^= atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
     }
     EvRec* dstp;
     uint32_t cap;
@@ -785,8 +790,8 @@ struct HostExec {
       const uint32_t slab = b == b1 ? keep_slab : S.bucket_slab[b];
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
-      atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
-                (unsigned long long)deliver);
+      sink ^= atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
+                        (unsigned long long)deliver);
       dstp = S.pool + idx * S.CAP;
       cap = S.CAP;
     } else {
@@ -1022,6 +1027,128 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return (uint32_t)__popcll(lane ? (m & ((~0ULL) >> (64 - lane))) : 0ULL);
 }
 
+// Round edge on one workgroup (any multiple of 64 threads): bucket bookkeeping, the local
+// minimum next event time over the waves' slots and the calendar, and (advance != 0, single
+// shard) Controller::manager_finished_current_round. sh: LDS scratch of >= 16 u64.
+__device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
+  Ctrl* C = S.ctrl;
+  // the waves' minima: events kept in the spare slab, and next local events
+  uint64_t kk = INVALID, wn = INVALID;
+  for (uint32_t g = threadIdx.x; g < S.G; g += blockDim.x) {
+    const uint64_t a = S.w_keep[g], b = S.w_next[g];
+    kk = a < kk ? a : kk;
+    wn = b < wn ? b : wn;
+  }
+  kk = block_min_u64(kk, sh);
+  wn = block_min_u64(wn, sh);
+  if (threadIdx.x == 0) {
+    const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
+    for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1)) S.bucket_min[b] = INVALID;  // consumed
+    // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
+    const uint32_t old = S.bucket_slab[b1];
+    S.bucket_slab[b1] = C->keep_slab;
+    C->keep_slab = old;
+    S.bucket_min[b1] = C->keep_min < kk ? C->keep_min : kk;
+    C->keep_min = INVALID;
+  }
+  __syncthreads();
+  uint64_t m = INVALID;
+  for (uint32_t b = threadIdx.x; b < S.NB; b += blockDim.x) {
+    const uint64_t bm = S.bucket_min[b];
+    m = bm < m ? bm : m;
+  }
+  m = block_min_u64(m, sh);
+  if (threadIdx.x == 0) {
+    m = wn < m ? wn : m;
+    m = C->round_min < m ? C->round_min : m;
+    C->round_min = m;  // local minimum (reduced across shards when advance == 0)
+    if (advance) {
+      const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
+      C->last_min_next = min_next;
+      // Runahead::get (runahead.rs:44-57)
+      uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
+      ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+      // Controller::manager_finished_current_round (controller.rs:88-112)
+      uint64_t ne = min_next + ra;
+      if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
+      ne = ne < S.end_time ? ne : S.end_time;
+      C->active = min_next < ne ? 1u : 0u;
+      C->ws = min_next;
+      C->we = ne;
+      C->round_min = INVALID;
+      C->rounds++;
+    }
+  }
+}
+
+// finalize_round for the fused single-shard path, run by the last wave of k_execute: the
+// waves' minima come from the chunk slots; every value another wave changed during this
+// launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
+__device__ void finalize_fused(const DevSim& S, uint32_t lane) {
+  Ctrl* C = S.ctrl;
+  const uint32_t nch = (S.G + 63) >> 6;
+  uint64_t kk = INVALID, wn = INVALID;
+  for (uint32_t i = lane; i < nch; i += 64) {
+    const uint64_t a = __hip_atomic_exchange(&S.fin_keep[i], (unsigned long long)INVALID,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_exchange(&S.fin_next[i], (unsigned long long)INVALID,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.fin_cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    kk = a < kk ? a : kk;
+    wn = b < wn ? b : wn;
+  }
+  if (lane == 0) __hip_atomic_store(&S.fin_cnt[nch], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  kk = wave_min_u64(kk);
+  wn = wave_min_u64(wn);
+  const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
+  if (lane == 0) {
+    for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1))
+      __hip_atomic_store(&S.bucket_min[b], (unsigned long long)INVALID, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);  // consumed
+    // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
+    const uint32_t old = S.bucket_slab[b1];
+    S.bucket_slab[b1] = C->keep_slab;
+    C->keep_slab = old;
+    const uint64_t km = __hip_atomic_exchange(&C->keep_min, (unsigned long long)INVALID,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.bucket_min[b1], (unsigned long long)(km < kk ? km : kk),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint64_t m = INVALID;
+  for (uint32_t b = lane; b < S.NB; b += 64) {
+    const uint64_t bm = __hip_atomic_load(&S.bucket_min[b], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    m = bm < m ? bm : m;
+  }
+  m = wave_min_u64(m);
+  if (lane == 0) {
+    m = wn < m ? wn : m;
+    const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
+    C->last_min_next = min_next;
+    // Runahead::get (runahead.rs:44-57)
+    const uint64_t mu = __hip_atomic_load(&C->min_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t ra = (S.dynamic && mu != INVALID) ? mu : S.min_possible;
+    ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+    // Controller::manager_finished_current_round (controller.rs:88-112)
+    uint64_t ne = min_next + ra;
+    if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
+    ne = ne < S.end_time ? ne : S.end_time;
+    C->active = min_next < ne ? 1u : 0u;
+    C->ws = min_next;
+    C->we = ne;
+    C->round_min = INVALID;
+    C->rounds++;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
+  if (!S.ctrl->active) return;
+  __shared__ uint64_t sh[16];
+  finalize_round(S, sh, advance);
+}
+
 // One wave per host group (GROUP consecutive hosts), lane = host. A round is:
 //  1. gather: the group's slabs of the window's buckets are read; runs due in the window go
 //     to LDS, the last bucket's later runs move to the spare slab (Ctrl::keep_slab);
@@ -1231,63 +1358,40 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     if (N_all) S.w_cnt[S.G + g] += N_all;
     if (n_sorted) S.w_cnt[2 * (size_t)S.G + g] += n_sorted;
   }
+  if (!S.fuse_finalize) return;
+  // ---- 5. single shard: the last wave to finish runs the round edge (no second launch).
+  // Only device-scope atomics cross between waves here (no fences: an agent-scope release
+  // writes the whole L2 back on gfx950): every wave folds its minima into its chunk's
+  // slots with returning atomics, waits for them, then counts itself in (64 waves per
+  // chunk counter, then chunks); the last arrival reads the slots with atomic loads.
+  uint32_t last = 0;
+  if (lane == 0) {
+    const uint32_t ch = g >> 6;
+    const uint32_t csz = min(64u, S.G - (ch << 6));
+    const uint32_t nch = (S.G + 63) >> 6;
+    if (kmin != INVALID)
+      __hip_atomic_fetch_min(&S.fin_keep[ch], (unsigned long long)kmin, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    if (m != INVALID)
+      __hip_atomic_fetch_min(&S.fin_next[ch], (unsigned long long)m, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t c = __hip_atomic_fetch_add(&S.fin_cnt[ch], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (c == csz - 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(&S.fin_cnt[nch], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      last = t == nch - 1 ? 1u : 0u;
+    }
+  }
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  finalize_fused(S, lane);
 }
 
 // Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
 // window; multi-shard runs reduce C->round_min/min_used across ranks first.
-__global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  __shared__ uint64_t sh[16];
-  // the waves' minima: events kept in the spare slab, and next local events
-  uint64_t kk = INVALID, wn = INVALID;
-  for (uint32_t g = threadIdx.x; g < S.G; g += blockDim.x) {
-    const uint64_t a = S.w_keep[g], b = S.w_next[g];
-    kk = a < kk ? a : kk;
-    wn = b < wn ? b : wn;
-  }
-  kk = block_min_u64(kk, sh);
-  wn = block_min_u64(wn, sh);
-  if (threadIdx.x == 0) {
-    const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
-    for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1)) S.bucket_min[b] = INVALID;  // consumed
-    // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
-    const uint32_t old = S.bucket_slab[b1];
-    S.bucket_slab[b1] = C->keep_slab;
-    C->keep_slab = old;
-    S.bucket_min[b1] = C->keep_min < kk ? C->keep_min : kk;
-    C->keep_min = INVALID;
-  }
-  __syncthreads();
-  uint64_t m = INVALID;
-  for (uint32_t b = threadIdx.x; b < S.NB; b += blockDim.x) {
-    const uint64_t bm = S.bucket_min[b];
-    m = bm < m ? bm : m;
-  }
-  m = block_min_u64(m, sh);
-  if (threadIdx.x == 0) {
-    m = wn < m ? wn : m;
-    m = C->round_min < m ? C->round_min : m;
-    C->round_min = m;  // local minimum (reduced across shards when advance == 0)
-    if (advance) {
-      const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
-      C->last_min_next = min_next;
-      // Runahead::get (runahead.rs:44-57)
-      uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
-      ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
-      // Controller::manager_finished_current_round (controller.rs:88-112)
-      uint64_t ne = min_next + ra;
-      if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
-      ne = ne < S.end_time ? ne : S.end_time;
-      C->active = min_next < ne ? 1u : 0u;
-      C->ws = min_next;
-      C->we = ne;
-      C->round_min = INVALID;
-      C->rounds++;
-    }
-  }
-}
-
 // Multi-shard: window advance from the all-reduced {min_next, min_used}.
 __global__ void k_advance(DevSim S, const uint64_t* red) {
   Ctrl* C = S.ctrl;
@@ -1388,9 +1492,7 @@ int launch_round(sgn_ctx* ctx) {
     int rc = comm_round_exchange(ctx);
     if (rc) return rc;
   } else {
-    time_begin(ctx, K_FINALIZE);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, st, S, 1);
-    time_end(ctx);
+    // single shard: k_execute's last wave runs the round edge (finalize_round)
   }
   SGN_HIP(ctx, hipGetLastError());
   ctx->rounds_enqueued++;
@@ -1771,6 +1873,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
+  S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
+  S.fin_cnt = dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
+  {
+    std::vector<uint64_t> inv((G + 63) / 64, INVALID);
+    if ((rc = up64(inv, &S.fin_keep)) || (rc = up64(inv, &S.fin_next))) return rc;
+  }
+  if (!S.fin_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   ctx->d_S = dalloc<DevSim>(ctx, 1);
   if (!ctx->d_S) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   SGN_HIP(ctx, hipMemcpy(ctx->d_S, &S, sizeof(S), hipMemcpyHostToDevice));

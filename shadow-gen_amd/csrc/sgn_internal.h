@@ -240,6 +240,11 @@ struct DevSim {
   uint64_t* w_next;       // [G]
   uint64_t* w_keep;       // [G]
   uint64_t* w_cnt;        // [3 * G]
+  uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
+  uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
+  uint64_t* fin_next;
+  uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
+  uint32_t pad3;
   uint64_t BW;
   UDiv64 bw_div;          // division by BW
   uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
