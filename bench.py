@@ -48,7 +48,7 @@ def build_workload(n_hosts, V, seed=1):
                           req_payload=64, servers=servers,
                           file_bytes=(50 * 1024, 1024 * 1024, 5 * 1024 * 1024))
     cfg = sgn.make_config(3600 * 1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64,
-                          codel_cap=4096, event_capacity=1 << 25)
+                          codel_cap=4096, event_capacity=1 << 24)
     return g, used, hosts, cfg, tr
 
 

@@ -140,6 +140,10 @@ struct LaneLDS {
   sgn_drun run[3];   // tx, rx, app (sgn_workload.h)
   uint64_t dig[3];   // tx, rx, app digests
   CodelEnt hd, tl;   // head run being consumed / tail run being extended
+  uint64_t tbc[4];   // token buckets' refill increments [2] and capacities [2]
+  FifoEnt fh;        // copy of the send queue's head entry ...
+  uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
+  uint32_t pad[3];
 };
 
 struct HostExec {
@@ -172,14 +176,15 @@ struct HostExec {
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
+  const uint32_t* bslab;  // bucket -> slab table (an LDS copy when NB is small)
 #ifdef SGN_DIAG
   uint32_t dg[DG_N];
   uint32_t dgt[DGT_N];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS* l)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l) {}
+                      LaneLDS* l, const uint32_t* bs)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ void load() {
@@ -216,12 +221,27 @@ struct HostExec {
     cq_bytes = S.f64(H_CQ_BYTES)[h];
     fq_head = S.f32(H_FQ_HEAD)[h];
     fq_len = S.f32(H_FQ_LEN)[h];
+    // prefetched with the rest of the state (no dependent round trip later in the round):
+    // token-bucket constants, the CoDel queue's head run, the send queue's head entry
+    L->tbc[0] = S.f64(H_TB_INC)[h];
+    L->tbc[1] = S.f64(H_TB_INC)[nH + h];
+    L->tbc[2] = S.f64(H_TB_CAP)[h];
+    L->tbc[3] = S.f64(H_TB_CAP)[nH + h];
     L->dig[0] = S.f64(H_D_TX)[h];
     L->dig[1] = S.f64(H_D_RX)[h];
     L->dig[2] = S.f64(H_D_APP)[h];
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
     c_maxcodel = (uint32_t)S.f64(H_CNT)[CNT_MAX_CODEL * (size_t)nH + h];
     hd_valid = tl_open = false;
+    if (cq_nr > 0) {
+      L->hd = *cq_slot(0);
+      hd_valid = true;
+    }
+    L->fh_idx = NO_HOST;
+    if (fq_len > 0) {
+      L->fh = *fq_slot(0);
+      L->fh_idx = fq_head;
+    }
     sink = 0;
     L->run[0].n = L->run[1].n = L->run[2].n = 0;
 #ifdef SGN_DIAG
@@ -374,12 +394,12 @@ struct HostExec {
     uint64_t span = now - last;
     if (span >= interval) {
       DG(DG_TBREF);
-      const uint64_t inc = S.f64(H_TB_INC)[(size_t)W * S.nH + h];
+      const uint64_t inc = L->tbc[W];
       uint64_t nref = span / interval;
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
       if (b < bal) b = ~0ULL;
-      const uint64_t cap = S.f64(H_TB_CAP)[(size_t)W * S.nH + h];
+      const uint64_t cap = L->tbc[2 + W];
       bal = b > cap ? cap : b;
       uint64_t adv = mul_sat(interval, nref, SIMTIME_MAX);
       last = emu_sat_add(last, adv);
@@ -388,7 +408,7 @@ struct HostExec {
     uint64_t next_refill_span = interval - span;
     if (dec > bal) {
       // compute_conforming_duration (:91-117)
-      const uint64_t inc = S.f64(H_TB_INC)[(size_t)W * S.nH + h];
+      const uint64_t inc = L->tbc[W];
       uint64_t req = dec - bal;
       uint64_t n;
       if (((req | inc) >> 32) == 0) {  // u32 division: the u64 routine is long
@@ -561,34 +581,30 @@ struct HostExec {
     if (idx >= S.fifo_cap) idx -= S.fifo_cap;
     return S.fifo + (size_t)h * S.fifo_cap + idx;
   }
-  __device__ bool fifo_push(uint32_t dst_ip, uint32_t payload, uint32_t last, uint32_t count,
+  __device__ bool fifo_push(uint32_t dst, uint32_t payload, uint32_t last, uint32_t count,
                             uint32_t tag) {
     if (fq_len >= S.fifo_cap) return false;
     FifoEnt e;
-    e.dst_ip = dst_ip;
+    e.dst = dst;
     e.pay = (payload & 0xFFFFu) | (last << 16);
     e.count = count;
     e.tag = tag;
     *fq_slot(fq_len) = e;
+    if (fq_len == 0) {  // the new head: keep its copy
+      L->fh = e;
+      L->fh_idx = fq_head;
+    }
     fq_len++;
     return true;
   }
-  __device__ bool fifo_pop(Pkt* p) {
-    if (fq_len == 0) return false;
-    FifoEnt* s = fq_slot(0);
-    FifoEnt e = *s;
-    p->src = gid;
-    p->dst_ip = e.dst_ip;
-    p->payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
-    p->tag = e.tag;
-    p->eid = 0;
-    if (e.count == 1) {
-      fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
-      fq_len--;
-    } else {
-      s->count = e.count - 1;
-    }
-    return true;
+  // the head entry (from the LDS copy when it is current)
+  __device__ __forceinline__ FifoEnt fifo_head() {
+    if (L->fh_idx == fq_head) return L->fh;
+    DG(DG_FQLOAD);
+    const FifoEnt e = *fq_slot(0);
+    L->fh = e;
+    L->fh_idx = fq_head;
+    return e;
   }
 
   // ---- Dns::addr_to_host_id (network/dns.rs:174) ----
@@ -619,9 +635,8 @@ struct HostExec {
       const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
       if (n == 0) return;
       const uint32_t last = (uint32_t)(size - (n - 1) * SGN_TGEN_MSS);
-      const uint32_t dip = S.ip[src];
       for (uint32_t k = 0; k < m; k++) {
-        if (fifo_push(dip, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
+        if (fifo_push(src, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
           relay_notify<0>();
         else
           cnt_add(CNT_BLOCKED, 1);
@@ -728,17 +743,17 @@ struct HostExec {
   // digest takes runs of equal outcomes. Sent packets take consecutive source event ids and
   // share one delivery time, so their events are reserved with one atomic and written as
   // one contiguous run.
-  __device__ void send_batch(uint32_t dst_ip, uint32_t payload, uint32_t tag, uint32_t n) {
+  __device__ void send_batch(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
     DGT_BEGIN(t0);
-    send_batch_(dst_ip, payload, tag, n);
+    send_batch_(dst, payload, tag, n);
     DGT_END(DGT_SEND, t0);
   }
-  __device__ void send_batch_(uint32_t dst_ip, uint32_t payload, uint32_t tag, uint32_t n) {
+  // dst: the HostId the address resolves to (FifoEnt), NO_HOST: not in the simulation
+  __device__ void send_batch_(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
     if (n == 0 || now >= S.end_time) return;
     DG(DG_BATCH);
     const bool boot = now < S.boot_end;
-    uint32_t dst;
-    if (!dns_lookup(dst_ip, &dst)) {
+    if (dst == NO_HOST) {  // resolve_ip_to_host_id failed: InetDropped (worker.rs:347-357)
       cnt_add(CNT_UNKNOWN, n);
       sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (S.trace_on)
@@ -787,7 +802,7 @@ struct HostExec {
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
       const uint32_t b = bucket_of(S, deliver);
-      const uint32_t slab = b == b1 ? keep_slab : S.bucket_slab[b];
+      const uint32_t slab = b == b1 ? keep_slab : bslab[b];
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
       sink ^= atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
@@ -832,7 +847,7 @@ struct HostExec {
     set_relay_state<0>(RELAY_FORWARDING);
     if (fl & F_RO_NEXT) {
       fl &= ~F_RO_NEXT;
-      const bool is_local = ro_dst == my_ip;
+      const bool is_local = ro_dst == gid;
       if (!boot && !is_local) {
         if (!tb_remove<0>((uint64_t)ro_pay + SGN_UDP_HEADER_BYTES, dur)) {
           fl |= F_RO_NEXT;
@@ -842,7 +857,7 @@ struct HostExec {
       }
       Pkt p;
       p.src = gid;
-      p.dst_ip = ro_dst;
+      p.dst_ip = my_ip;
       p.payload = ro_pay;
       p.tag = ro_tag;
       p.eid = 0;
@@ -852,13 +867,11 @@ struct HostExec {
         send_batch(ro_dst, ro_pay, ro_tag, 1);
     }
     while (fq_len > 0) {
-      DG(DG_FQLOAD);
-      FifoEnt* s = fq_slot(0);
-      const FifoEnt e = *s;
+      const FifoEnt e = fifo_head();
       const uint32_t run = e.count == 1 ? 1u : e.count - 1;
       const uint32_t payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
       const uint64_t wire = (uint64_t)payload + SGN_UDP_HEADER_BYTES;
-      const bool is_local = e.dst_ip == my_ip;
+      const bool is_local = e.dst == gid;
       uint32_t n_ok = run;
       bool blocked = false;
       if (!boot && !is_local) {
@@ -880,24 +893,25 @@ struct HostExec {
       if (is_local) {
         Pkt p;
         p.src = gid;
-        p.dst_ip = e.dst_ip;
+        p.dst_ip = my_ip;
         p.payload = payload;
         p.tag = e.tag;
         p.eid = 0;
         for (uint32_t j = 0; j < n_ok; j++) deliver_local(p);
       } else {
-        send_batch(e.dst_ip, payload, e.tag, n_ok);
+        send_batch(e.dst, payload, e.tag, n_ok);
       }
       const uint32_t consumed = n_ok + (blocked ? 1u : 0u);
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         fq_len--;
       } else {
-        s->count = e.count - consumed;
+        fq_slot(0)->count = e.count - consumed;
+        L->fh.count = e.count - consumed;
       }
       if (blocked) {
         fl |= F_RO_NEXT;
-        ro_dst = e.dst_ip;
+        ro_dst = e.dst;
         ro_pay = payload;
         ro_tag = e.tag;
         set_relay_state<0>(RELAY_IDLE);
@@ -921,26 +935,25 @@ struct HostExec {
 
   __device__ void app_task() {
     const uint64_t k = S.f64(H_APPK)[h]++;
-    uint32_t dst_ip, payload, tag;
+    uint32_t dst, payload, tag;
     uint64_t next_delay;
     if (S.tkind == SGN_TRAFFIC_PERIODIC) {
       uint32_t peer = 0, uip = 0;
-      if (sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip))
-        dst_ip = S.ip[peer];
-      else
-        dst_ip = uip;
+      // an address outside the simulation (10.255.0.0/16, never registered) is NO_HOST
+      dst = sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip)
+                ? peer : NO_HOST;
       payload = S.payload_len;
       tag = SGN_TAG_DATA;
       next_delay = S.period;
     } else {
       uint32_t si = 0, cls = 0;
       sgn_tgen_fetch(S.flow_seed, gid, k, S.n_servers, &si, &cls);
-      dst_ip = S.ip[S.servers[si]];
+      dst = S.servers[si];
       payload = S.req_payload;
       tag = SGN_TAG_REQ | cls;
       next_delay = sgn_tgen_think(S.flow_seed, gid, k, S.period, S.period_jitter);
     }
-    if (fifo_push(dst_ip, payload, payload, 1, tag))
+    if (fifo_push(dst, payload, payload, 1, tag))
       relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
     else
       cnt_add(CNT_BLOCKED, 1);
@@ -1171,6 +1184,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   uint16_t* lc = lb + S.CAP;                    // ... ordered inside each destination segment
   __shared__ uint32_t lcnt[64], lstart[64], lcur[64];
   __shared__ LaneLDS lslot[64];  // the lanes' LDS slots
+  __shared__ uint32_t lbs[LDS_BSLAB];  // bucket -> slab table for this round's sends
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x;
   const uint32_t gsz = 1u << S.gsh;
@@ -1193,7 +1207,10 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     lmin = t0 < t1 ? t0 : t1;
     lmin = t2 < lmin ? t2 : lmin;
   }
-  HostExec ex(S, h, we, be, ks, lslot + lane);
+  const bool bs_lds = S.NB <= LDS_BSLAB;
+  if (bs_lds)
+    for (uint32_t i = lane; i < S.NB; i += 64) lbs[i] = S.bucket_slab[i];
+  HostExec ex(S, h, we, be, ks, lslot + lane, bs_lds ? lbs : S.bucket_slab);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;

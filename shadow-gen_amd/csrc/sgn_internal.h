@@ -57,9 +57,13 @@ struct __attribute__((aligned(16))) CodelEnt {
 };
 static_assert(sizeof(CodelEnt) == 32, "");
 
-// One entry of the synthetic socket send queue (a train of `count` datagrams).
+// One entry of the synthetic socket send queue (a train of `count` datagrams). The peer is
+// resolved to its HostId when the datagram is queued: Dns::addr_to_host_id
+// (network/dns.rs:174) is a pure function of the address and host addresses are unique
+// (dns.rs:97-131), so resolving at enqueue gives Worker::send_packet the same HostId.
+constexpr uint32_t NO_HOST = 0xFFFFFFFFu;  // address not in the simulation (InetDropped)
 struct __attribute__((aligned(16))) FifoEnt {
-  uint32_t dst_ip;
+  uint32_t dst;    // destination HostId, or NO_HOST
   uint32_t pay;    // payload (low 16) | last payload (high 16)
   uint32_t count;
   uint32_t tag;
@@ -129,7 +133,7 @@ enum : uint32_t {
 };
 // per-host u32 fields (DevSim::f32)
 enum : uint32_t {
-  H_FLAGS = 0, H_RO_DST, H_RO_PAY, H_RO_TAG, H_RI_SRC, H_RI_PAY, H_RI_TAG,
+  H_FLAGS = 0, H_RO_DST /* HostId */, H_RO_PAY, H_RO_TAG, H_RI_SRC, H_RI_PAY, H_RI_TAG,
   H_CQ_HEAD, H_CQ_NR, H_CQ_LEN, H_FQ_HEAD, H_FQ_LEN,
   H32_N
 };
@@ -267,6 +271,8 @@ constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute
 // event runs per (bucket, group) slab: one bucket's due runs of a group are ordered in LDS
 // (k_execute's dynamic LDS = CAP * 36 B), so CAP also sets k_execute's occupancy
 constexpr uint32_t CAP_MIN = 64, CAP_MAX = 1024;
+constexpr uint32_t LDS_BSLAB = 256;  // calendars with up to this many buckets keep their
+                                     // bucket -> slab table in k_execute's LDS
 
 }  // namespace sgn
 
