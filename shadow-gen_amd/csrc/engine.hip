@@ -176,7 +176,7 @@ struct HostExec {
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
-  const uint32_t* bslab;  // bucket -> slab table (an LDS copy when NB is small)
+  const uint32_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
 #ifdef SGN_DIAG
   uint32_t dg[DG_N];
   uint32_t dgt[DGT_N];
@@ -802,7 +802,7 @@ struct HostExec {
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
       const uint32_t b = bucket_of(S, deliver);
-      const uint32_t slab = b == b1 ? keep_slab : bslab[b];
+      const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : S.bucket_slab[b]);
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
       sink ^= atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const bool bs_lds = S.NB <= LDS_BSLAB;
   if (bs_lds)
     for (uint32_t i = lane; i < S.NB; i += 64) lbs[i] = S.bucket_slab[i];
-  HostExec ex(S, h, we, be, ks, lslot + lane, bs_lds ? lbs : S.bucket_slab);
+  HostExec ex(S, h, we, be, ks, lslot + lane, lbs);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -1716,8 +1716,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (min_possible == 0) return set_error(ctx, SGN_EINVAL, "route latency 0 (Runahead::new asserts)");
 
   // routing (device copies made by sgn_routes_build)
-  S.rlat = ctx->d_lat;
-  S.rloss = ctx->d_loss;
+  S.rlat = (decltype(S.rlat))ctx->d_lat;
+  S.rloss = (decltype(S.rloss))ctx->d_loss;
   uint32_t* d_unode = dalloc<uint32_t>(ctx, N);
   uint32_t* d_ip = dalloc<uint32_t>(ctx, N);
   uint32_t* d_dk = dalloc<uint32_t>(ctx, ctx->dns_key.size());
@@ -1727,10 +1727,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   SGN_HIP(ctx, hipMemcpy(d_ip, ctx->ip.data(), N * 4, hipMemcpyHostToDevice));
   SGN_HIP(ctx, hipMemcpy(d_dk, ctx->dns_key.data(), ctx->dns_key.size() * 4, hipMemcpyHostToDevice));
   SGN_HIP(ctx, hipMemcpy(d_dv, ctx->dns_val.data(), ctx->dns_val.size() * 4, hipMemcpyHostToDevice));
-  S.unode = d_unode;
-  S.ip = d_ip;
-  S.dns_key = d_dk;
-  S.dns_val = d_dv;
+  S.unode = (decltype(S.unode))d_unode;
+  S.ip = (decltype(S.ip))d_ip;
+  S.dns_key = (decltype(S.dns_key))d_dk;
+  S.dns_val = (decltype(S.dns_val))d_dv;
   S.dns_mask = ctx->dns_mask;
   std::vector<uint8_t> is_server(N, 0);
   if (tr->kind == SGN_TRAFFIC_TGEN) {
@@ -1741,7 +1741,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       is_server[tr->server_hosts[i]] = 1;
     }
     SGN_HIP(ctx, hipMemcpy(d_sv, tr->server_hosts, tr->n_servers * 4, hipMemcpyHostToDevice));
-    S.servers = d_sv;
+    S.servers = (decltype(S.servers))d_sv;
   }
 
   // ---- per-host state, initialised on the host ----
@@ -1779,25 +1779,25 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       }
     }
   }
-  auto up64 = [&](const std::vector<uint64_t>& v, uint64_t** out) -> int {
-    *out = dalloc<uint64_t>(ctx, v.size());
+  auto up64 = [&](const std::vector<uint64_t>& v, auto* out) -> int {
+    *out = (std::remove_reference_t<decltype(*out)>)dalloc<uint64_t>(ctx, v.size());
     if (!*out) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
-    SGN_HIP(ctx, hipMemcpy(*out, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+    SGN_HIP(ctx, hipMemcpy((void*)*out, v.data(), v.size() * 8, hipMemcpyHostToDevice));
     return 0;
   };
-  auto up32 = [&](const std::vector<uint32_t>& v, uint32_t** out) -> int {
-    *out = dalloc<uint32_t>(ctx, v.size());
+  auto up32 = [&](const std::vector<uint32_t>& v, auto* out) -> int {
+    *out = (std::remove_reference_t<decltype(*out)>)dalloc<uint32_t>(ctx, v.size());
     if (!*out) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
-    SGN_HIP(ctx, hipMemcpy(*out, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    SGN_HIP(ctx, hipMemcpy((void*)*out, v.data(), v.size() * 4, hipMemcpyHostToDevice));
     return 0;
   };
   int rc = 0;
   // the per-host state: one block of u64 fields and one of u32 fields, field f of host h at
   // [f * nH + h] (few base pointers keep the round kernel's scalar registers free)
-  S.hs64 = dalloc<uint64_t>(ctx, (size_t)H64_N * nH);
-  S.hs32 = dalloc<uint32_t>(ctx, (size_t)H32_N * nH);
-  S.codel = dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
-  S.fifo = dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
+  S.hs64 = (decltype(S.hs64))dalloc<uint64_t>(ctx, (size_t)H64_N * nH);
+  S.hs32 = (decltype(S.hs32))dalloc<uint32_t>(ctx, (size_t)H32_N * nH);
+  S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
+  S.fifo = (decltype(S.fifo))dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
   if (!S.hs64 || !S.hs32 || !S.codel || !S.fifo)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   auto put64 = [&](uint32_t f, const std::vector<uint64_t>& v) -> int {
@@ -1836,21 +1836,21 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.CAP = (uint32_t)CAP;
   S.BW = BW;
   S.bw_div.init(BW);
-  S.pool = dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
-  S.w_next = dalloc<uint64_t>(ctx, G);
-  S.w_keep = dalloc<uint64_t>(ctx, G);
-  S.w_cnt = dalloc<uint64_t>(ctx, 3 * G);
+  S.pool = (decltype(S.pool))dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
+  S.w_next = (decltype(S.w_next))dalloc<uint64_t>(ctx, G);
+  S.w_keep = (decltype(S.w_keep))dalloc<uint64_t>(ctx, G);
+  S.w_cnt = (decltype(S.w_cnt))dalloc<uint64_t>(ctx, 3 * G);
   if (!S.w_next || !S.w_keep || !S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
-  S.slab_n = dalloc<uint32_t>(ctx, (NB + 1) * G);
+  S.slab_n = (decltype(S.slab_n))dalloc<uint32_t>(ctx, (NB + 1) * G);
   if (!S.pool || !S.slab_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event calendar)");
   std::vector<uint32_t> bslab(NB);
   for (uint64_t b = 0; b < NB; b++) bslab[b] = (uint32_t)b;
   if ((rc = up32(bslab, &S.bucket_slab))) return rc;
   std::vector<uint64_t> bmin(NB, INVALID);
   if ((rc = up64(bmin, &S.bucket_min))) return rc;
-  if (getenv("SGN_STAMPS")) S.stamps = dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
+  if (getenv("SGN_STAMPS")) S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
   if (ctx->trace_cap) {
-    S.trace = dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
+    S.trace = (decltype(S.trace))dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
     if (!S.trace) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
     S.trace_cap = ctx->trace_cap;
   }
@@ -1864,15 +1864,15 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       sgn_shard_range(N, r < ctx->nranks ? r : ctx->nranks - 1, ctx->nranks, &lo, &hi);
       rl[r] = r < ctx->nranks ? lo : N;
     }
-    if ((rc = up32(rl, (uint32_t**)&S.rank_lo))) return rc;
+    if ((rc = up32(rl, &S.rank_lo))) return rc;
   }
   if (ctx->nranks > 1) {
     if (!ctx->comm) return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init before sgn_sim_init");
     S.xslot = (uint32_t)ctx->xslot;
-    S.xout = dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
-    S.xin = dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
-    S.xout_n = dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
-    S.xin_n = dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
+    S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
+    S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
   }
   Ctrl c{};
@@ -1885,13 +1885,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
   c.remote_min = INVALID;
-  S.ctrl = dalloc<Ctrl>(ctx, 1);
+  S.ctrl = (decltype(S.ctrl))dalloc<Ctrl>(ctx, 1);
   if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
-  S.fin_cnt = dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
+  S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
   {
     std::vector<uint64_t> inv((G + 63) / 64, INVALID);
     if ((rc = up64(inv, &S.fin_keep)) || (rc = up64(inv, &S.fin_next))) return rc;

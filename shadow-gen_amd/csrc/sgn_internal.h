@@ -21,6 +21,14 @@
 
 namespace sgn {
 
+// Device pointers in DevSim carry the global address space in device code, so loads and
+// stores through them are global_* (not flat_*) even though DevSim is read from memory.
+#ifdef __HIP_DEVICE_COMPILE__
+#define SGN_GLB __attribute__((address_space(1)))
+#else
+#define SGN_GLB
+#endif
+
 constexpr uint64_t SIM_START = SGN_SIMULATION_START;
 constexpr uint64_t EMU_MAX = SGN_EMUTIME_MAX;
 constexpr uint64_t INVALID = SGN_EMUTIME_INVALID;
@@ -210,61 +218,61 @@ struct DevSim {
   uint32_t diag_mode;  // diagnostic build only (SGN_DIAG_MODE): 1 = light waves skip
   uint64_t flow_seed, period, period_jitter;
   uint64_t file_bytes[3];
-  const uint32_t* servers;
+  SGN_GLB const uint32_t* servers;
   // routing (replicated on every shard)
-  const uint64_t* rlat;
-  const float* rloss;
-  const uint32_t* unode;  // [n_all] used-node index of every host
-  const uint32_t* ip;     // [n_all]
-  const uint32_t* dns_key;
-  const uint32_t* dns_val;
+  SGN_GLB const uint64_t* rlat;
+  SGN_GLB const float* rloss;
+  SGN_GLB const uint32_t* unode;  // [n_all] used-node index of every host
+  SGN_GLB const uint32_t* ip;     // [n_all]
+  SGN_GLB const uint32_t* dns_key;
+  SGN_GLB const uint32_t* dns_val;
   uint32_t dns_mask;
   uint32_t pad1;
   // host state, SoA: field f of local host h at hs64[f * nH + h] / hs32[f * nH + h]
-  uint64_t* hs64;        // [H64_N * nH]
-  uint32_t* hs32;        // [H32_N * nH]
-  CodelEnt* codel;       // [nH * codel_cap] run ring per host
-  FifoEnt* fifo;         // [nH * fifo_cap] send queue per host
-  __host__ __device__ __forceinline__ uint64_t* f64(uint32_t f) const { return hs64 + (size_t)f * nH; }
-  __host__ __device__ __forceinline__ uint32_t* f32(uint32_t f) const { return hs32 + (size_t)f * nH; }
+  SGN_GLB uint64_t* hs64;        // [H64_N * nH]
+  SGN_GLB uint32_t* hs32;        // [H32_N * nH]
+  SGN_GLB CodelEnt* codel;       // [nH * codel_cap] run ring per host
+  SGN_GLB FifoEnt* fifo;         // [nH * fifo_cap] send queue per host
+  __host__ __device__ __forceinline__ SGN_GLB uint64_t* f64(uint32_t f) const { return hs64 + (size_t)f * nH; }
+  __host__ __device__ __forceinline__ SGN_GLB uint32_t* f32(uint32_t f) const { return hs32 + (size_t)f * nH; }
   // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host
   // group (2^gsh consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
   // ids are indirect (bucket_slab) so the partially consumed last bucket of a window can
   // swap with the spare slab set (Ctrl::keep_slab) instead of being copied.
-  EvRec* pool;            // [(NB + 1) * G * CAP]
-  uint32_t* slab_n;       // [(NB + 1) * G] fill of slab (s, g)
-  uint32_t* bucket_slab;  // [NB] slab id of bucket b
-  uint64_t* bucket_min;   // [NB] earliest event in bucket b (INVALID = empty)
+  SGN_GLB EvRec* pool;            // [(NB + 1) * G * CAP]
+  SGN_GLB uint32_t* slab_n;       // [(NB + 1) * G] fill of slab (s, g)
+  SGN_GLB uint32_t* bucket_slab;  // [NB] slab id of bucket b
+  SGN_GLB uint64_t* bucket_min;   // [NB] earliest event in bucket b (INVALID = empty)
   uint32_t NB, G;         // NB: a power of two (bucket index = (t / BW) & (NB - 1))
   uint32_t CAP;
   uint32_t gsh;           // log2(hosts per group); a group is served by one 64-lane wave
   // per-wave results of k_execute (plain stores, reduced by k_finalize: no same-address
   // atomics across thousands of waves): next local event, min time kept in the spare slab,
   // and cumulative {host executions, due runs, sorted segments}
-  uint64_t* w_next;       // [G]
-  uint64_t* w_keep;       // [G]
-  uint64_t* w_cnt;        // [3 * G]
-  uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
-  uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
-  uint64_t* fin_next;
+  SGN_GLB uint64_t* w_next;       // [G]
+  SGN_GLB uint64_t* w_keep;       // [G]
+  SGN_GLB uint64_t* w_cnt;        // [3 * G]
+  SGN_GLB uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
+  SGN_GLB uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
+  SGN_GLB uint64_t* fin_next;
   uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
   uint32_t pad3;
   uint64_t BW;
   UDiv64 bw_div;          // division by BW
-  uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
+  SGN_GLB uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
   uint32_t n_ranks;
-  Ctrl* ctrl;
+  SGN_GLB Ctrl* ctrl;
   // trace
-  sgn_trace_rec* trace;
+  SGN_GLB sgn_trace_rec* trace;
   uint64_t trace_cap;
   // multi-GPU exchange: out slot r holds events for rank r
-  EvRec* xout;
-  uint32_t* xout_n;  // [n_ranks]
-  EvRec* xin;
-  uint32_t* xin_n;   // [n_ranks] (received counts)
+  SGN_GLB EvRec* xout;
+  SGN_GLB uint32_t* xout_n;  // [n_ranks]
+  SGN_GLB EvRec* xin;
+  SGN_GLB uint32_t* xin_n;   // [n_ranks] (received counts)
   uint32_t xslot;    // events per slot
   uint32_t rank;
-  const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
+  SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
 
 constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute wave
