@@ -331,7 +331,7 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out);
  * events handled, max events of one host, hosts with events, then (diagnostic build
  * libsgn_diag.so only) lane 0's per-event-kind cycles and counts}. Needs SGN_STAMPS=1 in
  * the environment at sgn_sim_init; n = number of waves (0 when disabled), cap in waves. */
-#define SGN_STAMP_WORDS 32
+#define SGN_STAMP_WORDS 48
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n);
 
 #ifdef __cplusplus

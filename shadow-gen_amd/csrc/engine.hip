@@ -142,8 +142,10 @@ struct LaneLDS {
   CodelEnt hd, tl;   // head run being consumed / tail run being extended
   uint64_t tbc[4];   // token buckets' refill increments [2] and capacities [2]
   FifoEnt fh;        // copy of the send queue's head entry ...
+  uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
+  uint64_t rc_T;
   uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
-  uint32_t pad[3];
+  uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
 };
 
 struct HostExec {
@@ -180,6 +182,7 @@ struct HostExec {
 #ifdef SGN_DIAG
   uint32_t dg[DG_N];
   uint32_t dgt[DGT_N];
+  uint32_t wk[5];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
@@ -223,6 +226,9 @@ struct HostExec {
     fq_len = S.f32(H_FQ_LEN)[h];
     // prefetched with the rest of the state (no dependent round trip later in the round):
     // token-bucket constants, the CoDel queue's head run, the send queue's head entry
+    L->rc_dst = S.f32(H_RC_DST)[h];
+    L->rc_lat = S.f64(H_RC_LAT)[h];
+    L->rc_T = S.f64(H_RC_T)[h];
     L->tbc[0] = S.f64(H_TB_INC)[h];
     L->tbc[1] = S.f64(H_TB_INC)[nH + h];
     L->tbc[2] = S.f64(H_TB_CAP)[h];
@@ -247,6 +253,7 @@ struct HostExec {
 #ifdef SGN_DIAG
     for (int i = 0; i < DG_N; i++) dg[i] = 0;
     for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
+    for (int i = 0; i < 5; i++) wk[i] = 0;
 #endif
   }
 
@@ -283,6 +290,9 @@ struct HostExec {
     S.f64(H_CQ_BYTES)[h] = cq_bytes;
     S.f32(H_FQ_HEAD)[h] = fq_head;
     S.f32(H_FQ_LEN)[h] = fq_len;
+    S.f32(H_RC_DST)[h] = L->rc_dst;
+    S.f64(H_RC_LAT)[h] = L->rc_lat;
+    S.f64(H_RC_T)[h] = L->rc_T;
     S.f64(H_D_TX)[h] = L->dig[0];
     S.f64(H_D_RX)[h] = L->dig[1];
     S.f64(H_D_APP)[h] = L->dig[2];
@@ -760,16 +770,27 @@ struct HostExec {
         for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
       return;
     }
-    const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
-    const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
-    const uint64_t delay = S.rlat[ri];
+    // the route (WorkerShared::latency / reliability, worker.rs:523-537): a train goes to
+    // one peer for many rounds, so the host keeps its last (peer, latency, threshold)
+    uint64_t delay, T;
+    if (L->rc_dst == dst) {
+      delay = L->rc_lat;
+      T = L->rc_T;
+    } else {
+      const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
+      const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
+      delay = S.rlat[ri];
+      // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53:
+      // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an
+      // exact integer T and the test is (x >> 11) >= T, bit for bit the same decision
+      T = (uint64_t)((double)rel32 * 9007199254740992.0);
+      L->rc_dst = dst;
+      L->rc_lat = delay;
+      L->rc_T = T;
+    }
     uint64_t deliver = now + delay;
     if (deliver < we) deliver = we;
     const uint64_t eid0 = eid;
-    // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53:
-    // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an exact
-    // integer T and the test is (x >> 11) >= T, bit for bit the same decision
-    const uint64_t T = (uint64_t)((double)rel32 * 9007199254740992.0);
     const bool can_drop = !boot && payload > 0;
     uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
     for (uint32_t j = 0; j < n; j++) {
@@ -975,6 +996,22 @@ struct HostExec {
       int ls = 0;
       if (st1 < lt || (st1 == lt && se1 < le)) { lt = st1; le = se1; ls = 1; }
       if (st2 < lt || (st2 == lt && se2 < le)) { lt = st2; le = se2; ls = 2; }
+#ifdef SGN_DIAG
+      {  // wave-level: iterations, and iterations in which some lane runs each handler
+        const bool ispop = pi < s1 && ev[ord[pi]].time <= lt;
+        const int kind = ispop ? 0 : (lt >= until ? 4 : 1 + ls);
+        const uint64_t act = __ballot(1);
+        const uint64_t b0 = __ballot(kind == 0), b1 = __ballot(kind == 1),
+                       b2 = __ballot(kind == 2), b3 = __ballot(kind == 3);
+        if ((uint32_t)(__ffsll((long long)act) - 1) == (threadIdx.x & 63)) {
+          wk[0]++;
+          wk[1] += b0 != 0;
+          wk[2] += b1 != 0;
+          wk[3] += b2 != 0;
+          wk[4] += b3 != 0;
+        }
+      }
+#endif
       if (pi < s1) {
         const EvRec& e = ev[ord[pi]];
         if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
@@ -1216,6 +1253,9 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   uint64_t kmin = INVALID;
 
   uint64_t t_gather = 0, t_exec = 0;
+#ifdef SGN_DIAG
+  uint64_t w_load = 0, w_run = 0;
+#endif
   for (uint32_t bi = 0; bi < nbk; bi++) {
     const uint64_t c0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t b = (bs + bi) & (S.NB - 1);
@@ -1293,19 +1333,29 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     __syncthreads();
     // ---- 3. execute the sub-window [.., sub_end) ----
     const uint64_t c1 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#ifdef SGN_DIAG
+    // wave-level phase times (the loads are drained inside the load phase here)
+    const bool go = valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end);
+    const uint64_t ta = __builtin_amdgcn_s_memtime();
+    if (go && !loaded) {
+      ex.load();
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      loaded = true;
+    }
+    const uint64_t tb = __builtin_amdgcn_s_memtime();
+    if (go) ex.run(lev, lc, start, start + cnt, sub_end);
+    const uint64_t tc = __builtin_amdgcn_s_memtime();
+    w_load += tb - ta;
+    w_run += tc - tb;
+#else
     if (valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end)) {
       if (!loaded) {
-#ifdef SGN_DIAG
-        const uint64_t t0 = __builtin_amdgcn_s_memtime();
         ex.load();
-        ex.dgt[DGT_LOAD] += (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
-#else
-        ex.load();
-#endif
         loaded = true;
       }
       ex.run(lev, lc, start, start + cnt, sub_end);
     }
+#endif
     __syncthreads();  // LDS is reused by the next bucket
     if (S.stamps) {
       const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -1316,11 +1366,18 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
 
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
   uint32_t n_ev = 0;
+#ifdef SGN_DIAG
+  const uint64_t td = __builtin_amdgcn_s_memtime();
+#endif
   if (loaded) {
     my_min = ex.next_local_time();
     ex.store();
     n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_deliv + ex.c_localev;
   }
+#ifdef SGN_DIAG
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const uint64_t w_store = __builtin_amdgcn_s_memtime() - td;
+#endif
   kmin = wave_min_u64(kmin);
   if (S.stamps) {
     // per-wave diagnostics: shader cycles, total and max events over the wave's lanes
@@ -1361,6 +1418,15 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
       const uint32_t v = loaded ? ex.dgt[i] : 0u;
       const uint32_t vb = __shfl(v, bl, 64);
       if (lane == 0) st[24 + i] = vb;
+    }
+    if (lane == 0) {
+      st[32] = w_load;
+      st[33] = w_run;
+      st[34] = w_store;
+    }
+    for (int i = 0; i < 5; i++) {
+      const uint32_t v = wave_sum_u32(loaded ? ex.wk[i] : 0u);
+      if (lane == 0) st[35 + i] = v;
     }
 #endif
   }
@@ -1812,6 +1878,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       (rc = put64(H_D_TX, dig)) || (rc = put64(H_D_RX, dig)) || (rc = put64(H_D_APP, dig)))
     return rc;
   SGN_HIP(ctx, hipMemcpy(S.f32(H_FLAGS), flags.data(), (size_t)nH * 4, hipMemcpyHostToDevice));
+  {
+    std::vector<uint32_t> none(nH, NO_HOST);  // empty route caches
+    SGN_HIP(ctx, hipMemcpy(S.f32(H_RC_DST), none.data(), (size_t)nH * 4, hipMemcpyHostToDevice));
+  }
 
   // ---- calendar: bucket width >= any window length, horizon > max latency ----
   // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least

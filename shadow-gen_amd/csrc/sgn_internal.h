@@ -136,6 +136,7 @@ enum : uint32_t {
   H_CQ_BYTES = H_TB_INC + 2, H_CQ_IE, H_CQ_DN, H_CQ_CUR, H_CQ_PREV,  // CoDel state
   H_D_TX, H_D_RX, H_D_APP,             // digests
   H_TSEQ,                              // trace sequence
+  H_RC_LAT, H_RC_T,                    // route cache: latency, loss threshold
   H_CNT,                               // counters [NCNT]
   H64_N = H_CNT + NCNT
 };
@@ -143,6 +144,7 @@ enum : uint32_t {
 enum : uint32_t {
   H_FLAGS = 0, H_RO_DST /* HostId */, H_RO_PAY, H_RO_TAG, H_RI_SRC, H_RI_PAY, H_RI_TAG,
   H_CQ_HEAD, H_CQ_NR, H_CQ_LEN, H_FQ_HEAD, H_FQ_LEN,
+  H_RC_DST,                            // route cache: peer HostId (NO_HOST: empty)
   H32_N
 };
 

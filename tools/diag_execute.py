@@ -13,7 +13,7 @@ import bench
 import sgn
 
 g, used, hosts, cfg, tr = bench.build_workload(int(sys.argv[1]) if len(sys.argv) > 1 else 100_000, 1000)
-ctx = sgn.Context()
+ctx = sgn.Context(flags=2)
 ctx.routes_build(g, used)
 ctx.hosts_set(hosts)
 ctx.sim_init(cfg, tr)
@@ -22,7 +22,10 @@ n = sgn.C.c_uint64()
 ctx.check(ctx.L.sgn_debug_stamps(ctx.h, None, 0, sgn.C.byref(n)))
 W = n.value
 for r in range(3):
+    k0 = ctx.kernel_times()["k_execute"]
     ctx.round()
+    k1 = ctx.kernel_times()["k_execute"]
+    print(f"k_execute event-timed: {(k1[1] - k0[1]) * 1e3:.1f} us")
     out = np.zeros(sgn.STAMP_WORDS * W, dtype=np.uint64)
     ctx.check(ctx.L.sgn_debug_stamps(ctx.h, sgn.ptr(out, sgn.C.c_uint64), W, sgn.C.byref(n)))
     s = out.reshape(W, sgn.STAMP_WORDS).astype(np.int64)
@@ -41,6 +44,16 @@ for r in range(3):
             tn = ["send", "fwdout", "fwdin", "pop", "app", "load"]
             print("      busiest lane cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
+    if s[:, 32:35].any():
+        wl, wr, ws_ = s[:, 32], s[:, 33], s[:, 34]
+        print(f"   wave phases (diag build) median: load={np.median(wl):.0f} run={np.median(wr):.0f} store={np.median(ws_):.0f}"
+              f" | p99: load={np.percentile(wl, 99):.0f} run={np.percentile(wr, 99):.0f} store={np.percentile(ws_, 99):.0f}")
+        it = s[:, 35:40]
+        print(f"   wave loop iterations median: all={np.median(it[:, 0]):.0f} pop={np.median(it[:, 1]):.0f} ro={np.median(it[:, 2]):.0f} ri={np.median(it[:, 3]):.0f} app={np.median(it[:, 4]):.0f}"
+              f" | run cycles/iteration median={np.median(wr / np.maximum(it[:, 0], 1)):.0f}")
+        top = np.argsort(cyc)[::-1][:3]
+        for i in top:
+            print(f"     top wave {i}: iters={it[i].tolist()} run={wr[i]} cyc/iter={wr[i] / max(it[i, 0], 1):.0f}")
     r0, r1 = s[:, 7], s[:, 30]
     t0 = r0.min()
     st_us, en_us = (r0 - t0) / 100.0, (r1 - t0) / 100.0
