@@ -104,6 +104,12 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int off) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, off, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), off, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -178,6 +184,7 @@ struct HostExec {
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
+  SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint32_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
 #ifdef SGN_DIAG
   uint32_t dg[DG_N];
@@ -191,53 +198,55 @@ struct HostExec {
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ void load() {
-    const uint32_t nH = S.nH;
+    R = S.hrec + h;
+    const HostRec& r = *R;
     gid = S.lo + h;
-    my_ip = S.ip[gid];
-    my_unode = S.unode[gid];
-    r0 = S.f64(H_RNG0)[h];
-    r1 = S.f64(H_RNG1)[h];
-    r2 = S.f64(H_RNG2)[h];
-    r3 = S.f64(H_RNG3)[h];
-    eid = S.f64(H_EID)[h];
-    st0 = S.f64(H_SLOT_T)[h];
-    st1 = S.f64(H_SLOT_T)[nH + h];
-    st2 = S.f64(H_SLOT_T)[2 * nH + h];
-    se0 = S.f64(H_SLOT_E)[h];
-    se1 = S.f64(H_SLOT_E)[nH + h];
-    se2 = S.f64(H_SLOT_E)[2 * nH + h];
-    fl = S.f32(H_FLAGS)[h];
-    ro_dst = S.f32(H_RO_DST)[h];
-    ro_pay = S.f32(H_RO_PAY)[h];
-    ro_tag = S.f32(H_RO_TAG)[h];
-    ri_src = S.f32(H_RI_SRC)[h];
-    ri_pay = S.f32(H_RI_PAY)[h];
-    ri_tag = S.f32(H_RI_TAG)[h];
-    ri_eid = S.f64(H_RI_EID)[h];
-    tbb0 = S.f64(H_TB_BAL)[h];
-    tbl0 = S.f64(H_TB_LAST)[h];
-    tbb1 = S.f64(H_TB_BAL)[nH + h];
-    tbl1 = S.f64(H_TB_LAST)[nH + h];
-    cq_head = S.f32(H_CQ_HEAD)[h];
-    cq_nr = S.f32(H_CQ_NR)[h];
-    cq_len = S.f32(H_CQ_LEN)[h];
-    cq_bytes = S.f64(H_CQ_BYTES)[h];
-    fq_head = S.f32(H_FQ_HEAD)[h];
-    fq_len = S.f32(H_FQ_LEN)[h];
-    // prefetched with the rest of the state (no dependent round trip later in the round):
-    // token-bucket constants, the CoDel queue's head run, the send queue's head entry
-    L->rc_dst = S.f32(H_RC_DST)[h];
-    L->rc_lat = S.f64(H_RC_LAT)[h];
-    L->rc_T = S.f64(H_RC_T)[h];
-    L->tbc[0] = S.f64(H_TB_INC)[h];
-    L->tbc[1] = S.f64(H_TB_INC)[nH + h];
-    L->tbc[2] = S.f64(H_TB_CAP)[h];
-    L->tbc[3] = S.f64(H_TB_CAP)[nH + h];
-    L->dig[0] = S.f64(H_D_TX)[h];
-    L->dig[1] = S.f64(H_D_RX)[h];
-    L->dig[2] = S.f64(H_D_APP)[h];
+    my_ip = r.ip;
+    my_unode = r.unode;
+    r0 = r.rng[0];
+    r1 = r.rng[1];
+    r2 = r.rng[2];
+    r3 = r.rng[3];
+    eid = r.eid;
+    st0 = r.slot_t[0];
+    st1 = r.slot_t[1];
+    st2 = r.slot_t[2];
+    se0 = r.slot_e[0];
+    se1 = r.slot_e[1];
+    se2 = r.slot_e[2];
+    fl = r.flags;
+    ro_dst = r.ro_dst;
+    ro_pay = r.ro_pay;
+    ro_tag = r.ro_tag;
+    ri_src = r.ri_src;
+    ri_pay = r.ri_pay;
+    ri_tag = r.ri_tag;
+    ri_eid = r.ri_eid;
+    tbb0 = r.tb_bal[0];
+    tbl0 = r.tb_last[0];
+    tbb1 = r.tb_bal[1];
+    tbl1 = r.tb_last[1];
+    cq_head = r.cq_head;
+    cq_nr = r.cq_nr;
+    cq_len = r.cq_len;
+    cq_bytes = r.cq_bytes;
+    fq_head = r.fq_head;
+    fq_len = r.fq_len;
+    // with the rest of the record (no dependent round trip later in the round): route
+    // cache, token-bucket constants, digests; then the CoDel queue's head run and the send
+    // queue's head entry
+    L->rc_dst = r.rc_dst;
+    L->rc_lat = r.rc_lat;
+    L->rc_T = r.rc_T;
+    L->tbc[0] = r.tb_inc[0];
+    L->tbc[1] = r.tb_inc[1];
+    L->tbc[2] = r.tb_cap[0];
+    L->tbc[3] = r.tb_cap[1];
+    L->dig[0] = r.dig[0];
+    L->dig[1] = r.dig[1];
+    L->dig[2] = r.dig[2];
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
-    c_maxcodel = (uint32_t)S.f64(H_CNT)[CNT_MAX_CODEL * (size_t)nH + h];
+    c_maxcodel = r.max_codel;
     hd_valid = tl_open = false;
     if (cq_nr > 0) {
       L->hd = *cq_slot(0);
@@ -258,58 +267,54 @@ struct HostExec {
   }
 
   __device__ void store() {
-    const uint32_t nH = S.nH;
-    S.f64(H_RNG0)[h] = r0;
-    S.f64(H_RNG1)[h] = r1;
-    S.f64(H_RNG2)[h] = r2;
-    S.f64(H_RNG3)[h] = r3;
-    S.f64(H_EID)[h] = eid;
-    S.f64(H_SLOT_T)[h] = st0;
-    S.f64(H_SLOT_T)[nH + h] = st1;
-    S.f64(H_SLOT_T)[2 * nH + h] = st2;
-    S.f64(H_SLOT_E)[h] = se0;
-    S.f64(H_SLOT_E)[nH + h] = se1;
-    S.f64(H_SLOT_E)[2 * nH + h] = se2;
-    S.f32(H_FLAGS)[h] = fl;
-    S.f32(H_RO_DST)[h] = ro_dst;
-    S.f32(H_RO_PAY)[h] = ro_pay;
-    S.f32(H_RO_TAG)[h] = ro_tag;
-    S.f32(H_RI_SRC)[h] = ri_src;
-    S.f32(H_RI_PAY)[h] = ri_pay;
-    S.f32(H_RI_TAG)[h] = ri_tag;
-    S.f64(H_RI_EID)[h] = ri_eid;
-    S.f64(H_TB_BAL)[h] = tbb0;
-    S.f64(H_TB_LAST)[h] = tbl0;
-    S.f64(H_TB_BAL)[nH + h] = tbb1;
-    S.f64(H_TB_LAST)[nH + h] = tbl1;
+    HostRec& r = *R;
+    r.rng[0] = r0;
+    r.rng[1] = r1;
+    r.rng[2] = r2;
+    r.rng[3] = r3;
+    r.eid = eid;
+    r.ri_eid = ri_eid;
+    r.slot_t[0] = st0;
+    r.slot_t[1] = st1;
+    r.slot_t[2] = st2;
+    r.slot_e[0] = se0;
+    r.slot_e[1] = se1;
+    r.slot_e[2] = se2;
+    r.tb_bal[0] = tbb0;
+    r.tb_bal[1] = tbb1;
+    r.tb_last[0] = tbl0;
+    r.tb_last[1] = tbl1;
+    r.cq_bytes = cq_bytes;
+    r.rc_lat = L->rc_lat;
+    r.rc_T = L->rc_T;
+    r.dig[0] = L->dig[0];
+    r.dig[1] = L->dig[1];
+    r.dig[2] = L->dig[2];
+    r.flags = fl;
+    r.ro_dst = ro_dst;
+    r.ro_pay = ro_pay;
+    r.ro_tag = ro_tag;
+    r.ri_src = ri_src;
+    r.ri_pay = ri_pay;
+    r.ri_tag = ri_tag;
+    r.cq_head = cq_head;
+    r.cq_nr = cq_nr;
+    r.cq_len = cq_len;
+    r.fq_head = fq_head;
+    r.fq_len = fq_len;
+    r.rc_dst = L->rc_dst;
+    r.max_codel = c_maxcodel;
+    r.n_sent += c_sent;
+    r.n_popped += c_popped;
+    r.n_delivered += c_deliv;
+    S.nextloc[h] = next_local_time();
     if (hd_valid) *cq_slot(0) = L->hd;
     if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
-    S.f32(H_CQ_HEAD)[h] = cq_head;
-    S.f32(H_CQ_NR)[h] = cq_nr;
-    S.f32(H_CQ_LEN)[h] = cq_len;
-    S.f64(H_CQ_BYTES)[h] = cq_bytes;
-    S.f32(H_FQ_HEAD)[h] = fq_head;
-    S.f32(H_FQ_LEN)[h] = fq_len;
-    S.f32(H_RC_DST)[h] = L->rc_dst;
-    S.f64(H_RC_LAT)[h] = L->rc_lat;
-    S.f64(H_RC_T)[h] = L->rc_T;
-    S.f64(H_D_TX)[h] = L->dig[0];
-    S.f64(H_D_RX)[h] = L->dig[1];
-    S.f64(H_D_APP)[h] = L->dig[2];
-    uint64_t* c = S.f64(H_CNT);
-    const size_t n = nH;
-    c[CNT_SENT * n + h] += c_sent;
-    c[CNT_LOSS * n + h] += c_loss;
-    c[CNT_POPPED * n + h] += c_popped;
-    c[CNT_DELIV * n + h] += c_deliv;
-    c[CNT_LOCAL_EV * n + h] += c_localev;
-    c[CNT_BYTES * n + h] += c_bytes;
-    c[CNT_MAX_CODEL * n + h] = c_maxcodel;
     if (sink == 0x9e3779b97f4a7c15ULL) C->overflow_info = 0;  // keeps the atomics returning
   }
 
   // rare counters go straight to memory (registers are kept for the per-packet ones)
-  __device__ __forceinline__ void cnt_add(int k, uint32_t v) { S.f64(H_CNT)[(size_t)k * S.nH + h] += v; }
+
 
   __device__ uint64_t next_local_time() const {
     uint64_t m = st0;
@@ -337,7 +342,7 @@ struct HostExec {
   __device__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
                         uint64_t c) {
     if (!S.trace_on) return;
-    const uint64_t seq = S.f64(H_TSEQ)[h]++;
+    const uint64_t seq = R->tseq++;
     uint64_t pos = atomicAdd((unsigned long long*)&C->trace_n, 1ULL);
     if (pos >= S.trace_cap) {
       atomicOr(&C->overflow, OVF_TRACE);
@@ -490,9 +495,9 @@ struct HostExec {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    if (fl & F_CODEL_IE) return now >= S.f64(H_CQ_IE)[h];
+    if (fl & F_CODEL_IE) return now >= R->cq_ie;
     fl |= F_CODEL_IE;
-    S.f64(H_CQ_IE)[h] = emu_sat_add(now, CODEL_INTERVAL);
+    R->cq_ie = emu_sat_add(now, CODEL_INTERVAL);
     return false;
   }
   // the head run into registers (queue not empty)
@@ -532,13 +537,13 @@ struct HostExec {
     return true;
   }
   __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
-    cnt_add(CNT_CODEL, 1);
+    R->n_codel++;
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
   __device__ bool codel_was_dropping_recently() const {  // :273-281
     if (!(fl & F_CODEL_DN)) return false;
-    return sat_sub(now, S.f64(H_CQ_DN)[h]) < CODEL_INTERVAL * 16;
+    return sat_sub(now, R->cq_dn) < CODEL_INTERVAL * 16;
   }
   // CoDelQueue::pop (:125-201)
   __device__ bool codel_pop(Pkt* out) {
@@ -560,24 +565,24 @@ struct HostExec {
       bool nok;
       bool has_n = codel_pop_raw(&n, &nok);
       fl |= F_CODEL_DROP;
-      uint64_t delta = sat_sub(S.f64(H_CQ_CUR)[h], S.f64(H_CQ_PREV)[h]);
-      S.f64(H_CQ_CUR)[h] = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      uint64_t delta = sat_sub(R->cq_cur, R->cq_prev);
+      R->cq_cur = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
       fl |= F_CODEL_DN;
-      S.f64(H_CQ_DN)[h] = codel_law(now, S.f64(H_CQ_CUR)[h]);
-      S.f64(H_CQ_PREV)[h] = S.f64(H_CQ_CUR)[h];
+      R->cq_dn = codel_law(now, R->cq_cur);
+      R->cq_prev = R->cq_cur;
       if (has_n) *out = n;
       return has_n;
     }
     // drop_from_drop_mode (:172-201)
     bool has_item = true;
     Pkt item = p;
-    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= S.f64(H_CQ_DN)[h]) {
+    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= R->cq_dn) {
       codel_drop(item);
-      S.f64(H_CQ_CUR)[h]++;
+      R->cq_cur++;
       bool iok = false;
       has_item = codel_pop_raw(&item, &iok);
       if (has_item && iok)
-        S.f64(H_CQ_DN)[h] = codel_law(S.f64(H_CQ_DN)[h], S.f64(H_CQ_CUR)[h]);
+        R->cq_dn = codel_law(R->cq_dn, R->cq_cur);
       else
         fl &= ~F_CODEL_DROP;
     }
@@ -649,12 +654,12 @@ struct HostExec {
         if (fifo_push(src, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
           relay_notify<0>();
         else
-          cnt_add(CNT_BLOCKED, 1);
+          R->n_blocked++;
       }
     }
   }
   __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
-    cnt_add(CNT_LOCAL_DELIV, 1);
+    R->n_local_deliv++;
     sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
     L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
   }
@@ -764,7 +769,7 @@ struct HostExec {
     DG(DG_BATCH);
     const bool boot = now < S.boot_end;
     if (dst == NO_HOST) {  // resolve_ip_to_host_id failed: InetDropped (worker.rs:347-357)
-      cnt_add(CNT_UNKNOWN, n);
+      R->n_unknown += n;
       sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (S.trace_on)
         for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
@@ -955,7 +960,7 @@ struct HostExec {
   }
 
   __device__ void app_task() {
-    const uint64_t k = S.f64(H_APPK)[h]++;
+    const uint64_t k = R->app_k++;
     uint32_t dst, payload, tag;
     uint64_t next_delay;
     if (S.tkind == SGN_TRAFFIC_PERIODIC) {
@@ -977,7 +982,7 @@ struct HostExec {
     if (fifo_push(dst, payload, payload, 1, tag))
       relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
     else
-      cnt_add(CNT_BLOCKED, 1);
+      R->n_blocked++;
     schedule<SLOT_APP>(now + next_delay);
   }
 
@@ -1238,12 +1243,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   EvRec* pk = S.pool + ik * S.CAP;
 
   uint64_t lmin = INVALID;
-  if (valid) {
-    const uint32_t nH = S.nH;
-    const uint64_t t0 = S.f64(H_SLOT_T)[h], t1 = S.f64(H_SLOT_T)[nH + h], t2 = S.f64(H_SLOT_T)[2 * nH + h];
-    lmin = t0 < t1 ? t0 : t1;
-    lmin = t2 < lmin ? t2 : lmin;
-  }
+  if (valid) lmin = S.nextloc[h];
   const bool bs_lds = S.NB <= LDS_BSLAB;
   if (bs_lds)
     for (uint32_t i = lane; i < S.NB; i += 64) lbs[i] = S.bucket_slab[i];
@@ -1434,12 +1434,22 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const uint64_t ex_mask = __ballot(loaded);
   const uint32_t n_sorted = wave_sum_u32(sorted);
   const uint64_t m = wave_min_u64(my_min);
+  // counters only ever summed over hosts: accumulated per wave
+  const uint32_t w_loss = wave_sum_u32(loaded ? ex.c_loss : 0u);
+  const uint32_t w_lev = wave_sum_u32(loaded ? ex.c_localev : 0u);
+  uint64_t w_bytes = loaded ? ex.c_bytes : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) w_bytes += shfl_xor64(w_bytes, off);
   if (lane == 0) {
     S.w_keep[g] = kmin;
     S.w_next[g] = m;
-    if (ex_mask) S.w_cnt[g] += (uint64_t)__popcll(ex_mask);
-    if (N_all) S.w_cnt[S.G + g] += N_all;
-    if (n_sorted) S.w_cnt[2 * (size_t)S.G + g] += n_sorted;
+    const size_t G = S.G;
+    if (ex_mask) S.w_cnt[W_EXEC * G + g] += (uint64_t)__popcll(ex_mask);
+    if (N_all) S.w_cnt[W_RUNS * G + g] += N_all;
+    if (n_sorted) S.w_cnt[W_SORTED * G + g] += n_sorted;
+    if (w_loss) S.w_cnt[W_LOSS * G + g] += w_loss;
+    if (w_lev) S.w_cnt[W_LOCAL_EV * G + g] += w_lev;
+    if (w_bytes) S.w_cnt[W_BYTES * G + g] += w_bytes;
   }
   if (!S.fuse_finalize) return;
   // ---- 5. single shard: the last wave to finish runs the round edge (no second launch).
@@ -1810,38 +1820,40 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     S.servers = (decltype(S.servers))d_sv;
   }
 
-  // ---- per-host state, initialised on the host ----
-  std::vector<uint64_t> r0(nH), r1(nH), r2(nH), r3(nH), eid(nH, 0), app_k(nH, 0);
-  std::vector<uint64_t> slot_t(3 * (size_t)nH, INVALID), slot_e(3 * (size_t)nH, 0);
-  std::vector<uint32_t> flags(nH, 0);
-  std::vector<uint64_t> tb_bal(2 * (size_t)nH), tb_last(2 * (size_t)nH, SIM_START),
-      tb_cap(2 * (size_t)nH), tb_inc(2 * (size_t)nH);
-  std::vector<uint64_t> dig(nH, SGN_DIGEST_SEED);
+  // ---- per-host state records, initialised on the host ----
+  std::vector<HostRec> recs(nH);
+  std::vector<uint64_t> nextloc(nH, INVALID);
+  std::memset(recs.data(), 0, recs.size() * sizeof(HostRec));
   for (uint32_t h = 0; h < nH; h++) {
     const uint32_t g = ctx->lo + h;
+    HostRec& r = recs[h];
     // Xoshiro256PlusPlus::seed_from_u64 (SplitMix64 fill), host.rs:234
     uint64_t sm = ctx->seed[g];
-    r0[h] = host_splitmix(sm);
-    r1[h] = host_splitmix(sm);
-    r2[h] = host_splitmix(sm);
-    r3[h] = host_splitmix(sm);
+    for (int i = 0; i < 4; i++) r.rng[i] = host_splitmix(sm);
+    for (int i = 0; i < 3; i++) r.slot_t[i] = INVALID;
     // create_token_bucket (relay/mod.rs:278-288) for inet_out (up) and inet_in (down)
     for (int w = 0; w < 2; w++) {
       const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
       const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
-      tb_inc[(size_t)w * nH + h] = inc;
-      tb_cap[(size_t)w * nH + h] = inc + SGN_CONFIG_MTU;
-      tb_bal[(size_t)w * nH + h] = inc + SGN_CONFIG_MTU;
+      r.tb_inc[w] = inc;
+      r.tb_cap[w] = inc + SGN_CONFIG_MTU;
+      r.tb_bal[w] = inc + SGN_CONFIG_MTU;
+      r.tb_last[w] = SIM_START;
     }
-    if (is_server[g]) flags[h] |= F_SERVER;
+    for (int i = 0; i < 3; i++) r.dig[i] = SGN_DIGEST_SEED;
+    r.rc_dst = NO_HOST;  // empty route cache
+    r.ip = ctx->ip[g];
+    r.unode = ctx->unode[g];
+    if (is_server[g]) r.flags |= F_SERVER;
     const bool has_app = tr->kind == SGN_TRAFFIC_PERIODIC || (tr->kind == SGN_TRAFFIC_TGEN && !is_server[g]);
     if (has_app) {
-      flags[h] |= F_HAS_APP;
+      r.flags |= F_HAS_APP;
       const uint64_t t = SIM_START + sgn_app_start_rel(tr->flow_seed, g, tr->start_ns, tr->start_jitter_ns);
-      const uint64_t e = eid[h]++;
+      const uint64_t e = r.eid++;
       if (t < S.end_time) {
-        slot_t[2 * (size_t)nH + h] = t;
-        slot_e[2 * (size_t)nH + h] = e;
+        r.slot_t[2] = t;
+        r.slot_e[2] = e;
+        nextloc[h] = t;
       }
     }
   }
@@ -1858,30 +1870,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     return 0;
   };
   int rc = 0;
-  // the per-host state: one block of u64 fields and one of u32 fields, field f of host h at
-  // [f * nH + h] (few base pointers keep the round kernel's scalar registers free)
-  S.hs64 = (decltype(S.hs64))dalloc<uint64_t>(ctx, (size_t)H64_N * nH);
-  S.hs32 = (decltype(S.hs32))dalloc<uint32_t>(ctx, (size_t)H32_N * nH);
+  S.hrec = (decltype(S.hrec))dalloc<HostRec>(ctx, nH);
   S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
   S.fifo = (decltype(S.fifo))dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
-  if (!S.hs64 || !S.hs32 || !S.codel || !S.fifo)
+  if (!S.hrec || !S.codel || !S.fifo)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
-  auto put64 = [&](uint32_t f, const std::vector<uint64_t>& v) -> int {
-    SGN_HIP(ctx, hipMemcpy(S.f64(f), v.data(), v.size() * 8, hipMemcpyHostToDevice));
-    return 0;
-  };
-  if ((rc = put64(H_RNG0, r0)) || (rc = put64(H_RNG1, r1)) || (rc = put64(H_RNG2, r2)) ||
-      (rc = put64(H_RNG3, r3)) || (rc = put64(H_EID, eid)) || (rc = put64(H_APPK, app_k)) ||
-      (rc = put64(H_SLOT_T, slot_t)) || (rc = put64(H_SLOT_E, slot_e)) ||
-      (rc = put64(H_TB_BAL, tb_bal)) || (rc = put64(H_TB_LAST, tb_last)) ||
-      (rc = put64(H_TB_CAP, tb_cap)) || (rc = put64(H_TB_INC, tb_inc)) ||
-      (rc = put64(H_D_TX, dig)) || (rc = put64(H_D_RX, dig)) || (rc = put64(H_D_APP, dig)))
-    return rc;
-  SGN_HIP(ctx, hipMemcpy(S.f32(H_FLAGS), flags.data(), (size_t)nH * 4, hipMemcpyHostToDevice));
-  {
-    std::vector<uint32_t> none(nH, NO_HOST);  // empty route caches
-    SGN_HIP(ctx, hipMemcpy(S.f32(H_RC_DST), none.data(), (size_t)nH * 4, hipMemcpyHostToDevice));
-  }
+  SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
+  if ((rc = up64(nextloc, &S.nextloc))) return rc;
 
   // ---- calendar: bucket width >= any window length, horizon > max latency ----
   // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least
@@ -1909,7 +1904,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.pool = (decltype(S.pool))dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
   S.w_next = (decltype(S.w_next))dalloc<uint64_t>(ctx, G);
   S.w_keep = (decltype(S.w_keep))dalloc<uint64_t>(ctx, G);
-  S.w_cnt = (decltype(S.w_cnt))dalloc<uint64_t>(ctx, 3 * G);
+  S.w_cnt = (decltype(S.w_cnt))dalloc<uint64_t>(ctx, W_N * G);
   if (!S.w_next || !S.w_keep || !S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
   S.slab_n = (decltype(S.slab_n))dalloc<uint32_t>(ctx, (NB + 1) * G);
   if (!S.pool || !S.slab_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event calendar)");
@@ -2042,46 +2037,52 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   return 0;
 }
 
+namespace {
+// the records of owned hosts [off, off + n) (device -> host)
+int read_recs(sgn_ctx* ctx, uint32_t off, uint32_t n, std::vector<HostRec>* out) {
+  out->resize(n);
+  if (n) SGN_HIP(ctx, hipMemcpy(out->data(), (const void*)(ctx->S.hrec + off), (size_t)n * sizeof(HostRec),
+                                hipMemcpyDeviceToHost));
+  return 0;
+}
+}  // namespace
+
 int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   if (!ctx || !out) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   int rc = sync_ctrl(ctx);
   const uint32_t nH = ctx->S.nH;
-  std::vector<uint64_t> cnt((size_t)NCNT * nH);
-  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.f64(H_CNT), cnt.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<HostRec> recs;
+  if (int e = read_recs(ctx, 0, nH, &recs)) return e;
   sgn_stats s{};
-  auto sum = [&](int k) {
-    uint64_t t = 0;
-    for (uint32_t h = 0; h < nH; h++) t += cnt[(size_t)k * nH + h];
-    return t;
-  };
-  s.rounds = ctx->h_ctrl->rounds;
-  s.packets_sent = sum(CNT_SENT);
-  s.packets_loss_dropped = sum(CNT_LOSS);
-  s.packets_sent += 0;
-  s.packets_unknown_dst = sum(CNT_UNKNOWN);
-  s.packet_events_popped = sum(CNT_POPPED);
-  s.codel_dropped = sum(CNT_CODEL);
-  s.delivered = sum(CNT_DELIV);
-  s.local_delivered = sum(CNT_LOCAL_DELIV);
-  s.app_blocked = sum(CNT_BLOCKED);
-  s.local_events = sum(CNT_LOCAL_EV);
-  s.bytes_delivered = sum(CNT_BYTES);
-  s.min_used_latency_ns = ctx->h_ctrl->min_used;
   uint64_t mc = 0;
-  for (uint32_t h = 0; h < nH; h++) mc = std::max(mc, cnt[(size_t)CNT_MAX_CODEL * nH + h]);
+  for (const HostRec& r : recs) {
+    s.packets_sent += r.n_sent;
+    s.packets_unknown_dst += r.n_unknown;
+    s.packet_events_popped += r.n_popped;
+    s.codel_dropped += r.n_codel;
+    s.delivered += r.n_delivered;
+    s.local_delivered += r.n_local_deliv;
+    s.app_blocked += r.n_blocked;
+    mc = std::max<uint64_t>(mc, r.max_codel);
+  }
+  s.rounds = ctx->h_ctrl->rounds;
+  s.min_used_latency_ns = ctx->h_ctrl->min_used;
   s.max_codel_len = mc;
   s.max_pending_events = ctx->h_ctrl->max_bucket;
   {
     const size_t G = ctx->S.G;
-    std::vector<uint64_t> wc(3 * G);
-    SGN_HIP(ctx, hipMemcpy(wc.data(), ctx->S.w_cnt, wc.size() * 8, hipMemcpyDeviceToHost));
-    uint64_t acc[3] = {0, 0, 0};
-    for (int k = 0; k < 3; k++)
+    std::vector<uint64_t> wc(W_N * G);
+    SGN_HIP(ctx, hipMemcpy(wc.data(), (const void*)ctx->S.w_cnt, wc.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t acc[W_N] = {};
+    for (int k = 0; k < W_N; k++)
       for (size_t g = 0; g < G; g++) acc[k] += wc[k * G + g];
-    s.host_executions = acc[0];
-    s.event_runs = acc[1];
-    s.sched_sorted_segments = acc[2];
+    s.host_executions = acc[W_EXEC];
+    s.event_runs = acc[W_RUNS];
+    s.sched_sorted_segments = acc[W_SORTED];
+    s.packets_loss_dropped = acc[W_LOSS];
+    s.local_events = acc[W_LOCAL_EV];
+    s.bytes_delivered = acc[W_BYTES];
   }
   s.sched_heavy_hosts = 0;
   *out = s;
@@ -2093,34 +2094,21 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   if (lo < ctx->lo || hi > ctx->hi || lo > hi) return set_error(ctx, SGN_EINVAL, "range outside the owned shard");
   int rc = sync_ctrl(ctx);
-  const uint32_t n = hi - lo, off = lo - ctx->lo, nH = ctx->S.nH;
-  if (n == 0) return rc;
-  std::vector<uint64_t> tx(n), rx(n), ap(n), a(n), b(n), c(n), d(n), e(n);
-  std::vector<uint64_t> cnt((size_t)NCNT * nH);
-  SGN_HIP(ctx, hipMemcpy(tx.data(), ctx->S.f64(H_D_TX) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(rx.data(), ctx->S.f64(H_D_RX) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(ap.data(), ctx->S.f64(H_D_APP) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(a.data(), ctx->S.f64(H_RNG0) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(b.data(), ctx->S.f64(H_RNG1) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(c.data(), ctx->S.f64(H_RNG2) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(d.data(), ctx->S.f64(H_RNG3) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(e.data(), ctx->S.f64(H_EID) + off, n * 8, hipMemcpyDeviceToHost));
-  SGN_HIP(ctx, hipMemcpy(cnt.data(), ctx->S.f64(H_CNT), cnt.size() * 8, hipMemcpyDeviceToHost));
+  const uint32_t n = hi - lo, off = lo - ctx->lo;
+  std::vector<HostRec> recs;
+  if (int e = read_recs(ctx, off, n, &recs)) return e;
   for (uint32_t i = 0; i < n; i++) {
+    const HostRec& r = recs[i];
     sgn_host_digest& o = out[i];
-    o.tx = tx[i];
-    o.rx = rx[i];
-    o.app = ap[i];
-    o.rng[0] = a[i];
-    o.rng[1] = b[i];
-    o.rng[2] = c[i];
-    o.rng[3] = d[i];
-    o.next_event_id = e[i];
-    const size_t h = off + i;
-    o.n_sent = cnt[(size_t)CNT_SENT * nH + h];
-    o.n_popped = cnt[(size_t)CNT_POPPED * nH + h];
-    o.n_delivered = cnt[(size_t)CNT_DELIV * nH + h];
-    o.n_codel_dropped = cnt[(size_t)CNT_CODEL * nH + h];
+    o.tx = r.dig[0];
+    o.rx = r.dig[1];
+    o.app = r.dig[2];
+    for (int k = 0; k < 4; k++) o.rng[k] = r.rng[k];
+    o.next_event_id = r.eid;
+    o.n_sent = r.n_sent;
+    o.n_popped = r.n_popped;
+    o.n_delivered = r.n_delivered;
+    o.n_codel_dropped = r.n_codel;
   }
   return rc;
 }
@@ -2131,26 +2119,24 @@ int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
   if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
-  const uint32_t h = host - ctx->lo, nH = ctx->S.nH;
+  const uint32_t h = host - ctx->lo;
+  std::vector<HostRec> rec;
+  if (int e = read_recs(ctx, h, 1, &rec)) return e;
   uint64_t m = INVALID;
-  for (int s = 0; s < NSLOT; s++) {
-    uint64_t v;
-    SGN_HIP(ctx, hipMemcpy(&v, ctx->S.f64(H_SLOT_T) + (size_t)s * nH + h, 8, hipMemcpyDeviceToHost));
-    m = std::min(m, v);
-  }
+  for (int s = 0; s < NSLOT; s++) m = std::min(m, rec[0].slot_t[s]);
   // pending packet events for this host: its group's slab in every bucket
   const DevSim& S = ctx->S;
   const uint32_t g = h >> S.gsh;
   std::vector<uint32_t> bs(S.NB);
-  SGN_HIP(ctx, hipMemcpy(bs.data(), S.bucket_slab, bs.size() * 4, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(bs.data(), (const void*)S.bucket_slab, bs.size() * 4, hipMemcpyDeviceToHost));
   for (uint32_t b = 0; b < S.NB; b++) {
     const size_t idx = (size_t)bs[b] * S.G + g;
     uint32_t n = 0;
-    SGN_HIP(ctx, hipMemcpy(&n, S.slab_n + idx, 4, hipMemcpyDeviceToHost));
+    SGN_HIP(ctx, hipMemcpy(&n, (const void*)(S.slab_n + idx), 4, hipMemcpyDeviceToHost));
     n = std::min(n, S.CAP);
     if (!n) continue;
     std::vector<EvRec> ev(n);
-    SGN_HIP(ctx, hipMemcpy(ev.data(), S.pool + idx * S.CAP, n * sizeof(EvRec), hipMemcpyDeviceToHost));
+    SGN_HIP(ctx, hipMemcpy(ev.data(), (const void*)(S.pool + idx * S.CAP), n * sizeof(EvRec), hipMemcpyDeviceToHost));
     for (const EvRec& e : ev)
       if (e.dst == host) m = std::min(m, e.time);
   }

@@ -108,45 +108,40 @@ enum : uint32_t {
   OVF_TRACE = 32u,
 };
 
-// per-host counters (index * nH + host)
-enum {
-  CNT_SENT = 0,
-  CNT_LOSS,
-  CNT_UNKNOWN,
-  CNT_POPPED,
-  CNT_CODEL,
-  CNT_DELIV,
-  CNT_LOCAL_DELIV,
-  CNT_BLOCKED,
-  CNT_LOCAL_EV,
-  CNT_BYTES,
-  CNT_MAX_CODEL,
-  NCNT
+// One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
+// A round touches only the hosts with something due (~1 in 8 at the bench workload), so a
+// record per host turns each executed host's state into 3 contiguous cache lines; the hot
+// part (bytes 0..303) is what Host::execute reads and writes every time it runs.
+struct __attribute__((aligned(128))) HostRec {
+  uint64_t rng[4];           // Xoshiro256++ state (host/host.rs:234)
+  uint64_t eid;              // next event id (host.rs:259,662-666)
+  uint64_t ri_eid;           // relay_inet_in cached packet: src event id
+  uint64_t slot_t[3];        // local event slots (relay out, relay in, app): time ...
+  uint64_t slot_e[3];        // ... and event id
+  uint64_t tb_bal[2];        // token buckets (0 = inet_out, 1 = inet_in): balance ...
+  uint64_t tb_last[2];       // ... last refill
+  uint64_t tb_inc[2];        // ... refill increment (constant)
+  uint64_t tb_cap[2];        // ... capacity (constant)
+  uint64_t cq_bytes;         // CoDel queued bytes
+  uint64_t rc_lat, rc_T;     // route cache: latency, integer loss threshold ...
+  uint64_t dig[3];           // digests tx, rx, app
+  uint32_t flags, ro_dst, ro_pay, ro_tag;    // flag bits; relay_inet_out cached packet
+  uint32_t ri_src, ri_pay, ri_tag, cq_head;  // relay_inet_in cached packet; CoDel ring head
+  uint32_t cq_nr, cq_len, fq_head, fq_len;   // CoDel runs / packets; send queue
+  uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
+  uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
+  // cold: rare paths only
+  uint64_t app_k;                            // synthetic app counter
+  uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
+  uint64_t tseq;                             // trace sequence
+  uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
+  uint64_t pad[17];
 };
+static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
+static_assert(offsetof(HostRec, n_sent) + 24 <= 304, "hot part");
 
-// per-host u64 fields (DevSim::f64); multi-slot fields take consecutive field indices
-enum : uint32_t {
-  H_RNG0 = 0, H_RNG1, H_RNG2, H_RNG3,  // Xoshiro256++ state (host/host.rs:234)
-  H_EID,                               // next event id (host.rs:259,662-666)
-  H_APPK,                              // synthetic app counter
-  H_SLOT_T, H_SLOT_E = H_SLOT_T + 3,   // local event slots: time / event id [3]
-  H_RI_EID = H_SLOT_E + 3,             // relay_inet_in cached packet's event id
-  H_TB_BAL, H_TB_LAST = H_TB_BAL + 2,  // token buckets [2]: 0 = inet_out, 1 = inet_in
-  H_TB_CAP = H_TB_LAST + 2, H_TB_INC = H_TB_CAP + 2,
-  H_CQ_BYTES = H_TB_INC + 2, H_CQ_IE, H_CQ_DN, H_CQ_CUR, H_CQ_PREV,  // CoDel state
-  H_D_TX, H_D_RX, H_D_APP,             // digests
-  H_TSEQ,                              // trace sequence
-  H_RC_LAT, H_RC_T,                    // route cache: latency, loss threshold
-  H_CNT,                               // counters [NCNT]
-  H64_N = H_CNT + NCNT
-};
-// per-host u32 fields (DevSim::f32)
-enum : uint32_t {
-  H_FLAGS = 0, H_RO_DST /* HostId */, H_RO_PAY, H_RO_TAG, H_RI_SRC, H_RI_PAY, H_RI_TAG,
-  H_CQ_HEAD, H_CQ_NR, H_CQ_LEN, H_FQ_HEAD, H_FQ_LEN,
-  H_RC_DST,                            // route cache: peer HostId (NO_HOST: empty)
-  H32_N
-};
+// per-wave counters (DevSim::w_cnt rows of G)
+enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_N };
 
 // host flag bits
 enum : uint32_t {
@@ -230,13 +225,12 @@ struct DevSim {
   SGN_GLB const uint32_t* dns_val;
   uint32_t dns_mask;
   uint32_t pad1;
-  // host state, SoA: field f of local host h at hs64[f * nH + h] / hs32[f * nH + h]
-  SGN_GLB uint64_t* hs64;        // [H64_N * nH]
-  SGN_GLB uint32_t* hs32;        // [H32_N * nH]
-  SGN_GLB CodelEnt* codel;       // [nH * codel_cap] run ring per host
-  SGN_GLB FifoEnt* fifo;         // [nH * fifo_cap] send queue per host
-  __host__ __device__ __forceinline__ SGN_GLB uint64_t* f64(uint32_t f) const { return hs64 + (size_t)f * nH; }
-  __host__ __device__ __forceinline__ SGN_GLB uint32_t* f32(uint32_t f) const { return hs32 + (size_t)f * nH; }
+  // host state: one record per owned host, and each host's next local event time (read
+  // for all hosts at the start of a round: a dense array keeps that read coalesced)
+  SGN_GLB HostRec* hrec;        // [nH]
+  SGN_GLB uint64_t* nextloc;    // [nH]
+  SGN_GLB CodelEnt* codel;      // [nH * codel_cap] run ring per host
+  SGN_GLB FifoEnt* fifo;        // [nH * fifo_cap] send queue per host
   // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host
   // group (2^gsh consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
   // ids are indirect (bucket_slab) so the partially consumed last bucket of a window can
@@ -253,7 +247,7 @@ struct DevSim {
   // and cumulative {host executions, due runs, sorted segments}
   SGN_GLB uint64_t* w_next;       // [G]
   SGN_GLB uint64_t* w_keep;       // [G]
-  SGN_GLB uint64_t* w_cnt;        // [3 * G]
+  SGN_GLB uint64_t* w_cnt;        // [W_N * G]
   SGN_GLB uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
   SGN_GLB uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
   SGN_GLB uint64_t* fin_next;
