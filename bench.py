@@ -148,15 +148,16 @@ def main():
         ev = int(e.item())
     d = {k: st1[k] - st0[k] for k in st1}
     rounds = d["rounds"]
-    # roofline of the dominant kernel (k_execute): algorithmic bytes per launch, DESIGN.md
+    # roofline of the dominant kernel (k_execute): algorithmic bytes per launch
+    # = SURVEY.md §8(d)'s packet-path model, 128 B per packet (send record, DNS, node
+    # indices, route entry, event record write, sort/merge, pop read) + 96 B per active
+    # host-round (RNG state, event-id counter, queue head), over the units one launch
+    # processes, / the launch's average duration (HIP events on the engine stream).
     launches = kt1[0] - kt0[0]
     exec_ms = kt1[1] - kt0[1]
-    pops = d["packet_events_popped"]
-    sends = d["packets_sent"] + d["packets_loss_dropped"] + d["packets_unknown_dst"]
-    local_ev = d["local_events"]
+    n_pkt = d["packets_sent"] + d["packets_loss_dropped"]
     host_exec = d["host_executions"]
-    idle = rounds * (hosts.n // world) - host_exec
-    alg_bytes = 96 * pops + 64 * sends + 736 * host_exec + 36 * idle
+    alg_bytes = 128 * n_pkt + 96 * host_exec
     roof = None
     if launches and exec_ms > 0:
         avg_s = exec_ms / launches / 1e3
@@ -164,7 +165,19 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                 "kernel": "k_execute", "avg_launch_us": round(avg_s * 1e6, 2),
-                "alg_bytes_per_launch": int(alg_bytes / launches)}
+                "alg_bytes_per_launch": int(alg_bytes / launches),
+                "units_per_launch": {"packets": round(n_pkt / launches, 1),
+                                     "active_host_rounds": round(host_exec / launches, 1)}}
+        # HBM bytes per launch measured by PMC (tools/pmc_traffic.sh: FETCH_SIZE x2 +
+        # WRITE_SIZE over the same default run's timed dispatches), when it matches this run
+        tf = ROOT / "profiles" / "k_execute_traffic.json"
+        default_run = (args.hosts, args.nodes, args.rounds_per_step, args.steps, args.warmup,
+                       world) == (100_000, 1000, 100, 10, 5, 1)
+        if tf.exists() and default_run:
+            t = json.loads(tf.read_text())
+            roof["traffic"] = t["traffic_bytes_per_launch"]
+            roof["traffic_unit"] = "bytes/launch (PMC, profiles/k_execute_traffic.json)"
+            roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
     out = {
         "metric": METRIC,
         "value": ev / el,
