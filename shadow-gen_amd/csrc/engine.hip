@@ -72,6 +72,25 @@ __device__ __forceinline__ bool ev_less(const EvRec& a, const EvRec& b) {
   return a.eid < b.eid;
 }
 
+// ---- cross-workgroup data inside one launch (persistent rounds; MI355X L2s are per XCD and
+// not coherent): data another workgroup reads in a later round is stored write-through with
+// device-scope atomic stores, and control words are read with device-scope atomic loads.
+template <typename T>
+__device__ __forceinline__ T ld_dev(SGN_GLB T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_dev(SGN_GLB T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  st_dev(q, r.time);
+  st_dev(q + 1, r.eid);
+  st_dev(q + 2, (uint64_t)r.src | ((uint64_t)r.dst << 32));
+  st_dev(q + 3, (uint64_t)r.pc | ((uint64_t)r.tag << 32));
+}
+
 // a / b for a divisor below 2^32: u32 division when the dividend fits too
 __device__ __forceinline__ uint64_t div_small(uint64_t a, uint64_t b) {
   if (((a | b) >> 32) == 0) return (uint32_t)a / (uint32_t)b;
@@ -156,7 +175,7 @@ struct LaneLDS {
 
 struct HostExec {
   const DevSim& S;
-  Ctrl* C;
+  SGN_GLB Ctrl* C;
   uint32_t h, gid, my_ip, my_unode;
   uint64_t now, we;
   uint32_t b1, keep_slab;  // the window's last bucket (its new events go to the spare slab)
@@ -822,7 +841,7 @@ struct HostExec {
     if (S.dynamic) {  // Worker::update_lowest_used_latency (no return value: fire and forget)
       sink ^= atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
     }
-    EvRec* dstp;
+    SGN_GLB EvRec* dstp;
     uint32_t cap;
     uint32_t pos;
     const bool owned = dst - S.lo < S.nH;
@@ -858,7 +877,7 @@ struct HostExec {
       r.dst = dst;
       r.pc = payload | (k << 16);
       r.tag = tag;
-      dstp[pos + m] = r;
+      st_dev_rec(dstp + pos + m, r);
     }
   }
 
@@ -1139,62 +1158,58 @@ __device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
 // finalize_round for the fused single-shard path, run by the last wave of k_execute: the
 // waves' minima come from the chunk slots; every value another wave changed during this
 // launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
-__device__ void finalize_fused(const DevSim& S, uint32_t lane) {
-  Ctrl* C = S.ctrl;
-  const uint32_t nch = (S.G + 63) >> 6;
+__device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uint64_t ws,
+                               uint64_t we, uint32_t ks, uint32_t slab_b1) {
+  SGN_GLB Ctrl* C = S.ctrl;
   uint64_t kk = INVALID, wn = INVALID;
   for (uint32_t i = lane; i < nch; i += 64) {
     const uint64_t a = __hip_atomic_exchange(&S.fin_keep[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t b = __hip_atomic_exchange(&S.fin_next[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&S.fin_cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_dev(&S.fin_cnt[i], 0u);
     kk = a < kk ? a : kk;
     wn = b < wn ? b : wn;
   }
-  if (lane == 0) __hip_atomic_store(&S.fin_cnt[nch], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) st_dev(&S.fin_cnt[nch], 0u);
   kk = wave_min_u64(kk);
   wn = wave_min_u64(wn);
-  const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
+  const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
   if (lane == 0) {
     for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1))
-      __hip_atomic_store(&S.bucket_min[b], (unsigned long long)INVALID, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);  // consumed
+      st_dev(&S.bucket_min[b], (uint64_t)INVALID);  // consumed
     // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
-    const uint32_t old = S.bucket_slab[b1];
-    S.bucket_slab[b1] = C->keep_slab;
-    C->keep_slab = old;
+    st_dev(&S.bucket_slab[b1], ks);
+    st_dev(&C->keep_slab, slab_b1);
     const uint64_t km = __hip_atomic_exchange(&C->keep_min, (unsigned long long)INVALID,
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&S.bucket_min[b1], (unsigned long long)(km < kk ? km : kk),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_dev(&S.bucket_min[b1], km < kk ? km : kk);
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint64_t m = INVALID;
   for (uint32_t b = lane; b < S.NB; b += 64) {
-    const uint64_t bm = __hip_atomic_load(&S.bucket_min[b], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t bm = ld_dev(&S.bucket_min[b]);
     m = bm < m ? bm : m;
   }
   m = wave_min_u64(m);
   if (lane == 0) {
     m = wn < m ? wn : m;
     const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
-    C->last_min_next = min_next;
+    st_dev(&C->last_min_next, min_next);
     // Runahead::get (runahead.rs:44-57)
-    const uint64_t mu = __hip_atomic_load(&C->min_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t mu = ld_dev(&C->min_used);
     uint64_t ra = (S.dynamic && mu != INVALID) ? mu : S.min_possible;
     ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
     // Controller::manager_finished_current_round (controller.rs:88-112)
     uint64_t ne = min_next + ra;
     if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
     ne = ne < S.end_time ? ne : S.end_time;
-    C->active = min_next < ne ? 1u : 0u;
-    C->ws = min_next;
-    C->we = ne;
-    C->round_min = INVALID;
-    C->rounds++;
+    st_dev(&C->active, min_next < ne ? 1u : 0u);
+    st_dev(&C->ws, min_next);
+    st_dev(&C->we, ne);
+    st_dev(&C->round_min, (uint64_t)INVALID);
+    __hip_atomic_fetch_add(&C->rounds, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1213,40 +1228,52 @@ __global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
 //  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
 //     segment and local slots, emitting new runs into the calendar / exchange slots;
 //  4. the wave's minimum next local event time goes to Ctrl::round_min.
-__global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg) {
-  // the simulation constants are read from device memory where they are used (a by-value
-  // kernel argument would pin ~90 scalar registers for the whole kernel)
-  const DevSim& S = *Sg;
-  Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  // dynamic LDS sized by the slab capacity S.CAP (a bucket's runs of one group fit a slab)
-  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  EvRec* lev = (EvRec*)lds_dyn;                 // due runs of the bucket
-  uint16_t* lb = (uint16_t*)(lev + S.CAP);      // grouped by destination lane (unordered)
-  uint16_t* lc = lb + S.CAP;                    // ... ordered inside each destination segment
-  __shared__ uint32_t lcnt[64], lstart[64], lcur[64];
-  __shared__ LaneLDS lslot[64];  // the lanes' LDS slots
-  __shared__ uint32_t lbs[LDS_BSLAB];  // bucket -> slab table for this round's sends
+// LDS of the round kernels (one wave per workgroup)
+struct ExecLDS {
+  EvRec* lev;         // due runs of one bucket (dynamic LDS, CAP entries)
+  uint16_t* lb;       // grouped by destination lane (unordered)
+  uint16_t* lc;       // ... ordered inside each destination segment
+  uint32_t* lcnt;
+  uint32_t* lstart;
+  uint32_t* lcur;
+  LaneLDS* lslot;     // the lanes' LDS slots
+  uint32_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB)
+};
+
+// One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
+//  1. gather: the group's slabs of the window's buckets are read; runs due in the window go
+//     to LDS, the last bucket's later runs move to the spare slab set ks;
+//  2. order: counting sort of the due runs by destination lane (LDS atomics + wave scan),
+//     then a rank sort inside each destination's segment by (time, src host, src event
+//     id) — Shadow's EventQueue order (core/work/event.rs:84-155; keys are unique);
+//  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
+//     segment and local slots, emitting new runs into the calendar / exchange slots;
+//  4. the group's minimum kept-event time and next local event time are returned.
+__device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
+                           const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out) {
+  SGN_GLB Ctrl* C = S.ctrl;
+  EvRec* lev = X.lev;
+  uint16_t* lb = X.lb;
+  uint16_t* lc = X.lc;
+  uint32_t* lcnt = X.lcnt;
+  uint32_t* lstart = X.lstart;
+  uint32_t* lcur = X.lcur;
+  LaneLDS* lslot = X.lslot;
+  uint32_t* lbs = X.lbs;
   const uint32_t lane = threadIdx.x;
-  const uint32_t g = blockIdx.x;
   const uint32_t gsz = 1u << S.gsh;
   const uint32_t h = (g << S.gsh) + lane;  // local host index
   const bool valid = lane < gsz && h < S.nH;
-  const uint64_t ws = C->ws, we = C->we;
   const uint32_t bs = bucket_of(S, ws), be = bucket_of(S, we - 1);
   const uint32_t nbk = ((be + S.NB - bs) & (S.NB - 1)) + 1;  // buckets overlapping the window
-  const uint32_t ks = C->keep_slab;
   const uint32_t gbase = S.lo + (g << S.gsh);  // HostId of lane 0
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt0 = S.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const size_t ik = (size_t)ks * S.G + g;
-  EvRec* pk = S.pool + ik * S.CAP;
+  SGN_GLB EvRec* pk = S.pool + ik * S.CAP;
 
   uint64_t lmin = INVALID;
   if (valid) lmin = S.nextloc[h];
-  const bool bs_lds = S.NB <= LDS_BSLAB;
-  if (bs_lds)
-    for (uint32_t i = lane; i < S.NB; i += 64) lbs[i] = S.bucket_slab[i];
   HostExec ex(S, h, we, be, ks, lslot + lane, lbs);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
@@ -1263,9 +1290,9 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     const uint64_t sub_end = last ? we : SIM_START + (S.bw_div.div(ws - SIM_START) + bi + 1) * S.BW;
     // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
-    const size_t ib = (size_t)S.bucket_slab[b] * S.G + g;
-    const uint32_t n = min(S.slab_n[ib], S.CAP);
-    const EvRec* pb = S.pool + ib * S.CAP;
+    const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
+    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
+    SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
     lcnt[lane] = 0;
     uint32_t N = 0;
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
@@ -1283,7 +1310,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
         base = __shfl(base, 0, 64) + lanes_below(km);
         if (keep) {
           if (base < S.CAP)
-            pk[base] = r;
+            st_dev_rec(pk + base, r);
           else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
             C->overflow_info = r.dst;
           kmin = r.time < kmin ? r.time : kmin;
@@ -1291,8 +1318,8 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
       }
     }
     if (lane == 0) {
-      S.slab_n[ib] = 0;  // consumed (or moved); nobody appends to it this round
-      if (n > C->max_bucket) atomicMax((unsigned long long*)&C->max_bucket, (unsigned long long)n);
+      st_dev(&S.slab_n[ib], 0u);  // consumed (or moved); nobody appends to it this round
+      if (n > ld_dev(&C->max_bucket)) atomicMax((unsigned long long*)&C->max_bucket, (unsigned long long)n);
     }
     N_all += N;
     __syncthreads();
@@ -1389,7 +1416,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
       mx = o > mx ? o : mx;
     }
     const uint32_t busy = __popcll(__ballot(n_ev > 0));
-    uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)blockIdx.x;
+    SGN_GLB uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)g;
     if (lane == 0) {
       st[0] = clk1 - clk0;
       st[1] = sum;
@@ -1434,6 +1461,8 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const uint64_t ex_mask = __ballot(loaded);
   const uint32_t n_sorted = wave_sum_u32(sorted);
   const uint64_t m = wave_min_u64(my_min);
+  *kmin_out = kmin;
+  *next_out = m;
   // counters only ever summed over hosts: accumulated per wave
   const uint32_t w_loss = wave_sum_u32(loaded ? ex.c_loss : 0u);
   const uint32_t w_lev = wave_sum_u32(loaded ? ex.c_localev : 0u);
@@ -1451,24 +1480,40 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     if (w_lev) S.w_cnt[W_LOCAL_EV * G + g] += w_lev;
     if (w_bytes) S.w_cnt[W_BYTES * G + g] += w_bytes;
   }
-  if (!S.fuse_finalize) return;
-  // ---- 5. single shard: the last wave to finish runs the round edge (no second launch).
-  // Only device-scope atomics cross between waves here (no fences: an agent-scope release
-  // writes the whole L2 back on gfx950): every wave folds its minima into its chunk's
-  // slots with returning atomics, waits for them, then counts itself in (64 waves per
-  // chunk counter, then chunks); the last arrival reads the slots with atomic loads.
+}
+
+#define SGN_EXEC_LDS(X)                                                              \
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];                     \
+  __shared__ uint32_t lcnt_[64], lstart_[64], lcur_[64];                             \
+  __shared__ LaneLDS lslot_[64];                                                     \
+  __shared__ uint32_t lbs_[LDS_BSLAB];                                               \
+  ExecLDS X;                                                                         \
+  X.lev = (EvRec*)lds_dyn;                                                           \
+  X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \
+  X.lc = X.lb + S.CAP;                                                               \
+  X.lcnt = lcnt_;                                                                    \
+  X.lstart = lstart_;                                                                \
+  X.lcur = lcur_;                                                                    \
+  X.lslot = lslot_;                                                                  \
+  X.lbs = lbs_;
+
+// Arrival of one workgroup at the end of a round: its minima go into its chunk's slots with
+// returning device-scope atomics, then it counts itself in (64 workgroups per chunk counter,
+// then chunks). Only atomics cross between workgroups (no fences: an agent-scope release
+// writes the whole L2 back on gfx950). Returns true (all lanes) for the last arrival.
+__device__ bool arrive(const DevSim& S, uint32_t w, uint32_t nw, uint64_t kmin, uint64_t m) {
   uint32_t last = 0;
-  if (lane == 0) {
-    const uint32_t ch = g >> 6;
-    const uint32_t csz = min(64u, S.G - (ch << 6));
-    const uint32_t nch = (S.G + 63) >> 6;
+  if (threadIdx.x == 0) {
+    const uint32_t ch = w >> 6;
+    const uint32_t csz = min(64u, nw - (ch << 6));
+    const uint32_t nch = (nw + 63) >> 6;
     if (kmin != INVALID)
       __hip_atomic_fetch_min(&S.fin_keep[ch], (unsigned long long)kmin, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     if (m != INVALID)
       __hip_atomic_fetch_min(&S.fin_next[ch], (unsigned long long)m, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store/atomic of the round done
     const uint32_t c = __hip_atomic_fetch_add(&S.fin_cnt[ch], 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
     if (c == csz - 1) {
@@ -1478,9 +1523,84 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
       last = t == nch - 1 ? 1u : 0u;
     }
   }
-  last = __shfl(last, 0, 64);
-  if (!last) return;
-  finalize_fused(S, lane);
+  return __shfl(last, 0, 64) != 0;
+}
+
+// One round per launch: one workgroup (one wave) per group; single shard: the last arrival
+// runs the round edge (finalize_fused), multi-shard: comm.cpp's exchange follows.
+__global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg) {
+  // the simulation constants are read from device memory where they are used (a by-value
+  // kernel argument would pin ~90 scalar registers for the whole kernel)
+  const DevSim& S = *Sg;
+  SGN_GLB Ctrl* C = S.ctrl;
+  if (!C->active) return;
+  SGN_EXEC_LDS(X)
+  const uint64_t ws = C->ws, we = C->we;
+  const uint32_t ks = C->keep_slab;
+  if (S.NB <= LDS_BSLAB)
+    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = S.bucket_slab[i];
+  __syncthreads();
+  uint64_t kmin, m;
+  exec_group(S, blockIdx.x, ws, we, ks, X, &kmin, &m);
+  if (!S.fuse_finalize) return;
+  if (!arrive(S, blockIdx.x, gridDim.x, kmin, m)) return;
+  const uint32_t b1 = bucket_of(S, we - 1);
+  finalize_fused(S, threadIdx.x, (gridDim.x + 63) >> 6, ws, we, ks,
+                 S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]));
+}
+
+// Persistent rounds (single shard): the grid stays resident and runs up to max_rounds
+// rounds, workgroup w serving groups w, w + P, ... every round (a group's host state stays
+// with one CU). A grid barrier per round replaces the kernel boundary: the last arrival
+// runs the round edge and publishes the round number in Ctrl::epoch (atomic store); the
+// others poll it (bounded: a spin past the limit flags OVF_TIMEOUT and exits) and then
+// acquire, so the next round's plain loads see every other workgroup's write-through
+// stores. Shared control words are read with atomic loads (never through the scalar cache).
+__global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds) {
+  const DevSim& S = *Sg;
+  SGN_GLB Ctrl* C = S.ctrl;
+  SGN_EXEC_LDS(X)
+  const uint32_t w = blockIdx.x, P = gridDim.x;
+  const uint64_t e0 = ld_dev(&C->epoch);
+  for (uint32_t r = 0; r < max_rounds; r++) {
+    if (!ld_dev(&C->active)) break;
+    const uint64_t ws = ld_dev(&C->ws), we = ld_dev(&C->we);
+    const uint32_t ks = ld_dev(&C->keep_slab);
+    if (S.NB <= LDS_BSLAB)
+      for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = ld_dev(&S.bucket_slab[i]);
+    __syncthreads();
+    uint64_t kall = INVALID, mall = INVALID;
+    for (uint32_t g = w; g < S.G; g += P) {
+      uint64_t kmin, m;
+      exec_group(S, g, ws, we, ks, X, &kmin, &m);
+      kall = kmin < kall ? kmin : kall;
+      mall = m < mall ? m : mall;
+      __syncthreads();
+    }
+    if (arrive(S, w, P, kall, mall)) {
+      const uint32_t b1 = bucket_of(S, we - 1);
+      finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks,
+                     S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) st_dev(&C->epoch, e0 + r + 1);
+    }
+    // grid barrier: wait for the round edge, bounded
+    uint32_t spins = 0;
+    bool ok = true;
+    while (ld_dev(&C->epoch) < e0 + r + 1) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 22)) {
+        ok = false;
+        break;
+      }
+    }
+    if (!ok) {
+      if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+  }
 }
 
 // Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
@@ -1566,8 +1686,9 @@ const char* kKernelNames[K_NUM] = {"k_execute", "k_finalize", "k_import", "k_adv
 
 int launch_round(sgn_ctx* ctx);
 
-// dynamic LDS of k_execute: CAP event runs + two u16 index arrays
+// dynamic LDS of k_execute / k_rounds: CAP event runs + two u16 index arrays
 inline size_t exec_lds_bytes(uint32_t cap) { return (size_t)cap * (sizeof(EvRec) + 4); }
+constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then a host sync)
 
 }  // namespace
 
@@ -1956,6 +2077,21 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
+  // persistent rounds (single shard): a grid that is entirely resident — the occupancy
+  // query, capped by LDS per CU — with workgroups looping over groups when G exceeds it
+  ctx->persist_grid = 0;
+  if (ctx->nranks == 1 && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+    int occ = 0, ncu = 0;
+    const size_t dyn = exec_lds_bytes((uint32_t)CAP);
+    hipFuncAttributes fa{};
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_rounds, 64, dyn) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
+        hipFuncGetAttributes(&fa, (const void*)k_rounds) == hipSuccess && occ > 0 && ncu > 0) {
+      const int lds_occ = (int)((160u * 1024u) / (fa.sharedSizeBytes + dyn));
+      occ = std::min(occ, lds_occ);
+      ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, (uint64_t)occ * (uint64_t)ncu);
+    }
+  }
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
   {
     std::vector<uint64_t> inv((G + 63) / 64, INVALID);
@@ -2004,6 +2140,21 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   // shard a full batch is one hipGraph replay: the round's launches are captured once.
   const uint64_t batch = 32;
   const bool graph = ctx->nranks == 1 && ctx->use_graph;
+  if (ctx->nranks == 1 && ctx->persist_grid) {
+    // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside)
+    while (ctx->h_ctrl->active && enq < max_rounds) {
+      const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
+      time_begin(ctx, K_EXECUTE);
+      hipLaunchKernelGGL(k_rounds, dim3(ctx->persist_grid), dim3(64), exec_lds_bytes(ctx->S.CAP),
+                         ctx->stream, (const DevSim*)ctx->d_S, n);
+      time_end(ctx);
+      SGN_HIP(ctx, hipGetLastError());
+      enq += n;
+      if ((rc = sync_ctrl(ctx))) return rc;
+    }
+    if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
+    return 0;
+  }
   while (ctx->h_ctrl->active && enq < max_rounds) {
     const uint64_t n = std::min<uint64_t>(batch, max_rounds - enq);
     if (graph && n == batch) {

@@ -94,6 +94,7 @@ struct Ctrl {
   uint64_t max_bucket;    // high-water mark of any (bucket, host group) slab fill
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
+  uint64_t epoch;         // persistent rounds: round edges published (grid barrier)
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -106,6 +107,7 @@ enum : uint32_t {
   OVF_SEG = 8u,
   OVF_EXCHANGE = 16u,
   OVF_TRACE = 32u,
+  OVF_TIMEOUT = 64u,  // a persistent grid barrier gave up (grid not resident)
 };
 
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
@@ -338,6 +340,7 @@ struct sgn_ctx {
   std::vector<std::pair<int, size_t>> graph_timed;
   bool graph_pending = false;
   bool use_graph = true;
+  uint32_t persist_grid = 0;  // persistent-rounds grid size (0: per-round launches)
   bool capturing = false;
 
   ~sgn_ctx();
