@@ -106,7 +106,7 @@ def main():
     g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
 
     ctx = sgn.Context(device=local, shard_rank=rank, shard_count=world,
-                      flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around k_execute
+                      flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around the round kernel
     ctx.routes_build(g, used)
     apsp = ctx.routes_timing()
     ctx.hosts_set(hosts)
@@ -128,7 +128,9 @@ def main():
     for _ in range(args.warmup):
         ctx.run(args.rounds_per_step)
     st0 = ctx.stats()
-    kt0 = ctx.kernel_times()["k_execute"]
+    # the round kernel: k_rounds (persistent, many rounds per launch) or k_execute
+    rk = "k_rounds" if "k_rounds" in ctx.kernel_times() else "k_execute"
+    kt0 = ctx.kernel_times()[rk]
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -136,7 +138,7 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     st1 = ctx.stats()
-    kt1 = ctx.kernel_times()["k_execute"]
+    kt1 = ctx.kernel_times()[rk]
     ev = events_of(st1) - events_of(st0)
     if dist:
         import torch
@@ -164,19 +166,19 @@ def main():
         achieved = alg_bytes / launches / avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_execute", "avg_launch_us": round(avg_s * 1e6, 2),
+                "kernel": rk, "avg_launch_us": round(avg_s * 1e6, 2),
                 "alg_bytes_per_launch": int(alg_bytes / launches),
                 "units_per_launch": {"packets": round(n_pkt / launches, 1),
                                      "active_host_rounds": round(host_exec / launches, 1)}}
         # HBM bytes per launch measured by PMC (tools/pmc_traffic.sh: FETCH_SIZE x2 +
         # WRITE_SIZE over the same default run's timed dispatches), when it matches this run
-        tf = ROOT / "profiles" / "k_execute_traffic.json"
+        tf = ROOT / "profiles" / "round_kernel_traffic.json"
         default_run = (args.hosts, args.nodes, args.rounds_per_step, args.steps, args.warmup,
                        world) == (100_000, 1000, 100, 10, 5, 1)
         if tf.exists() and default_run:
             t = json.loads(tf.read_text())
             roof["traffic"] = t["traffic_bytes_per_launch"]
-            roof["traffic_unit"] = "bytes/launch (PMC, profiles/k_execute_traffic.json)"
+            roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
             roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
     out = {
         "metric": METRIC,

@@ -2319,6 +2319,8 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
     out->ms[i] = ctx->kt[i].ms;
     out->name[i] = kKernelNames[i];
   }
+  // the round kernel's slot: persistent launches (many rounds each) when enabled
+  if (ctx->persist_grid) out->name[K_EXECUTE] = "k_rounds";
   return 0;
 }
 
