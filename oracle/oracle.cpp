@@ -17,7 +17,11 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <atomic>
 #include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <queue>
 #include <string>
 #include <unordered_map>
@@ -900,6 +904,19 @@ struct Host {
 
 }  // namespace
 
+// Per-thread worker state, as the reference's thread-local Worker (core/worker.rs): the
+// current time, this round's counters, trace records and exports, and the lowest used
+// latency seen (Worker::update_lowest_used_latency); merged at the round barrier.
+struct Wk {
+  uint64_t now = 0;
+  sgn_stats st{};
+  std::vector<sgn_trace_rec> tr;
+  std::vector<uint64_t> exports;
+  bool min_set = false;
+  uint64_t min_used = 0;
+};
+static thread_local Wk* tl_wk = nullptr;
+
 struct ora_sim {
   std::vector<uint32_t> used;
   uint32_t U = 0;
@@ -916,8 +933,14 @@ struct ora_sim {
   uint64_t min_used = 0;
   uint64_t ws = 0, we = 0;
   bool active = true;
-  uint64_t now = 0;
   uint64_t round_end = 0;
+  // worker threads (thread-per-core round, core/manager.rs:568-601): hosts are taken in
+  // chunks from a shared counter (work stealing); pushes into another host's queue take that
+  // host's mutex (Mutex<EventQueue>, core/worker.rs:603-613)
+  int nthreads = 1;
+  std::vector<Wk> wks = std::vector<Wk>(1);
+  std::unique_ptr<std::mutex[]> qmu;
+  Wk& W() { return *tl_wk; }
   sgn_stats st;
   bool trace = false;
   std::vector<sgn_trace_rec> tr;
@@ -941,7 +964,7 @@ struct ora_sim {
     r.b = b;
     r.c = c;
     r.seq = seq;
-    tr.push_back(r);
+    W().tr.push_back(r);
   }
 
   bool owned(uint32_t host) const { return host >= lo && host < hi; }
@@ -963,7 +986,12 @@ struct ora_sim {
     ev.eid = h.eid_ctr++;
     ev.task = task;
     if (t >= end_time) return;
-    h.q.push(ev);
+    if (nthreads > 1) {
+      std::lock_guard<std::mutex> g(qmu[h.id]);
+      h.q.push(ev);
+    } else {
+      h.q.push(ev);
+    }
   }
 
   // Relay::notify (relay/mod.rs:111-136)
@@ -976,23 +1004,23 @@ struct ora_sim {
   void forward_later(Host& h, int which, uint64_t delay) {
     Relay& r = which == TASK_RELAY_OUT ? h.rout : h.rin;
     r.state = RELAY_PENDING;
-    schedule_task(h, which, now + delay);
+    schedule_task(h, which, W().now + delay);
   }
 
   // App-side delivery at the interface (NetworkInterface::push -> socket; synthetic sink).
   void deliver_to_app(Host& h, const Pkt& p, bool local) {
     if (local) {
-      st.local_delivered++;
+      W().st.local_delivered++;
       sgn_drun_flush_seq(&h.d_app, &h.r_app);  // a local delivery is a run of its own
-      h.d_app = sgn_digest3(h.d_app, now, (uint64_t)p.src_host | (1ULL << 62) | (1ULL << 32),
+      h.d_app = sgn_digest3(h.d_app, W().now, (uint64_t)p.src_host | (1ULL << 62) | (1ULL << 32),
                             p.payload);
       return;
     }
-    st.delivered++;
-    st.bytes_delivered += p.payload;
+    W().st.delivered++;
+    W().st.bytes_delivered += p.payload;
     h.n_delivered++;
-    sgn_drun_add_seq(&h.d_app, &h.r_app, now, p.src_host, p.src_eid, 1);
-    trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, now, 0, p.src_eid);
+    sgn_drun_add_seq(&h.d_app, &h.r_app, W().now, p.src_host, p.src_eid, 1);
+    trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, W().now, 0, p.src_eid);
     if (traffic.kind == SGN_TRAFFIC_TGEN && h.is_server && (p.tag & SGN_TAG_REQ)) {
       uint64_t size = traffic.file_bytes[p.tag & 3u];
       uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
@@ -1002,20 +1030,20 @@ struct ora_sim {
         h.fifo.push_back({hosts[p.src_host].ip, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP});
         relay_notify(h, TASK_RELAY_OUT);
       } else {
-        st.app_blocked++;
+        W().st.app_blocked++;
       }
     }
   }
 
   // Worker::send_packet (core/worker.rs:330-403)
   void send_packet(Host& h, Pkt p) {
-    if (now >= end_time) return;  // is_completed (:334,338-341)
-    bool bootstrapping = now < bootstrap_end;
+    if (W().now >= end_time) return;  // is_completed (:334,338-341)
+    bool bootstrapping = W().now < bootstrap_end;
     auto it = dns.find(p.dst_ip);  // resolve_ip_to_host_id (:347, dns.rs:174)
     if (it == dns.end()) {
-      st.packets_unknown_dst++;
-      sgn_drun_add_same(&h.d_tx, &h.r_tx, now, 0xFFFFFFFFULL | (2ULL << 32), 0, 1);
-      trace_rec(h, SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+      W().st.packets_unknown_dst++;
+      sgn_drun_add_same(&h.d_tx, &h.r_tx, W().now, 0xFFFFFFFFULL | (2ULL << 32), 0, 1);
+      trace_rec(h, SGN_TRACE_SEND, 0xFFFFFFFFu, 2, W().now, 0, 0);
       return;
     }
     uint32_t dst = it->second;
@@ -1025,26 +1053,20 @@ struct ora_sim {
     double reliability = (double)rel32;
     double chance = h.rng.next_f64();  // :366
     if (!bootstrapping && chance >= reliability && p.payload > 0) {  // :371
-      st.packets_loss_dropped++;
-      sgn_drun_add_same(&h.d_tx, &h.r_tx, now, (uint64_t)dst | (1ULL << 32), 0, 1);
-      trace_rec(h, SGN_TRACE_SEND, dst, 1, now, 0, 0);
+      W().st.packets_loss_dropped++;
+      sgn_drun_add_same(&h.d_tx, &h.r_tx, W().now, (uint64_t)dst | (1ULL << 32), 0, 1);
+      trace_rec(h, SGN_TRACE_SEND, dst, 1, W().now, 0, 0);
       return;
     }
     uint64_t delay = lat[ri];  // :376
     // Worker::update_lowest_used_latency -> Runahead (runahead.rs:61-107), dynamic only
-    if (cfg.use_dynamic_runahead) {
-      if (!local_min_used_set || delay < local_min_used) {
-        local_min_used_set = true;
-        local_min_used = delay;
-      }
-      if (!has_min_used || delay < min_used) {
-        has_min_used = true;
-        min_used = delay;
-      }
+    if (cfg.use_dynamic_runahead && (!W().min_set || delay < W().min_used)) {
+      W().min_set = true;
+      W().min_used = delay;
     }
-    st.packets_sent++;
+    W().st.packets_sent++;
     h.n_sent++;
-    uint64_t deliver = now + delay;  // :387-390
+    uint64_t deliver = W().now + delay;  // :387-390
     if (deliver < round_end) deliver = round_end;
     // push_packet_to_host (:603-613): Event::new_packet consumes the SOURCE host's id
     Event ev;
@@ -1055,15 +1077,21 @@ struct ora_sim {
     ev.task = -1;
     p.src_eid = ev.eid;
     ev.pkt = p;
-    sgn_drun_add_same(&h.d_tx, &h.r_tx, now, (uint64_t)dst, deliver, 1);
-    trace_rec(h, SGN_TRACE_SEND, dst, 0, now, deliver, ev.eid);
+    sgn_drun_add_same(&h.d_tx, &h.r_tx, W().now, (uint64_t)dst, deliver, 1);
+    trace_rec(h, SGN_TRACE_SEND, dst, 0, W().now, deliver, ev.eid);
     if (owned(dst)) {
       Host& d = hosts[dst];
-      if (ev.time < d.last_popped) std::abort();  // event_queue.rs:59
-      d.q.push(ev);
+      if (nthreads > 1) {
+        std::lock_guard<std::mutex> g(qmu[dst]);
+        if (ev.time < d.last_popped) std::abort();  // event_queue.rs:59
+        d.q.push(ev);
+      } else {
+        if (ev.time < d.last_popped) std::abort();  // event_queue.rs:59
+        d.q.push(ev);
+      }
     } else {
       uint64_t rec[6] = {dst, ev.time, ev.src_host, ev.eid, p.payload, p.tag};
-      exports.insert(exports.end(), rec, rec + 6);
+      W().exports.insert(W().exports.end(), rec, rec + 6);
     }
   }
 
@@ -1084,13 +1112,13 @@ struct ora_sim {
       *out = p;
       return true;
     }
-    // Router::pop -> CoDelQueue::pop(now) (router/mod.rs:65-68)
-    bool got = h.codel.pop(now, out);
+    // Router::pop -> CoDelQueue::pop(W().now) (router/mod.rs:65-68)
+    bool got = h.codel.pop(W().now, out);
     for (const Pkt& d : h.codel.dropped) {
-      st.codel_dropped++;
+      W().st.codel_dropped++;
       h.n_codel_dropped++;
-      sgn_drun_add_seq(&h.d_app, &h.r_app, now, (uint64_t)d.src_host | (1ULL << 63), d.src_eid, 1);
-      trace_rec(h, SGN_TRACE_CODEL_DROP, d.src_host, 0, now, 0, d.src_eid);
+      sgn_drun_add_seq(&h.d_app, &h.r_app, W().now, (uint64_t)d.src_host | (1ULL << 63), d.src_eid, 1);
+      trace_rec(h, SGN_TRACE_CODEL_DROP, d.src_host, 0, W().now, 0, d.src_eid);
     }
     h.codel.dropped.clear();
     return got;
@@ -1099,7 +1127,7 @@ struct ora_sim {
   // Relay::forward_until_blocked (relay/mod.rs:201-273); returns true and *dur if blocked
   bool forward_until_blocked(Host& h, int which, uint64_t* dur) {
     Relay& r = which == TASK_RELAY_OUT ? h.rout : h.rin;
-    bool bootstrapping = now < bootstrap_end;  // Worker::is_bootstrapping (worker.rs:482)
+    bool bootstrapping = W().now < bootstrap_end;  // Worker::is_bootstrapping (worker.rs:482)
     r.state = RELAY_FORWARDING;
     // src device address: eth0 = host ip for inet_out, router = 0.0.0.0 for inet_in
     uint32_t src_addr = which == TASK_RELAY_OUT ? h.ip : 0u;
@@ -1115,7 +1143,7 @@ struct ora_sim {
       bool is_local = src_addr == p.dst_ip;
       if (!bootstrapping && !is_local && r.limited) {
         uint64_t out;
-        if (!r.tb.remove(p.wire(), now, &out)) {
+        if (!r.tb.remove(p.wire(), W().now, &out)) {
           r.next = p;
           r.has_next = true;
           r.state = RELAY_IDLE;
@@ -1169,30 +1197,40 @@ struct ora_sim {
       h.fifo.push_back({dst_ip, payload, payload, 1, tag});
       relay_notify(h, TASK_RELAY_OUT);  // Host::notify_socket_has_packets (host.rs:969-983)
     } else {
-      st.app_blocked++;
+      W().st.app_blocked++;
     }
-    schedule_task(h, TASK_APP, now + next_delay);
+    schedule_task(h, TASK_APP, W().now + next_delay);
   }
 
   // Host::execute (host.rs:762-830)
   void execute(Host& h, uint64_t until) {
-    if (!h.q.empty() && h.q.top().time < until) st.host_executions++;
-    while (!h.q.empty() && h.q.top().time < until) {
-      Event ev = h.q.top();
+    // (pop under the host's own queue lock in threaded mode: other hosts push into it)
+    auto pop_due = [&](Event* out) {
+      std::unique_lock<std::mutex> g;
+      if (nthreads > 1) g = std::unique_lock<std::mutex>(qmu[h.id]);
+      if (h.q.empty() || h.q.top().time >= until) return false;
+      *out = h.q.top();
       h.q.pop();
+      return true;
+    };
+    bool first = true;
+    Event ev;
+    while (pop_due(&ev)) {
+      if (first) W().st.host_executions++;
+      first = false;
       if (ev.time < h.last_popped) std::abort();  // event_queue.rs:75
       h.last_popped = ev.time;
-      now = ev.time;  // Worker::set_current_time
+      W().now = ev.time;  // Worker::set_current_time
       if (ev.kind == EV_PACKET) {
-        st.packet_events_popped++;
+        W().st.packet_events_popped++;
         h.n_popped++;
         sgn_drun_add_seq(&h.d_rx, &h.r_rx, ev.time, ev.src_host, ev.eid, 1);
         trace_rec(h, SGN_TRACE_POP, ev.src_host, 0, ev.time, 0, ev.eid);
-        h.codel.push(ev.pkt, now);            // Router::route_incoming_packet (router/mod.rs:55)
+        h.codel.push(ev.pkt, W().now);            // Router::route_incoming_packet (router/mod.rs:55)
         relay_notify(h, TASK_RELAY_IN);       // notify_router_has_packets (host.rs:958)
-        st.max_codel_len = std::max<uint64_t>(st.max_codel_len, h.codel.elems.size());
+        W().st.max_codel_len = std::max<uint64_t>(W().st.max_codel_len, h.codel.elems.size());
       } else {
-        st.local_events++;
+        W().st.local_events++;
         if (ev.task == TASK_APP)
           app_task(h);
         else
@@ -1231,7 +1269,65 @@ struct ora_sim {
 
   void execute_round() {
     round_end = we;  // Worker::set_round_end_time (manager.rs:578)
-    for (uint32_t i = lo; i < hi; i++) execute(hosts[i], we);
+    if (nthreads <= 1) {
+      tl_wk = &wks[0];
+      for (uint32_t i = lo; i < hi; i++) execute(hosts[i], we);
+    } else {
+      std::atomic<uint32_t> next{lo};
+      auto worker = [&](int t) {
+        tl_wk = &wks[t];
+        while (true) {
+          const uint32_t a = next.fetch_add(256);
+          if (a >= hi) break;
+          const uint32_t e = std::min<uint32_t>(hi, a + 256);
+          for (uint32_t i = a; i < e; i++) execute(hosts[i], we);
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < nthreads; t++) th.emplace_back(worker, t);
+      worker(0);
+      for (auto& x : th) x.join();
+      tl_wk = &wks[0];
+    }
+    merge_workers();
+  }
+
+  // the round barrier (manager.rs:623-628): fold the workers' counters and minima
+  void merge_workers() {
+    for (Wk& w : wks) {
+      st.packets_sent += w.st.packets_sent;
+      st.packets_loss_dropped += w.st.packets_loss_dropped;
+      st.packets_unknown_dst += w.st.packets_unknown_dst;
+      st.packet_events_popped += w.st.packet_events_popped;
+      st.codel_dropped += w.st.codel_dropped;
+      st.delivered += w.st.delivered;
+      st.local_delivered += w.st.local_delivered;
+      st.app_blocked += w.st.app_blocked;
+      st.local_events += w.st.local_events;
+      st.bytes_delivered += w.st.bytes_delivered;
+      st.host_executions += w.st.host_executions;
+      st.max_codel_len = std::max(st.max_codel_len, w.st.max_codel_len);
+      w.st = sgn_stats{};
+      if (!w.tr.empty()) {
+        tr.insert(tr.end(), w.tr.begin(), w.tr.end());
+        w.tr.clear();
+      }
+      if (!w.exports.empty()) {
+        exports.insert(exports.end(), w.exports.begin(), w.exports.end());
+        w.exports.clear();
+      }
+      if (w.min_set) {
+        if (!local_min_used_set || w.min_used < local_min_used) {
+          local_min_used_set = true;
+          local_min_used = w.min_used;
+        }
+        if (!has_min_used || w.min_used < min_used) {
+          has_min_used = true;
+          min_used = w.min_used;
+        }
+        w.min_set = false;
+      }
+    }
   }
 };
 
@@ -1438,7 +1534,8 @@ int ora_sim_create(const uint32_t* used, uint32_t U, const uint64_t* lat, const 
     bool has_app = tr->kind == SGN_TRAFFIC_PERIODIC || (tr->kind == SGN_TRAFFIC_TGEN && !h.is_server);
     if (!has_app) continue;
     uint64_t t = SIM_START + sgn_app_start_rel(tr->flow_seed, i, tr->start_ns, tr->start_jitter_ns);
-    s->now = SIM_START;
+    tl_wk = &s->wks[0];
+    s->wks[0].now = SIM_START;
     s->schedule_task(h, TASK_APP, t);
   }
   *out = s;
@@ -1446,6 +1543,15 @@ int ora_sim_create(const uint32_t* used, uint32_t U, const uint64_t* lat, const 
 }
 
 void ora_sim_free(ora_sim* s) { delete s; }
+
+// Worker threads for the round loop (1 = sequential). Results do not depend on it.
+int ora_sim_set_threads(ora_sim* s, int n) {
+  if (n < 1 || n > 1024) return SGN_EINVAL;
+  s->nthreads = n;
+  s->wks.assign(n, Wk());
+  if (n > 1 && !s->qmu) s->qmu.reset(new std::mutex[s->hosts.size()]);
+  return 0;
+}
 
 int ora_sim_window(const ora_sim* s, uint64_t* start, uint64_t* end, int32_t* active) {
   *start = s->ws;

@@ -66,6 +66,7 @@ def load():
                                      C.POINTER(sgn.SimConfig), C.POINTER(sgn.Traffic), C.c_int,
                                      C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "ora_sim_free": (None, [vp]),
+        "ora_sim_set_threads": (C.c_int, [vp, C.c_int]),
         "ora_sim_window": (C.c_int, [vp, u64p, u64p, C.POINTER(C.c_int32)]),
         "ora_sim_round": (C.c_int, [vp, u64p]),
         "ora_sim_run": (C.c_int, [vp, C.c_uint64, u64p]),
@@ -155,7 +156,7 @@ def host_seeds(sim_seed, names):
 class Sim:
     """The reference-structured round loop (core/manager.rs:541-656) on the CPU."""
 
-    def __init__(self, used, lat, loss, hosts: sgn.HostArrays, cfg, traffic, trace=False):
+    def __init__(self, used, lat, loss, hosts: sgn.HostArrays, cfg, traffic, trace=False, threads=1):
         self.L = load()
         used = np.ascontiguousarray(used, dtype=np.uint32)
         lat = np.ascontiguousarray(lat, dtype=np.uint64).ravel()
@@ -170,6 +171,8 @@ class Sim:
         if rc != 0:
             raise sgn.SgnError(rc, err.value.decode())
         self.n = hosts.n
+        if threads != 1:
+            assert self.L.ora_sim_set_threads(self.h, threads) == 0
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -83,6 +83,18 @@ template <typename T>
 __device__ __forceinline__ void st_dev(SGN_GLB T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ EvRec ld_dev_rec(SGN_GLB const EvRec* p) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  EvRec r;
+  r.time = ld_dev(q);
+  r.eid = ld_dev(q + 1);
+  const uint64_t sd = ld_dev(q + 2), pt = ld_dev(q + 3);
+  r.src = (uint32_t)sd;
+  r.dst = (uint32_t)(sd >> 32);
+  r.pc = (uint32_t)pt;
+  r.tag = (uint32_t)(pt >> 32);
+  return r;
+}
 __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
   SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
   st_dev(q, r.time);
@@ -847,7 +859,7 @@ struct HostExec {
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
       const uint32_t b = bucket_of(S, deliver);
-      const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : S.bucket_slab[b]);
+      const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
       sink ^= atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
@@ -1298,7 +1310,7 @@ __device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
       const uint32_t j = j0 + lane;
       EvRec r;
-      if (j < n) r = pb[j];
+      if (j < n) r = ld_dev_rec(pb + j);
       const bool due = j < n && (!last || r.time < we);
       const bool keep = j < n && !due;
       const uint64_t dm = __ballot(due), km = __ballot(keep);
@@ -1562,13 +1574,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   SGN_EXEC_LDS(X)
   const uint32_t w = blockIdx.x, P = gridDim.x;
   const uint64_t e0 = ld_dev(&C->epoch);
+  // the spare slab and the bucket -> slab table change by one swap per round, the same on
+  // every workgroup: each keeps its own copy (LDS) and applies the swap itself
+  uint32_t ks = ld_dev(&C->keep_slab);
+  const bool lds_tab = S.NB <= LDS_BSLAB;
+  if (lds_tab)
+    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = ld_dev(&S.bucket_slab[i]);
+  __syncthreads();
   for (uint32_t r = 0; r < max_rounds; r++) {
     if (!ld_dev(&C->active)) break;
     const uint64_t ws = ld_dev(&C->ws), we = ld_dev(&C->we);
-    const uint32_t ks = ld_dev(&C->keep_slab);
-    if (S.NB <= LDS_BSLAB)
-      for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = ld_dev(&S.bucket_slab[i]);
-    __syncthreads();
     uint64_t kall = INVALID, mall = INVALID;
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
@@ -1577,18 +1592,21 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       mall = m < mall ? m : mall;
       __syncthreads();
     }
+    const uint32_t b1 = bucket_of(S, we - 1);
+    const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
     if (arrive(S, w, P, kall, mall)) {
-      const uint32_t b1 = bucket_of(S, we - 1);
-      finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks,
-                     S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]));
+      finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks, slab_b1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) st_dev(&C->epoch, e0 + r + 1);
     }
+    __syncthreads();
+    if (lds_tab && threadIdx.x == 0) X.lbs[b1] = ks;
+    ks = slab_b1;
     // grid barrier: wait for the round edge, bounded
     uint32_t spins = 0;
     bool ok = true;
     while (ld_dev(&C->epoch) < e0 + r + 1) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {
         ok = false;
         break;
@@ -1598,7 +1616,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
       return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // no acquire fence: every load of data another workgroup wrote in this launch is a
+    // device-scope atomic load (control words, slab fills, event records, bucket minima);
+    // the rest (host records, queues) belongs to this workgroup's groups
+    asm volatile("" ::: "memory");
     __syncthreads();
   }
 }
