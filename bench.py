@@ -130,7 +130,9 @@ def main():
         t = torch.tensor(list(bytes(idb)), dtype=torch.uint8)
         dist.broadcast(t, 0)
         idb = (sgn.C.c_uint8 * 128)(*t.tolist())
-        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 17))
+        # per-peer exchange slot: 8192 event runs (256 KB) per round; a round sends ~700 runs
+        # per peer at 100k hosts per GPU (overflow is detected and reported, never silent)
+        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 13))
     ctx.sim_init(cfg, tr)
 
     def barrier():

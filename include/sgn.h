@@ -280,6 +280,14 @@ int sgn_comm_get_unique_id(uint8_t id_out[SGN_COMM_ID_BYTES]);
  * exchange_slot_events = capacity (events) of each per-peer slot per round. */
 int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES],
                   uint64_t exchange_slot_events);
+/* Local shard group: ctxs[i] is shard i of n (sgn_create with shard_count n) in THIS
+ * process, on any devices (several may share one GPU). The round edge runs with device
+ * copies instead of RCCL (host-synchronous per round): a test transport that exercises the
+ * same device-side multi-shard path. Call before sgn_sim_init on every context; drive the
+ * rounds with sgn_run_local_group (not sgn_run). */
+int sgn_comm_init_local(sgn_ctx* const* ctxs, uint32_t n, uint64_t exchange_slot_events);
+int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds,
+                        uint64_t* rounds_done);
 /* Owned HostId range of a shard (same split on every rank). */
 int sgn_shard_range(uint32_t n_hosts, uint32_t shard_rank, uint32_t shard_count,
                     uint32_t* host_lo, uint32_t* host_hi);

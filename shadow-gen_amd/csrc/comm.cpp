@@ -14,11 +14,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "sgn_internal.h"
 
 namespace sgn {
+void launch_execute(sgn_ctx* ctx);
 void launch_finalize_local(sgn_ctx* ctx);
 void launch_import(sgn_ctx* ctx);
 void launch_advance(sgn_ctx* ctx, const uint64_t* red);
@@ -101,3 +104,92 @@ int comm_round_exchange(sgn_ctx* ctx) {
 }
 
 }  // namespace sgn
+
+// ------------------------------------------------------------------------------------
+// Local shard group: the same round-edge protocol between contexts of ONE process (any
+// devices, e.g. several shards on one GPU), with device copies in place of RCCL. It runs
+// the device-side multi-shard path (exchange slots, k_import, local finalize, window
+// advance) exactly as the RCCL transport does, so it can be checked against a single
+// shard on a one-GPU machine. Host-synchronous per round: a test transport, not a fast one.
+// ------------------------------------------------------------------------------------
+extern "C" {
+
+int sgn_comm_init_local(sgn_ctx* const* ctxs, uint32_t n, uint64_t slot_events) {
+  if (!ctxs || n < 2) return SGN_EINVAL;
+  if (slot_events == 0 || slot_events > (1ULL << 26)) return SGN_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    sgn_ctx* c = ctxs[i];
+    if (!c) return SGN_EINVAL;
+    if (c->nranks != n || c->rank != i)
+      return set_error(c, SGN_EINVAL, "local group: context i must be shard i of n");
+    if (c->sim_ready) return set_error(c, SGN_ESTATE, "sgn_comm_init_local must precede sgn_sim_init");
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    ctxs[i]->comm_local = true;
+    ctxs[i]->xslot = slot_events;
+    ctxs[i]->group.assign(ctxs, ctxs + n);
+  }
+  return 0;
+}
+
+int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, uint64_t* rounds_done) {
+  if (!ctxs || n < 2) return SGN_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    if (!ctxs[i] || !ctxs[i]->sim_ready || !ctxs[i]->comm_local || ctxs[i]->group.size() != n)
+      return ctxs[i] ? set_error(ctxs[i], SGN_ESTATE, "not a local shard group") : SGN_EINVAL;
+  uint64_t done = 0;
+  std::vector<uint32_t> cnt(n);
+  for (; done < max_rounds; done++) {
+    Ctrl h{};
+    SGN_HIP(ctxs[0], hipMemcpy(&h, (const void*)ctxs[0]->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    if (!h.active) break;
+    for (uint32_t i = 0; i < n; i++) {
+      SGN_HIP(ctxs[i], hipSetDevice(ctxs[i]->device));
+      launch_execute(ctxs[i]);
+    }
+    for (uint32_t i = 0; i < n; i++) SGN_HIP(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+    // the all-to-all: shard b's receive slot a <- shard a's send slot b
+    for (uint32_t a = 0; a < n; a++) {
+      sgn_ctx* A = ctxs[a];
+      SGN_HIP(A, hipMemcpy(cnt.data(), (const void*)A->S.xout_n, n * 4, hipMemcpyDeviceToHost));
+      for (uint32_t b = 0; b < n; b++) {
+        if (b == a) continue;
+        sgn_ctx* B = ctxs[b];
+        const uint32_t k = std::min<uint32_t>(cnt[b], (uint32_t)A->xslot);
+        if (k)
+          SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * B->S.xslot),
+                               (const void*)(A->S.xout + (size_t)b * A->S.xslot),
+                               (size_t)k * sizeof(EvRec), hipMemcpyDefault));
+        SGN_HIP(B, hipMemcpy((void*)(B->S.xin_n + a), &cnt[b], 4, hipMemcpyHostToDevice));
+      }
+    }
+    for (uint32_t i = 0; i < n; i++) {
+      sgn_ctx* c = ctxs[i];
+      SGN_HIP(c, hipSetDevice(c->device));
+      SGN_HIP(c, hipMemsetAsync((void*)(c->S.xin_n + c->S.rank), 0, 4, c->stream));
+      launch_import(c);
+      SGN_HIP(c, hipMemsetAsync((void*)c->S.xout_n, 0, (size_t)c->S.n_ranks * 4, c->stream));
+      launch_finalize_local(c);
+    }
+    // all-reduce(min) of {round_min, min_used}
+    uint64_t red[2] = {~0ULL, ~0ULL};
+    for (uint32_t i = 0; i < n; i++) {
+      sgn_ctx* c = ctxs[i];
+      SGN_HIP(c, hipStreamSynchronize(c->stream));
+      uint64_t v[2];
+      SGN_HIP(c, hipMemcpy(v, (const void*)&c->S.ctrl->round_min, 16, hipMemcpyDeviceToHost));
+      red[0] = std::min(red[0], v[0]);
+      red[1] = std::min(red[1], v[1]);
+    }
+    for (uint32_t i = 0; i < n; i++) {
+      sgn_ctx* c = ctxs[i];
+      SGN_HIP(c, hipMemcpy((void*)&c->S.ctrl->round_min, red, 16, hipMemcpyHostToDevice));
+      launch_advance(c, (const uint64_t*)&c->S.ctrl->round_min);
+      SGN_HIP(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  if (rounds_done) *rounds_done = done;
+  return 0;
+}
+
+}  // extern "C"

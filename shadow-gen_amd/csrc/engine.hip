@@ -2074,7 +2074,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     if ((rc = up32(rl, &S.rank_lo))) return rc;
   }
   if (ctx->nranks > 1) {
-    if (!ctx->comm) return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init before sgn_sim_init");
+    if (!ctx->comm && !ctx->comm_local)
+      return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init (or sgn_comm_init_local) before sgn_sim_init");
     S.xslot = (uint32_t)ctx->xslot;
     S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
     S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
@@ -2375,6 +2376,10 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
 
 // hooks used by comm.cpp
 namespace sgn {
+void launch_execute(sgn_ctx* ctx) {
+  hipLaunchKernelGGL(k_execute, dim3(ctx->S.G), dim3(64), exec_lds_bytes(ctx->S.CAP), ctx->stream,
+                     (const DevSim*)ctx->d_S);
+}
 void launch_finalize_local(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->S, 0);
 }

@@ -320,6 +320,8 @@ struct sgn_ctx {
 
   // multi-GPU
   void* comm = nullptr;  // ncclComm_t
+  bool comm_local = false;           // local shard group (sgn_comm_init_local)
+  std::vector<sgn_ctx*> group;       // ... its contexts, shard order
   uint64_t xslot = 0;
 
   // kernel timing

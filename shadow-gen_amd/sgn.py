@@ -174,6 +174,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_comm_get_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "sgn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_uint64]),
         "sgn_shard_range": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p]),
+        "sgn_comm_init_local": (C.c_int, [C.POINTER(vp), C.c_uint32, C.c_uint64]),
+        "sgn_run_local_group": (C.c_int, [C.POINTER(vp), C.c_uint32, C.c_uint64, u64p]),
         "sgn_worker_get_latency": (C.c_uint64, [vp, C.c_uint32, C.c_uint32]),
         "sgn_worker_is_routable": (C.c_int32, [vp, C.c_uint32, C.c_uint32]),
         "sgn_worker_get_bandwidth_up_bytes": (C.c_uint64, [vp, C.c_uint32]),

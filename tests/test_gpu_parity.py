@@ -232,3 +232,55 @@ def test_worker_exports(ctxf, oracle):
             assert c.L.sgn_worker_is_routable(c.h, be(hosts.ip[a]), be(hosts.ip[b])) == 1
     assert c.L.sgn_worker_get_latency(c.h, be(0x0A000001), be(hosts.ip[0])) == sgn.EMUTIME_INVALID
     assert c.L.sgn_worker_get_bandwidth_up_bytes(c.h, be(hosts.ip[3])) == hosts.bw_up[3] // 8
+
+
+@pytest.mark.parametrize("kind,dynamic", [("periodic", False), ("tgen", False), ("periodic", True)])
+def test_two_shards_one_gpu_match_single(ctxf, oracle, kind, dynamic):
+    """The multi-shard device path (per-peer exchange slots, k_import, local round edge,
+    min all-reduce, window advance) with two shards on one GPU through the local shard-group
+    transport: identical per-host digests, counters and final window to one shard (and so
+    to the oracle)."""
+    import ctypes as C
+    n = 300
+    if kind == "tgen":
+        bw = np.where(np.arange(n) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+        args = scenario(n=n, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=600_000_000, bw=bw, tor=True,
+                        tgen_think=100_000_000)
+    else:
+        args = scenario(n=n, dynamic=dynamic, runahead_ns=0 if dynamic else 1_000_000,
+                        stop_ns=300_000_000)
+    g, used, hosts, cfg, tr = args
+    one = ctxf()
+    one.routes_build(g, used)
+    one.hosts_set(hosts)
+    one.sim_init(cfg, tr)
+    one.run()
+    shards = [ctxf(shard_rank=r, shard_count=2) for r in range(2)]
+    arr = (C.c_void_p * 2)(*[c.h.value for c in shards])
+    for c in shards:
+        c.routes_build(g, used)
+        c.hosts_set(hosts)
+    shards[0].check(shards[0].L.sgn_comm_init_local(arr, 2, 1 << 16))
+    for c in shards:
+        c.sim_init(cfg, tr)
+    done = C.c_uint64()
+    shards[0].check(shards[0].L.sgn_run_local_group(arr, 2, 1 << 40, C.byref(done)))
+    s1 = one.stats()
+    tot = {k: 0 for k in s1}
+    for r, c in enumerate(shards):
+        lo, hi = C.c_uint32(), C.c_uint32()
+        c.L.sgn_shard_range(n, r, 2, C.byref(lo), C.byref(hi))
+        d1, d2 = one.digests(lo.value, hi.value), c.digests(lo.value, hi.value)
+        for f in ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered",
+                  "n_codel_dropped"):
+            assert np.array_equal(d1[f], d2[f]), (r, f)
+        assert c.window() == one.window()
+        st = c.stats()
+        for k in ("packets_sent", "packets_loss_dropped", "packets_unknown_dst",
+                  "packet_events_popped", "delivered", "codel_dropped", "local_events"):
+            tot[k] += st[k]
+    assert s1["packets_sent"] > 1000
+    for k in ("packets_sent", "packets_loss_dropped", "packets_unknown_dst", "packet_events_popped",
+              "delivered", "codel_dropped", "local_events"):
+        assert tot[k] == s1[k], k
+    assert done.value == s1["rounds"]
