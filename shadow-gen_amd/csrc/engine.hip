@@ -1173,44 +1173,50 @@ __device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
 __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uint64_t ws,
                                uint64_t we, uint32_t ks, uint32_t slab_b1) {
   SGN_GLB Ctrl* C = S.ctrl;
-  uint64_t kk = INVALID, wn = INVALID;
+  const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
+  // one round trip: every value to read (chunk minima, spare-slab minimum, bucket minima,
+  // lowest used latency) is fetched at once; the buckets [b0, b1) are consumed and b1 is
+  // replaced, so neither is read
+  uint64_t kk = INVALID, wn = INVALID, m = INVALID;
   for (uint32_t i = lane; i < nch; i += 64) {
     const uint64_t a = __hip_atomic_exchange(&S.fin_keep[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t b = __hip_atomic_exchange(&S.fin_next[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st_dev(&S.fin_cnt[i], 0u);
     kk = a < kk ? a : kk;
     wn = b < wn ? b : wn;
   }
-  if (lane == 0) st_dev(&S.fin_cnt[nch], 0u);
+  for (uint32_t b = lane; b < S.NB; b += 64) {
+    const bool consumed = ((b - b0) & (S.NB - 1)) < ((b1 - b0) & (S.NB - 1)) || b == b1;
+    if (!consumed) {
+      const uint64_t bm = ld_dev(&S.bucket_min[b]);
+      m = bm < m ? bm : m;
+    }
+  }
+  uint64_t km = INVALID, mu = INVALID;
+  if (lane == 0) {
+    km = __hip_atomic_exchange(&C->keep_min, (unsigned long long)INVALID, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    mu = ld_dev(&C->min_used);
+  }
   kk = wave_min_u64(kk);
   wn = wave_min_u64(wn);
-  const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
+  m = wave_min_u64(m);
+  // then the writes (the caller drains them before publishing the round edge)
+  for (uint32_t i = lane; i <= nch; i += 64) st_dev(&S.fin_cnt[i], 0u);
   if (lane == 0) {
     for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1))
       st_dev(&S.bucket_min[b], (uint64_t)INVALID);  // consumed
     // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
     st_dev(&S.bucket_slab[b1], ks);
     st_dev(&C->keep_slab, slab_b1);
-    const uint64_t km = __hip_atomic_exchange(&C->keep_min, (unsigned long long)INVALID,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st_dev(&S.bucket_min[b1], km < kk ? km : kk);
-  }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint64_t m = INVALID;
-  for (uint32_t b = lane; b < S.NB; b += 64) {
-    const uint64_t bm = ld_dev(&S.bucket_min[b]);
-    m = bm < m ? bm : m;
-  }
-  m = wave_min_u64(m);
-  if (lane == 0) {
+    const uint64_t nb1 = km < kk ? km : kk;
+    st_dev(&S.bucket_min[b1], nb1);
+    m = nb1 < m ? nb1 : m;
     m = wn < m ? wn : m;
     const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
     st_dev(&C->last_min_next, min_next);
     // Runahead::get (runahead.rs:44-57)
-    const uint64_t mu = ld_dev(&C->min_used);
     uint64_t ra = (S.dynamic && mu != INVALID) ? mu : S.min_possible;
     ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
     // Controller::manager_finished_current_round (controller.rs:88-112)
@@ -1584,6 +1590,12 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   for (uint32_t r = 0; r < max_rounds; r++) {
     if (!ld_dev(&C->active)) break;
     const uint64_t ws = ld_dev(&C->ws), we = ld_dev(&C->we);
+    // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
+    // round edge done} on the 100 MHz clock
+    SGN_GLB uint64_t* rd = S.stamps ? S.rdbg + 3 * (size_t)(r & 127) : nullptr;
+    if (rd && threadIdx.x == 0)
+      __hip_atomic_fetch_min(rd, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t kall = INVALID, mall = INVALID;
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
@@ -1594,10 +1606,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     }
     const uint32_t b1 = bucket_of(S, we - 1);
     const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
+    if (rd && threadIdx.x == 0)
+      __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (arrive(S, w, P, kall, mall)) {
       finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks, slab_b1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) st_dev(&C->epoch, e0 + r + 1);
+      if (threadIdx.x == 0) {
+        if (rd) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
+        st_dev(&C->epoch, e0 + r + 1);
+      }
     }
     __syncthreads();
     if (lds_tab && threadIdx.x == 0) X.lbs[b1] = ks;
@@ -2055,7 +2073,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if ((rc = up32(bslab, &S.bucket_slab))) return rc;
   std::vector<uint64_t> bmin(NB, INVALID);
   if ((rc = up64(bmin, &S.bucket_min))) return rc;
-  if (getenv("SGN_STAMPS")) S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
+  if (getenv("SGN_STAMPS")) {
+    S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
+    S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 3 * 128);
+  }
   if (ctx->trace_cap) {
     S.trace = (decltype(S.trace))dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
     if (!S.trace) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
@@ -2348,6 +2369,18 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
 
 // Diagnostics: per-wave {cycles, events, max lane events, busy lanes} of the last k_execute
 // (allocated when SGN_STAMPS=1 is set in the environment at sgn_sim_init).
+// Diagnostics of the last persistent launch: per round {earliest start, latest arrival,
+// round edge done} (100 MHz clock), 128 rounds; resets the buffer for the next launch.
+int sgn_debug_rounds(sgn_ctx* ctx, uint64_t* out) {
+  if (!ctx || !ctx->sim_ready || !ctx->S.rdbg) return SGN_EINVAL;
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SGN_HIP(ctx, hipMemcpy(out, (const void*)ctx->S.rdbg, 3 * 128 * 8, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> init(3 * 128, 0);
+  for (int r = 0; r < 128; r++) init[3 * r] = ~0ULL;
+  SGN_HIP(ctx, hipMemcpy((void*)ctx->S.rdbg, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (!ctx || !ctx->sim_ready) return SGN_EINVAL;
   const uint64_t waves = ctx->S.G;

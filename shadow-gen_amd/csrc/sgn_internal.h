@@ -258,6 +258,7 @@ struct DevSim {
   uint64_t BW;
   UDiv64 bw_div;          // division by BW
   SGN_GLB uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
+  SGN_GLB uint64_t* rdbg;       // ... per-round timeline of the persistent kernel
   uint32_t n_ranks;
   SGN_GLB Ctrl* ctrl;
   // trace

@@ -189,6 +189,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_units_parse": (C.c_int, [C.c_int32, C.c_char_p, u64p]),
         "sgn_selftest_codel_law": (C.c_int, [vp, C.c_uint64, u64p]),
         "sgn_debug_stamps": (C.c_int, [vp, u64p, C.c_uint64, u64p]),
+        "sgn_debug_rounds": (C.c_int, [vp, u64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
