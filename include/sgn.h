@@ -339,7 +339,7 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out);
  * events handled, max events of one host, hosts with events, then (diagnostic build
  * libsgn_diag.so only) lane 0's per-event-kind cycles and counts}. Needs SGN_STAMPS=1 in
  * the environment at sgn_sim_init; n = number of waves (0 when disabled), cap in waves. */
-#define SGN_STAMP_WORDS 48
+#define SGN_STAMP_WORDS 96
 int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n);
 /* Per-round timeline of the last persistent launch (SGN_STAMPS=1): 128 x {earliest round
  * start, latest arrival at the round barrier, round edge done} on the 100 MHz clock. */

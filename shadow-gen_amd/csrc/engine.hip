@@ -177,7 +177,8 @@ struct LaneLDS {
   sgn_drun run[3];   // tx, rx, app (sgn_workload.h)
   uint64_t dig[3];   // tx, rx, app digests
   CodelEnt hd, tl;   // head run being consumed / tail run being extended
-  uint64_t tbc[4];   // token buckets' refill increments [2] and capacities [2]
+  uint64_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU)
+  uint64_t cq[4];    // CoDel drop state: interval end, drop next, current / previous count
   FifoEnt fh;        // copy of the send queue's head entry ...
   uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
   uint64_t rc_T;
@@ -201,7 +202,7 @@ struct HostExec {
   uint64_t ri_eid;
   uint64_t tbb0, tbl0, tbb1, tbl1;  // balances / last refills (capacity, increment: memory)
   uint32_t cq_head, cq_nr, cq_len;  // head run slot, runs in the ring, packets queued
-  uint64_t cq_bytes;  // (CoDel drop-state fields: memory, slow path only)
+  uint64_t cq_bytes;  // (CoDel drop state: the lane's LDS slot)
   uint32_t fq_head, fq_len;
   // per-round counter increments (a host cannot see 2^32 events in one window)
   uint32_t c_sent, c_loss, c_popped, c_deliv, c_localev, c_maxcodel;
@@ -271,8 +272,10 @@ struct HostExec {
     L->rc_T = r.rc_T;
     L->tbc[0] = r.tb_inc[0];
     L->tbc[1] = r.tb_inc[1];
-    L->tbc[2] = r.tb_cap[0];
-    L->tbc[3] = r.tb_cap[1];
+    L->cq[0] = r.cq_ie;
+    L->cq[1] = r.cq_dn;
+    L->cq[2] = r.cq_cur;
+    L->cq[3] = r.cq_prev;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
@@ -338,6 +341,10 @@ struct HostExec {
     r.n_sent += c_sent;
     r.n_popped += c_popped;
     r.n_delivered += c_deliv;
+    r.cq_ie = L->cq[0];
+    r.cq_dn = L->cq[1];
+    r.cq_cur = L->cq[2];
+    r.cq_prev = L->cq[3];
     S.nextloc[h] = next_local_time();
     if (hd_valid) *cq_slot(0) = L->hd;
     if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
@@ -445,7 +452,7 @@ struct HostExec {
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
       if (b < bal) b = ~0ULL;
-      const uint64_t cap = L->tbc[2 + W];
+      const uint64_t cap = inc + SGN_CONFIG_MTU;  // every relay's bucket: sim_init
       bal = b > cap ? cap : b;
       uint64_t adv = mul_sat(interval, nref, SIMTIME_MAX);
       last = emu_sat_add(last, adv);
@@ -526,9 +533,9 @@ struct HostExec {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    if (fl & F_CODEL_IE) return now >= R->cq_ie;
+    if (fl & F_CODEL_IE) return now >= L->cq[0];
     fl |= F_CODEL_IE;
-    R->cq_ie = emu_sat_add(now, CODEL_INTERVAL);
+    L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
     return false;
   }
   // the head run into registers (queue not empty)
@@ -574,7 +581,7 @@ struct HostExec {
   }
   __device__ bool codel_was_dropping_recently() const {  // :273-281
     if (!(fl & F_CODEL_DN)) return false;
-    return sat_sub(now, R->cq_dn) < CODEL_INTERVAL * 16;
+    return sat_sub(now, L->cq[1]) < CODEL_INTERVAL * 16;
   }
   // CoDelQueue::pop (:125-201)
   __device__ bool codel_pop(Pkt* out) {
@@ -596,24 +603,24 @@ struct HostExec {
       bool nok;
       bool has_n = codel_pop_raw(&n, &nok);
       fl |= F_CODEL_DROP;
-      uint64_t delta = sat_sub(R->cq_cur, R->cq_prev);
-      R->cq_cur = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      uint64_t delta = sat_sub(L->cq[2], L->cq[3]);
+      L->cq[2] = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
       fl |= F_CODEL_DN;
-      R->cq_dn = codel_law(now, R->cq_cur);
-      R->cq_prev = R->cq_cur;
+      L->cq[1] = codel_law(now, L->cq[2]);
+      L->cq[3] = L->cq[2];
       if (has_n) *out = n;
       return has_n;
     }
     // drop_from_drop_mode (:172-201)
     bool has_item = true;
     Pkt item = p;
-    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= R->cq_dn) {
+    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= L->cq[1]) {
       codel_drop(item);
-      R->cq_cur++;
+      L->cq[2]++;
       bool iok = false;
       has_item = codel_pop_raw(&item, &iok);
       if (has_item && iok)
-        R->cq_dn = codel_law(R->cq_dn, R->cq_cur);
+        L->cq[1] = codel_law(L->cq[1], L->cq[2]);
       else
         fl &= ~F_CODEL_DROP;
     }
@@ -1026,6 +1033,10 @@ struct HostExec {
   __device__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
                       uint64_t until) {
     uint32_t pi = s0;
+#ifdef SGN_DIAG
+    uint32_t it_mask = 99;
+    uint64_t it_t = 0;
+#endif
     while (true) {
       // earliest local event by (time, event id)
       uint64_t lt = st0, le = se0;
@@ -1033,19 +1044,30 @@ struct HostExec {
       if (st1 < lt || (st1 == lt && se1 < le)) { lt = st1; le = se1; ls = 1; }
       if (st2 < lt || (st2 == lt && se2 < le)) { lt = st2; le = se2; ls = 2; }
 #ifdef SGN_DIAG
-      {  // wave-level: iterations, and iterations in which some lane runs each handler
+      {  // wave-level: iterations, and iterations in which some lane runs each handler;
+         // the previous iteration's cycles are added to its handler combination's slot
         const bool ispop = pi < s1 && ev[ord[pi]].time <= lt;
         const int kind = ispop ? 0 : (lt >= until ? 4 : 1 + ls);
         const uint64_t act = __ballot(1);
         const uint64_t b0 = __ballot(kind == 0), b1 = __ballot(kind == 1),
                        b2 = __ballot(kind == 2), b3 = __ballot(kind == 3);
+        const uint64_t tnow = __builtin_amdgcn_s_memtime();
         if ((uint32_t)(__ffsll((long long)act) - 1) == (threadIdx.x & 63)) {
           wk[0]++;
           wk[1] += b0 != 0;
           wk[2] += b1 != 0;
           wk[3] += b2 != 0;
           wk[4] += b3 != 0;
+          if (S.stamps) {
+            SGN_GLB uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)(h >> S.gsh);
+            if (it_mask < 16) {
+              st[48 + it_mask] += tnow - it_t;
+              st[64 + it_mask] += 1;
+            }
+          }
         }
+        it_mask = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u) | (b3 ? 8u : 0u);
+        it_t = tnow;
       }
 #endif
       if (pi < s1) {
@@ -1286,6 +1308,10 @@ __device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we
   const uint32_t nbk = ((be + S.NB - bs) & (S.NB - 1)) + 1;  // buckets overlapping the window
   const uint32_t gbase = S.lo + (g << S.gsh);  // HostId of lane 0
   const uint64_t clk0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#ifdef SGN_DIAG
+  if (S.stamps && lane < 32) S.stamps[SGN_STAMP_WORDS * (size_t)g + 48 + lane] = 0;
+  __syncthreads();
+#endif
   const uint64_t rt0 = S.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const size_t ik = (size_t)ks * S.G + g;
   SGN_GLB EvRec* pk = S.pool + ik * S.CAP;

@@ -113,7 +113,7 @@ enum : uint32_t {
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
 // A round touches only the hosts with something due (~1 in 8 at the bench workload), so a
 // record per host turns each executed host's state into 3 contiguous cache lines; the hot
-// part (bytes 0..303) is what Host::execute reads and writes every time it runs.
+// part (bytes 0..327) is what Host::execute reads and writes every time it runs.
 struct __attribute__((aligned(128))) HostRec {
   uint64_t rng[4];           // Xoshiro256++ state (host/host.rs:234)
   uint64_t eid;              // next event id (host.rs:259,662-666)
@@ -132,15 +132,15 @@ struct __attribute__((aligned(128))) HostRec {
   uint32_t cq_nr, cq_len, fq_head, fq_len;   // CoDel runs / packets; send queue
   uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
   uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
+  uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
   // cold: rare paths only
   uint64_t app_k;                            // synthetic app counter
-  uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
-  uint64_t tseq;                             // trace sequence
+  uint64_t tseq;                            // trace sequence
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
   uint64_t pad[17];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
-static_assert(offsetof(HostRec, n_sent) + 24 <= 304, "hot part");
+static_assert(offsetof(HostRec, cq_prev) + 8 <= 384, "hot part: three cache lines");
 
 // per-wave counters (DevSim::w_cnt rows of G)
 enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_N };

@@ -21,7 +21,7 @@ EMUTIME_INVALID = 0xFFFFFFFFFFFFFFFF
 EMUTIME_MAX = 0xFFFFFFFFFFFFFFFE
 TRAFFIC_PERIODIC = 1
 TRAFFIC_TGEN = 2
-STAMP_WORDS = 48  # include/sgn.h SGN_STAMP_WORDS
+STAMP_WORDS = 96  # include/sgn.h SGN_STAMP_WORDS
 CREATE_TIME_KERNELS = 1
 
 u32p = C.POINTER(C.c_uint32)

@@ -51,6 +51,15 @@ for r in range(3):
         it = s[:, 35:40]
         print(f"   wave loop iterations median: all={np.median(it[:, 0]):.0f} pop={np.median(it[:, 1]):.0f} ro={np.median(it[:, 2]):.0f} ri={np.median(it[:, 3]):.0f} app={np.median(it[:, 4]):.0f}"
               f" | run cycles/iteration median={np.median(wr / np.maximum(it[:, 0], 1)):.0f}")
+        ct, cn = s[:, 48:64].sum(0), s[:, 64:80].sum(0)
+        names = ["pop", "ro", "ri", "app"]
+        rows = [m for m in range(16) if cn[m] > 0]
+        for m in rows:
+            print(f"     iter combo {'+'.join(n for k, n in enumerate(names) if m >> k & 1) or 'none':16s} n={cn[m]:7d} cycles/iter={ct[m] / cn[m]:8.0f}")
+        A = np.array([[(m >> k) & 1 for k in range(4)] + [1] for m in rows], dtype=float)
+        w = np.sqrt(cn[rows].astype(float))
+        coef, *_ = np.linalg.lstsq(A * w[:, None], (ct[rows] / cn[rows]) * w, rcond=None)
+        print("     per-handler cycles (fit): " + " ".join(f"{n}={c:.0f}" for n, c in zip(names + ["base"], coef)))
         top = np.argsort(cyc)[::-1][:3]
         for i in top:
             print(f"     top wave {i}: iters={it[i].tolist()} run={wr[i]} cyc/iter={wr[i] / max(it[i, 0], 1):.0f}")
