@@ -162,6 +162,9 @@ typedef struct sgn_sim_config {
  * functions are defined once in sgn_workload.h. */
 #define SGN_TRAFFIC_PERIODIC 1u /* configs B/D: every host sends one datagram per period */
 #define SGN_TRAFFIC_TGEN 2u     /* config C: clients fetch files from servers as MTU trains */
+#define SGN_TRAFFIC_EXTERNAL 3u /* no synthetic app: every host's application lives on the CPU;
+                                   its datagrams enter with sgn_submit and its deliveries and
+                                   drops leave with sgn_drain (the mixed real-app mode) */
 
 typedef struct sgn_traffic {
   uint32_t kind;
@@ -256,6 +259,80 @@ typedef struct sgn_trace_rec {
 int sgn_trace_enable(sgn_ctx* ctx, uint64_t capacity);
 /* Copies up to cap records (unordered; sort by (host, seq)). n_total = records produced. */
 int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_total);
+
+/* ------------------------------------------------------------------------------------ */
+/* CPU-resident applications (SGN_TRAFFIC_EXTERNAL)                                      */
+/* ------------------------------------------------------------------------------------ */
+
+/* Packet ingress: datagrams written by CPU-side applications (the socket send that ends in
+ * Host::notify_socket_has_packets, host.rs:969-983, and then relay_inet_out + Router::push +
+ * Worker::send_packet, worker.rs:330). Each datagram is queued on the device as an event of
+ * its source host at send_time; when the host reaches it (ordered with the host's packet
+ * events at that time by (source = itself, submission order)), it enters the host's socket
+ * send queue and the relay path takes it from there exactly like a synthetic app's datagram
+ * (token bucket, loss draw from the device-held host RNG, source event id, delivery time).
+ * Rules: traffic kind SGN_TRAFFIC_EXTERNAL; src_host owned by this shard; send_time in
+ * [current window start, stop time) and within the event calendar's horizon (the
+ * longest route latency ahead of the window); payload_len <= 65535; wire_len 0 or
+ * payload_len + 28 (UDP over IPv4, packet.rs:388-396,477-484,737-740). handle is opaque
+ * (the payload stays on the CPU) and comes back in the packet's drain record. Call between
+ * rounds; a failed call queues nothing. Replaces Worker::send_packet's CPU callers. */
+typedef struct sgn_pkt_soa {
+  uint64_t n;
+  const uint32_t* src_host;    /* [n] HostId */
+  const uint32_t* dst_ip;      /* [n] IPv4, host byte order (unknown: InetDropped) */
+  const uint32_t* payload_len; /* [n] UDP payload bytes */
+  const uint32_t* wire_len;    /* [n] or NULL */
+  const uint64_t* send_time;   /* [n] EmulatedTime */
+  const uint64_t* handle;      /* [n] opaque, returned by sgn_drain (may be NULL: 0) */
+} sgn_pkt_soa;
+int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* batch);
+
+/* Packet egress: one record per datagram that left the network core, on the host where it
+ * happened. Every submitted datagram yields exactly one record (delivered or dropped) once
+ * its fate is decided; datagrams sent to EXTERNAL hosts are all submitted ones. */
+#define SGN_DRAIN_DELIVERED 0u /* handed to the destination's interface (relay_inet_in) */
+#define SGN_DRAIN_LOCAL 1u     /* to the host's own address (loopback, relay is_local) */
+#define SGN_DRAIN_LOSS 2u      /* dropped by path reliability at send (worker.rs:366-371) */
+#define SGN_DRAIN_UNKNOWN 3u   /* destination not in the simulation (InetDropped, :347) */
+#define SGN_DRAIN_CODEL 4u     /* dropped by the destination router's CoDel (:319-321) */
+#define SGN_DRAIN_BLOCKED 5u   /* the source's socket send queue was full */
+typedef struct sgn_drain_rec {
+  uint64_t time;        /* when it happened (EmulatedTime) */
+  uint64_t src_eid;     /* source event id (DELIVERED / CODEL; 0 otherwise) */
+  uint64_t handle;      /* sgn_submit handle (0 if submitted on another shard) */
+  uint32_t host;        /* HostId where it happened */
+  uint32_t src_host;    /* sender HostId */
+  uint32_t dst_host;    /* destination HostId (0xFFFFFFFF unknown / not resolved) */
+  uint32_t status;      /* SGN_DRAIN_* */
+  uint32_t payload_len;
+  uint32_t tag;         /* SGN_TAG_EXT | submission slot */
+} sgn_drain_rec;
+/* Device buffer for drain records between two sgn_drain calls (before sgn_sim_init;
+ * default 1<<20 for EXTERNAL traffic). Running out is SGN_EOVERFLOW at the round. */
+int sgn_drain_enable(sgn_ctx* ctx, uint64_t capacity);
+/* Moves the records of hosts [host_lo, host_hi) out, ordered by (host, time, src_host,
+ * src_eid, tag, status); records of other hosts stay for a later call. At most cap are
+ * returned (*n_out); the rest stay. Between rounds only. */
+int sgn_drain(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, sgn_drain_rec* out, uint64_t cap,
+              uint64_t* n_out);
+
+/* The next window, decided by a caller that also runs hosts of its own (Controller with CPU
+ * hosts, controller.rs:88-112): [start, end) with previous window end <= start <= the
+ * device's minimum next event time (sgn_window's start), start < end, end - start <= the
+ * runahead the calendar was sized for, end clamped to the stop time. */
+int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end);
+
+/* The host RNG, held on the device (the one authoritative copy): CPU-side draws
+ * of host_rngDouble / host_rngNextNBytes (host/host.rs:1324-1336) and raw next_u64. They
+ * advance the same Xoshiro256++ stream the loss draws use. Between rounds only. */
+int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out);
+/* rand 0.9 StandardUniform f64: (next_u64 >> 11) * 2^-53 */
+int sgn_rng_double(sgn_ctx* ctx, uint32_t host, double* out);
+/* rand_core 0.9 fill_bytes_via_next: little-endian next_u64 per 8 bytes; a tail of 5..7
+ * bytes takes the low bytes of one more next_u64, a tail of 1..4 those of next_u32 (the
+ * upper half of next_u64, rand_xoshiro 0.7). */
+int sgn_rng_fill_bytes(sgn_ctx* ctx, uint32_t host, uint8_t* buf, size_t len);
 
 /* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS). */
 typedef struct sgn_kernel_times {

@@ -84,6 +84,7 @@ SGN_HD uint64_t sgn_tgen_think(uint64_t flow_seed, uint32_t host, uint64_t k, ui
 #define SGN_TAG_DATA 0u        /* PERIODIC datagram */
 #define SGN_TAG_REQ 0x10000u   /* TGEN request | size class */
 #define SGN_TAG_RESP 0x20000u  /* TGEN response datagram */
+#define SGN_TAG_EXT 0x80000000u /* EXTERNAL datagram: low 31 bits = sgn_submit slot */
 
 /* Order-sensitive per-host digest step: each word is xored in and followed by a
  * bijective multiply / xorshift, so any change of value or order changes the result

@@ -13,6 +13,7 @@
 #include "oracle.h"
 
 #include <algorithm>
+#include <tuple>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -846,7 +847,7 @@ struct CoDel {
 // Events (core/work/event.rs:84-183) and the per-host EventQueue (event_queue.rs:11-90)
 // ------------------------------------------------------------------------------------
 enum { EV_PACKET = 0, EV_LOCAL = 1 };
-enum { TASK_RELAY_OUT = 0, TASK_RELAY_IN = 1, TASK_APP = 2 };
+enum { TASK_RELAY_OUT = 0, TASK_RELAY_IN = 1, TASK_APP = 2, TASK_SUBMIT = 3 };
 
 struct Event {
   uint64_t time;
@@ -912,6 +913,7 @@ struct Wk {
   sgn_stats st{};
   std::vector<sgn_trace_rec> tr;
   std::vector<uint64_t> exports;
+  std::vector<sgn_drain_rec> dr;  // EXTERNAL: datagram fates for the CPU-side apps
   bool min_set = false;
   uint64_t min_used = 0;
 };
@@ -949,6 +951,26 @@ struct ora_sim {
   std::vector<uint64_t> exports;
   bool local_min_used_set = false;
   uint64_t local_min_used = 0;
+  // EXTERNAL traffic (CPU-resident applications): sgn_submit / sgn_drain / sgn_set_window
+  uint64_t prev_we = SIM_START;           // end of the last executed window
+  std::vector<uint64_t> handles;          // by submission slot
+  std::vector<uint32_t> submit_seq;       // per host
+  std::vector<sgn_drain_rec> drain_held;
+  bool external() const { return traffic.kind == SGN_TRAFFIC_EXTERNAL; }
+  void drain_rec(const Host& h, uint32_t status, uint32_t src, uint32_t dst, uint64_t seid,
+                 uint32_t payload, uint32_t tag) {
+    sgn_drain_rec r;
+    r.time = W().now;
+    r.src_eid = seid;
+    r.handle = 0;
+    r.host = h.id;
+    r.src_host = src;
+    r.dst_host = dst;
+    r.status = status;
+    r.payload_len = payload;
+    r.tag = tag;
+    W().dr.push_back(r);
+  }
 
   // ---------------------------------------------------------------------------------
   void trace_rec(Host& h, uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
@@ -1011,6 +1033,7 @@ struct ora_sim {
   void deliver_to_app(Host& h, const Pkt& p, bool local) {
     if (local) {
       W().st.local_delivered++;
+      if (external()) drain_rec(h, SGN_DRAIN_LOCAL, h.id, h.id, 0, p.payload, p.tag);
       sgn_drun_flush_seq(&h.d_app, &h.r_app);  // a local delivery is a run of its own
       h.d_app = sgn_digest3(h.d_app, W().now, (uint64_t)p.src_host | (1ULL << 62) | (1ULL << 32),
                             p.payload);
@@ -1021,6 +1044,7 @@ struct ora_sim {
     h.n_delivered++;
     sgn_drun_add_seq(&h.d_app, &h.r_app, W().now, p.src_host, p.src_eid, 1);
     trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, W().now, 0, p.src_eid);
+    if (external()) drain_rec(h, SGN_DRAIN_DELIVERED, p.src_host, h.id, p.src_eid, p.payload, p.tag);
     if (traffic.kind == SGN_TRAFFIC_TGEN && h.is_server && (p.tag & SGN_TAG_REQ)) {
       uint64_t size = traffic.file_bytes[p.tag & 3u];
       uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
@@ -1044,6 +1068,7 @@ struct ora_sim {
       W().st.packets_unknown_dst++;
       sgn_drun_add_same(&h.d_tx, &h.r_tx, W().now, 0xFFFFFFFFULL | (2ULL << 32), 0, 1);
       trace_rec(h, SGN_TRACE_SEND, 0xFFFFFFFFu, 2, W().now, 0, 0);
+      if (external()) drain_rec(h, SGN_DRAIN_UNKNOWN, h.id, 0xFFFFFFFFu, 0, p.payload, p.tag);
       return;
     }
     uint32_t dst = it->second;
@@ -1056,6 +1081,7 @@ struct ora_sim {
       W().st.packets_loss_dropped++;
       sgn_drun_add_same(&h.d_tx, &h.r_tx, W().now, (uint64_t)dst | (1ULL << 32), 0, 1);
       trace_rec(h, SGN_TRACE_SEND, dst, 1, W().now, 0, 0);
+      if (external()) drain_rec(h, SGN_DRAIN_LOSS, h.id, dst, 0, p.payload, p.tag);
       return;
     }
     uint64_t delay = lat[ri];  // :376
@@ -1119,6 +1145,7 @@ struct ora_sim {
       h.n_codel_dropped++;
       sgn_drun_add_seq(&h.d_app, &h.r_app, W().now, (uint64_t)d.src_host | (1ULL << 63), d.src_eid, 1);
       trace_rec(h, SGN_TRACE_CODEL_DROP, d.src_host, 0, W().now, 0, d.src_eid);
+      if (external()) drain_rec(h, SGN_DRAIN_CODEL, d.src_host, h.id, d.src_eid, d.payload, d.tag);
     }
     h.codel.dropped.clear();
     return got;
@@ -1202,6 +1229,19 @@ struct ora_sim {
     schedule_task(h, TASK_APP, W().now + next_delay);
   }
 
+  // EXTERNAL traffic: a CPU application's datagram (sgn_submit) at its send time enters the
+  // socket send queue and notifies relay_inet_out (Host::notify_socket_has_packets,
+  // host.rs:969-983), as app_task does for the synthetic apps.
+  void app_submit(Host& h, const Pkt& p) {
+    if (h.fifo.size() < cfg.out_fifo_cap) {
+      h.fifo.push_back({p.dst_ip, p.payload, p.payload, 1, p.tag});
+      relay_notify(h, TASK_RELAY_OUT);
+    } else {
+      W().st.app_blocked++;
+      drain_rec(h, SGN_DRAIN_BLOCKED, h.id, 0xFFFFFFFFu, 0, p.payload, p.tag);
+    }
+  }
+
   // Host::execute (host.rs:762-830)
   void execute(Host& h, uint64_t until) {
     // (pop under the host's own queue lock in threaded mode: other hosts push into it)
@@ -1221,7 +1261,9 @@ struct ora_sim {
       if (ev.time < h.last_popped) std::abort();  // event_queue.rs:75
       h.last_popped = ev.time;
       W().now = ev.time;  // Worker::set_current_time
-      if (ev.kind == EV_PACKET) {
+      if (ev.kind == EV_PACKET && ev.task == TASK_SUBMIT) {
+        app_submit(h, ev.pkt);
+      } else if (ev.kind == EV_PACKET) {
         W().st.packet_events_popped++;
         h.n_popped++;
         sgn_drun_add_seq(&h.d_rx, &h.r_rx, ev.time, ev.src_host, ev.eid, 1);
@@ -1262,6 +1304,7 @@ struct ora_sim {
       new_end = x;
     new_end = std::min(new_end, end_time);
     active = new_start < new_end;
+    prev_we = we;
     ws = new_start;
     we = new_end;
     st.rounds++;
@@ -1315,6 +1358,10 @@ struct ora_sim {
       if (!w.exports.empty()) {
         exports.insert(exports.end(), w.exports.begin(), w.exports.end());
         w.exports.clear();
+      }
+      if (!w.dr.empty()) {
+        drain_held.insert(drain_held.end(), w.dr.begin(), w.dr.end());
+        w.dr.clear();
       }
       if (w.min_set) {
         if (!local_min_used_set || w.min_used < local_min_used) {
@@ -1522,6 +1569,7 @@ int ora_sim_create(const uint32_t* used, uint32_t U, const uint64_t* lat, const 
     s->dns[h.ip] = i;
   }
   for (uint32_t sv : s->servers) s->hosts[sv].is_server = true;
+  s->submit_seq.assign(H->n_hosts, 0u);
   s->lo = 0;
   s->hi = H->n_hosts;
   // the initial window (manager.rs:506-509)
@@ -1543,6 +1591,102 @@ int ora_sim_create(const uint32_t* used, uint32_t U, const uint64_t* lat, const 
 }
 
 void ora_sim_free(ora_sim* s) { delete s; }
+
+// ---- CPU-resident applications (SGN_TRAFFIC_EXTERNAL): the same contract as libsgn's
+//      sgn_submit / sgn_drain / sgn_set_window (include/sgn.h) ----
+int ora_sim_submit(ora_sim* s, const sgn_pkt_soa* b) {
+  if (!s->external()) return SGN_ESTATE;
+  std::vector<Event> evs;
+  std::vector<uint32_t> seq = s->submit_seq;
+  for (uint64_t i = 0; i < b->n; i++) {
+    const uint32_t src = b->src_host[i];
+    const uint64_t t = b->send_time[i];
+    const uint32_t pay = b->payload_len[i];
+    if (src < s->lo || src >= s->hi || t < s->ws || t >= s->end_time || pay > 0xFFFFu) return SGN_EINVAL;
+    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != pay + SGN_UDP_HEADER_BYTES) return SGN_EINVAL;
+    Event ev;
+    ev.time = t;
+    ev.kind = EV_PACKET;  // ordered with the host's packet events: (time, src = itself, order)
+    ev.src_host = src;
+    ev.eid = ((uint64_t)seq[src]++ << 32) | b->dst_ip[i];
+    ev.task = TASK_SUBMIT;
+    ev.pkt.src_host = src;
+    ev.pkt.dst_ip = b->dst_ip[i];
+    ev.pkt.payload = pay;
+    ev.pkt.tag = SGN_TAG_EXT | (uint32_t)(s->handles.size() + i);
+    ev.pkt.src_eid = 0;
+    evs.push_back(ev);
+  }
+  for (const Event& ev : evs) s->hosts[ev.src_host].q.push(ev);
+  for (uint64_t i = 0; i < b->n; i++) s->handles.push_back(b->handle ? b->handle[i] : 0);
+  s->submit_seq.swap(seq);
+  return 0;
+}
+
+int ora_sim_drain(ora_sim* s, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap, uint64_t* n_out) {
+  if (!s->external()) return SGN_ESTATE;
+  for (sgn_drain_rec& r : s->drain_held) {
+    const uint32_t slot = r.tag & ~SGN_TAG_EXT;
+    r.handle = ((r.tag & SGN_TAG_EXT) && slot < s->handles.size()) ? s->handles[slot] : 0;
+  }
+  std::vector<sgn_drain_rec> sel, keep;
+  for (const sgn_drain_rec& r : s->drain_held) (r.host >= lo && r.host < hi ? sel : keep).push_back(r);
+  auto key = [](const sgn_drain_rec& r) {
+    return std::make_tuple(r.host, r.time, r.src_host, r.src_eid, r.tag, r.status);
+  };
+  std::sort(sel.begin(), sel.end(), [&](const sgn_drain_rec& a, const sgn_drain_rec& c) { return key(a) < key(c); });
+  const uint64_t k = std::min<uint64_t>(cap, sel.size());
+  if (k) std::memcpy(out, sel.data(), k * sizeof(sgn_drain_rec));
+  keep.insert(keep.end(), sel.begin() + k, sel.end());
+  s->drain_held.swap(keep);
+  if (n_out) *n_out = k;
+  return 0;
+}
+
+int ora_sim_set_window(ora_sim* s, uint64_t start, uint64_t end) {
+  // Controller with CPU-side hosts (controller.rs:88-112): the caller's window must not skip
+  // an event (start <= the next event time) nor go back (start >= the last window's end)
+  if (start < s->prev_we || start > s->ws || end <= start) return SGN_EINVAL;
+  end = std::min(end, s->end_time);
+  if (end <= start) return SGN_EINVAL;
+  s->ws = start;
+  s->we = end;
+  s->active = true;
+  return 0;
+}
+
+// The host RNG (host/host.rs:1324-1336: host_rngDouble, host_rngNextNBytes)
+int ora_sim_rng_next_u64(ora_sim* s, uint32_t host, uint64_t* out) {
+  if (host >= s->hosts.size()) return SGN_EINVAL;
+  *out = s->hosts[host].rng.next_u64();
+  return 0;
+}
+int ora_sim_rng_double(ora_sim* s, uint32_t host, double* out) {
+  if (host >= s->hosts.size()) return SGN_EINVAL;
+  *out = s->hosts[host].rng.next_f64();  // rand 0.9 StandardUniform f64
+  return 0;
+}
+int ora_sim_rng_fill_bytes(ora_sim* s, uint32_t host, uint8_t* buf, size_t len) {
+  // rand_core 0.9.3 impls::fill_bytes_via_next (RngCore::fill_bytes of rand_xoshiro 0.7's
+  // Xoshiro256PlusPlus; its next_u32 is the upper half of next_u64)
+  if (host >= s->hosts.size()) return SGN_EINVAL;
+  Xoshiro& x = s->hosts[host].rng;
+  size_t i = 0;
+  while (len - i >= 8) {
+    const uint64_t v = x.next_u64();
+    for (int k = 0; k < 8; k++) buf[i + k] = (uint8_t)(v >> (8 * k));
+    i += 8;
+  }
+  const size_t n = len - i;
+  if (n > 4) {
+    const uint64_t v = x.next_u64();
+    for (size_t k = 0; k < n; k++) buf[i + k] = (uint8_t)(v >> (8 * k));
+  } else if (n > 0) {
+    const uint32_t v = (uint32_t)(x.next_u64() >> 32);
+    for (size_t k = 0; k < n; k++) buf[i + k] = (uint8_t)(v >> (8 * k));
+  }
+  return 0;
+}
 
 // Worker threads for the round loop (1 = sequential). Results do not depend on it.
 int ora_sim_set_threads(ora_sim* s, int n) {

@@ -97,6 +97,16 @@ int ora_sim_host_digests(const ora_sim* s, uint32_t lo, uint32_t hi, sgn_host_di
 uint64_t ora_sim_trace_count(const ora_sim* s);
 uint64_t ora_sim_trace_read(const ora_sim* s, sgn_trace_rec* out, uint64_t cap);
 int ora_sim_host_next_event_time(const ora_sim* s, uint32_t host, uint64_t* t);
+/* CPU-resident applications (SGN_TRAFFIC_EXTERNAL): same contract as libsgn's sgn_submit,
+ * sgn_drain (handles resolved from this oracle's own submissions) and sgn_set_window. */
+int ora_sim_submit(ora_sim* s, const sgn_pkt_soa* batch);
+int ora_sim_drain(ora_sim* s, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap,
+                  uint64_t* n_out);
+int ora_sim_set_window(ora_sim* s, uint64_t start, uint64_t end);
+/* The host RNG (host/host.rs:1324-1336); same contract as sgn_rng_*. */
+int ora_sim_rng_next_u64(ora_sim* s, uint32_t host, uint64_t* out);
+int ora_sim_rng_double(ora_sim* s, uint32_t host, double* out);
+int ora_sim_rng_fill_bytes(ora_sim* s, uint32_t host, uint8_t* buf, size_t len);
 /* Sharded mode (round-edge protocol rehearsal, tests only): restrict execution to
  * [lo,hi); packet events for other hosts are exported instead of queued. */
 int ora_sim_set_shard(ora_sim* s, uint32_t lo, uint32_t hi);

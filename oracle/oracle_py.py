@@ -81,6 +81,12 @@ def load():
         "ora_sim_shard_import": (C.c_int, [vp, u64p, C.c_uint64]),
         "ora_sim_shard_local_min": (C.c_int, [vp, u64p, u64p]),
         "ora_sim_shard_advance": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
+        "ora_sim_submit": (C.c_int, [vp, C.POINTER(sgn.PktSoa)]),
+        "ora_sim_drain": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(sgn.DrainRec), C.c_uint64, u64p]),
+        "ora_sim_set_window": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
+        "ora_sim_rng_next_u64": (C.c_int, [vp, C.c_uint32, u64p]),
+        "ora_sim_rng_double": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_double)]),
+        "ora_sim_rng_fill_bytes": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -242,3 +248,37 @@ class Sim:
 
     def shard_advance(self, gmin, gmin_used):
         self.L.ora_sim_shard_advance(self.h, gmin, gmin_used)
+
+    # CPU-resident applications (TRAFFIC_EXTERNAL) and the host RNG: libsgn's contract
+    def _ok(self, rc, what):
+        if rc != 0:
+            raise sgn.SgnError(rc, "oracle " + what)
+
+    def submit(self, src_host, dst_ip, payload_len, send_time, handle=None, wire_len=None):
+        b, keep = sgn.pkt_soa(src_host, dst_ip, payload_len, send_time, handle, wire_len)
+        self._ok(self.L.ora_sim_submit(self.h, C.byref(b)), "submit")
+
+    def drain(self, lo=0, hi=0xFFFFFFFF, cap=1 << 22):
+        out = np.zeros(cap, dtype=sgn.DRAIN_DTYPE)
+        n = C.c_uint64()
+        self._ok(self.L.ora_sim_drain(self.h, lo, hi, out.ctypes.data_as(C.POINTER(sgn.DrainRec)), cap,
+                                      C.byref(n)), "drain")
+        return out[: n.value]
+
+    def set_window(self, start, end):
+        self._ok(self.L.ora_sim_set_window(self.h, start, end), "set_window")
+
+    def rng_next_u64(self, host):
+        v = C.c_uint64()
+        self._ok(self.L.ora_sim_rng_next_u64(self.h, host, C.byref(v)), "rng")
+        return v.value
+
+    def rng_double(self, host):
+        v = C.c_double()
+        self._ok(self.L.ora_sim_rng_double(self.h, host, C.byref(v)), "rng")
+        return v.value
+
+    def rng_fill_bytes(self, host, n):
+        buf = (C.c_uint8 * max(1, n))()
+        self._ok(self.L.ora_sim_rng_fill_bytes(self.h, host, buf, n), "rng")
+        return bytes(buf[:n])

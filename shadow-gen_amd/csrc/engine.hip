@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
+#include <tuple>
 
 #include "sgn_internal.h"
 #include "sgn_workload.h"
@@ -39,7 +41,7 @@
 #define DGT_BEGIN(v) ((void)0)
 #define DGT_END(i, v) ((void)0)
 #endif
-enum { DG_RO = 0, DG_RI, DG_APP, DG_BATCH, DG_HDLOAD, DG_FQLOAD, DG_TBREF, DG_POPRUN, DG_N };
+enum { DG_RO = 0, DG_RI, DG_APP, DG_BATCH, DG_HDLOAD, DG_FQLOAD, DG_RMISS, DG_POPRUN, DG_N };
 // diagnostic timers: cycles while this lane was inside ...
 enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD, DGT_N };
 
@@ -101,6 +103,13 @@ __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
   st_dev(q + 1, r.eid);
   st_dev(q + 2, (uint64_t)r.src | ((uint64_t)r.dst << 32));
   st_dev(q + 3, (uint64_t)r.pc | ((uint64_t)r.tag << 32));
+}
+
+// device-scope atomic min whose result is not used: the wave does not wait for it here (a
+// returning one costs a round trip per call); the arrival's s_waitcnt vmcnt(0) completes it
+// before the round edge reads the minima
+__device__ __forceinline__ void min_nr(SGN_GLB uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // a / b for a divisor below 2^32: u32 division when the dividend fits too
@@ -210,9 +219,6 @@ struct HostExec {
   // CoDel run cache: the head run being consumed and the tail run being extended live in
   // registers; their ring slots are stale until store() (or until the tail is closed).
   bool hd_valid, tl_open;
-  // XOR of the returned values of the calendar's atomicMins: returning atomics are
-  // performed at the coherence point before the wave's arrival count (fused round edge)
-  uint64_t sink;
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
@@ -291,7 +297,6 @@ struct HostExec {
       L->fh = *fq_slot(0);
       L->fh_idx = fq_head;
     }
-    sink = 0;
     L->run[0].n = L->run[1].n = L->run[2].n = 0;
 #ifdef SGN_DIAG
     for (int i = 0; i < DG_N; i++) dg[i] = 0;
@@ -348,7 +353,6 @@ struct HostExec {
     S.nextloc[h] = next_local_time();
     if (hd_valid) *cq_slot(0) = L->hd;
     if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
-    if (sink == 0x9e3779b97f4a7c15ULL) C->overflow_info = 0;  // keeps the atomics returning
   }
 
   // rare counters go straight to memory (registers are kept for the per-packet ones)
@@ -402,6 +406,28 @@ struct HostExec {
     if ((atomicOr(&C->overflow, bit) & bit) == 0) C->overflow_info = gid;
   }
 
+  // EXTERNAL traffic: a datagram's fate for the CPU-side applications (sgn_drain)
+  __device__ void drain_rec(uint32_t status, uint32_t src, uint32_t dst, uint64_t seid,
+                            uint32_t payload, uint32_t tag) {
+    const uint64_t pos = atomicAdd((unsigned long long*)&C->drain_n, 1ULL);
+    if (pos >= S.drain_cap) {
+      overflow(OVF_DRAIN);
+      return;
+    }
+    sgn_drain_rec r;
+    r.time = now;
+    r.src_eid = seid;
+    r.handle = 0;
+    r.host = gid;
+    r.src_host = src;
+    r.dst_host = dst;
+    r.status = status;
+    r.payload_len = payload;
+    r.tag = tag;
+    S.drain[pos] = r;
+  }
+  __device__ __forceinline__ bool external() const { return S.tkind == SGN_TRAFFIC_EXTERNAL; }
+
   // ---- local event slots: Host::schedule_task_* / push_local_event (host.rs:703-722);
   //      Event::new_local consumes an event id even if the event is then dropped ----
   template <int SL>
@@ -446,7 +472,6 @@ struct HostExec {
     // when a refill is due or a removal fails, not on the per-packet fast path).
     uint64_t span = now - last;
     if (span >= interval) {
-      DG(DG_TBREF);
       const uint64_t inc = L->tbc[W];
       uint64_t nref = span / interval;
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
@@ -576,6 +601,7 @@ struct HostExec {
   }
   __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
     R->n_codel++;
+    if (external()) drain_rec(SGN_DRAIN_CODEL, p.src, gid, p.eid, p.payload, p.tag);
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
@@ -683,6 +709,8 @@ struct HostExec {
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, src, e0, m);
     if (S.trace_on)
       for (uint32_t k = 0; k < m; k++) trace(SGN_TRACE_DELIVER, src, 0, now, 0, e0 + k);
+    if (external())
+      for (uint32_t k = 0; k < m; k++) drain_rec(SGN_DRAIN_DELIVERED, src, gid, e0 + k, payload, tag);
     if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
       const uint64_t size = S.file_bytes[tag & 3u];
       const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
@@ -698,6 +726,7 @@ struct HostExec {
   }
   __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
     R->n_local_deliv++;
+    if (external()) drain_rec(SGN_DRAIN_LOCAL, gid, gid, 0, p.payload, p.tag);
     sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
     L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
   }
@@ -719,12 +748,17 @@ struct HostExec {
       } else {
         if (cq_len > 0) {
           load_head();
-          if (sat_sub(now, L->hd.enqueue_ts) < CODEL_TARGET) {
-            // Fast path over the head run: every packet of it has the same standing delay
-            // (< TARGET: CoDelQueue::pop returns it, clearing interval_end and drop mode,
-            // codel_queue.rs:204-262) and wire size, and all removals happen at the same
-            // `now`, so after the first comforming_remove (which applies the lazy refill)
-            // balance / wire more packets conform; the first that does not is cached.
+          // Fast path over the head run: every packet of it has the same standing delay and
+          // wire size, and all removals happen at the same `now`. CoDelQueue::pop returns
+          // each of them (codel_queue.rs:125-262) unless the delay is standing (>= TARGET)
+          // past an interval end that is already due: below TARGET it clears interval_end
+          // and drop mode; at or above it clears drop mode and only moves interval_end (set
+          // to now + INTERVAL by the first pop that leaves more than an MTU queued, cleared
+          // by the first that leaves less; the queued bytes only fall here, so the last pop
+          // decides). After the first comforming_remove (which applies the lazy refill)
+          // balance / wire more packets conform; the first that does not is cached.
+          const bool standing = sat_sub(now, L->hd.enqueue_ts) >= CODEL_TARGET;
+          if (!standing || !((fl & F_CODEL_IE) && now >= L->cq[0])) {
             const uint32_t n = L->hd.count;
             const uint64_t wire = (uint64_t)L->hd.payload + SGN_UDP_HEADER_BYTES;
             uint32_t m = n;
@@ -745,13 +779,19 @@ struct HostExec {
                 }
               }
             }
-            fl &= ~(F_CODEL_IE | F_CODEL_DROP);
             const uint32_t used = m + (blocked ? 1u : 0u);
             const CodelEnt r = L->hd;
             L->hd.eid += used;
             L->hd.count -= used;
             cq_len -= used;
             cq_bytes = sat_sub(cq_bytes, (uint64_t)used * wire);
+            fl &= ~F_CODEL_DROP;
+            if (!standing || cq_bytes <= SGN_CONFIG_MTU) {
+              fl &= ~F_CODEL_IE;
+            } else if (!(fl & F_CODEL_IE)) {
+              fl |= F_CODEL_IE;
+              L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
+            }
             if (L->hd.count == 0) {
               hd_valid = false;
               cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
@@ -811,6 +851,8 @@ struct HostExec {
       sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (S.trace_on)
         for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+      if (external())
+        for (uint32_t j = 0; j < n; j++) drain_rec(SGN_DRAIN_UNKNOWN, gid, NO_HOST, 0, payload, tag);
       return;
     }
     // the route (WorkerShared::latency / reliability, worker.rs:523-537): a train goes to
@@ -820,6 +862,7 @@ struct HostExec {
       delay = L->rc_lat;
       T = L->rc_T;
     } else {
+      DG(DG_RMISS);
       const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
       const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
       delay = S.rlat[ri];
@@ -844,6 +887,7 @@ struct HostExec {
         run = 0;
         sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
         if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+        if (external()) drain_rec(SGN_DRAIN_LOSS, gid, dst, 0, payload, tag);
       } else {
         const uint64_t e = eid++;
         run++;
@@ -858,7 +902,7 @@ struct HostExec {
     // RUN_MAX packets
     const uint32_t nrec = (nsent + RUN_MAX - 1) / RUN_MAX;
     if (S.dynamic) {  // Worker::update_lowest_used_latency (no return value: fire and forget)
-      sink ^= atomicMin((unsigned long long*)&C->min_used, (unsigned long long)delay);
+      min_nr(&C->min_used, delay);
     }
     SGN_GLB EvRec* dstp;
     uint32_t cap;
@@ -869,8 +913,7 @@ struct HostExec {
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
       pos = atomicAdd(&S.slab_n[idx], nrec);
-      sink ^= atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
-                        (unsigned long long)deliver);
+      min_nr(b == b1 ? &C->keep_min : &S.bucket_min[b], deliver);
       dstp = S.pool + idx * S.CAP;
       cap = S.CAP;
     } else {
@@ -931,6 +974,7 @@ struct HostExec {
         send_batch(ro_dst, ro_pay, ro_tag, 1);
     }
     while (fq_len > 0) {
+      DGT_BEGIN(tq0);
       const FifoEnt e = fifo_head();
       const uint32_t run = e.count == 1 ? 1u : e.count - 1;
       const uint32_t payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
@@ -954,6 +998,7 @@ struct HostExec {
           }
         }
       }
+      DGT_END(DGT_LOAD, tq0);
       if (is_local) {
         Pkt p;
         p.src = gid;
@@ -965,6 +1010,7 @@ struct HostExec {
       } else {
         send_batch(e.dst, payload, e.tag, n_ok);
       }
+      DGT_BEGIN(tq1);
       const uint32_t consumed = n_ok + (blocked ? 1u : 0u);
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
@@ -973,6 +1019,7 @@ struct HostExec {
         fq_slot(0)->count = e.count - consumed;
         L->fh.count = e.count - consumed;
       }
+      DGT_END(DGT_APP, tq1);
       if (blocked) {
         fl |= F_RO_NEXT;
         ro_dst = e.dst;
@@ -1022,6 +1069,22 @@ struct HostExec {
     else
       R->n_blocked++;
     schedule<SLOT_APP>(now + next_delay);
+  }
+
+  // EXTERNAL traffic: the application's socket write (sgn_submit) enters the socket send
+  // queue and notifies relay_inet_out (Host::notify_socket_has_packets, host.rs:969-983),
+  // as app_task does for the synthetic apps. The record carries the destination address in
+  // the low half of its event id (the high half is the submission order).
+  __device__ void app_submit(const EvRec& e) {
+    uint32_t dst;
+    if (!dns_lookup((uint32_t)e.eid, &dst)) dst = NO_HOST;
+    const uint32_t payload = ev_payload(e);
+    if (fifo_push(dst, payload, payload, 1, e.tag)) {
+      relay_notify<0>();
+    } else {
+      R->n_blocked++;
+      drain_rec(SGN_DRAIN_BLOCKED, gid, NO_HOST, 0, payload, e.tag);
+    }
   }
 
   // ---- Host::execute (host.rs:762-830) over the host's due event runs + local slots ----
@@ -1074,9 +1137,13 @@ struct HostExec {
         const EvRec& e = ev[ord[pi]];
         if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           pi++;
+          now = e.time;
+          if (external() && e.src == gid) {  // a CPU application's datagram (sgn_submit)
+            app_submit(e);
+            continue;
+          }
           DG(DG_POPRUN);
           DGT_BEGIN(t0);
-          now = e.time;
           // the run's packets pop back to back (nothing sorts between them); each is
           // routed into CoDel and notifies relay_inet_in, which schedules its task on
           // the first notification only (Relay::notify, relay/mod.rs:111-136)
@@ -1181,6 +1248,7 @@ __device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
       if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
       ne = ne < S.end_time ? ne : S.end_time;
       C->active = min_next < ne ? 1u : 0u;
+      C->prev_we = C->we;
       C->ws = min_next;
       C->we = ne;
       C->round_min = INVALID;
@@ -1246,6 +1314,7 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
     ne = ne < S.end_time ? ne : S.end_time;
     st_dev(&C->active, min_next < ne ? 1u : 0u);
+    st_dev(&C->prev_we, we);
     st_dev(&C->ws, min_next);
     st_dev(&C->we, ne);
     st_dev(&C->round_min, (uint64_t)INVALID);
@@ -1684,6 +1753,7 @@ __global__ void k_advance(DevSim S, const uint64_t* red) {
   if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
   ne = ne < S.end_time ? ne : S.end_time;
   C->active = min_next < ne ? 1u : 0u;
+  C->prev_we = C->we;
   C->ws = min_next;
   C->we = ne;
   C->round_min = INVALID;
@@ -1722,6 +1792,46 @@ __global__ void k_codel_law_test(uint64_t n, uint64_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = codel_law(SIM_START, i) - SIM_START;
+}
+
+// sgn_submit: each datagram becomes an event record of its source host in the calendar
+// bucket of its send time (validated on the host: owned source, time within the horizon).
+__global__ void k_inject(const DevSim* Sp, const EvRec* recs, uint32_t n) {
+  const DevSim& S = *Sp;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const EvRec r = recs[i];
+  const uint32_t g = (r.dst - S.lo) >> S.gsh;
+  const uint32_t b = bucket_of(S, r.time);
+  const size_t idx = (size_t)S.bucket_slab[b] * S.G + g;
+  const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+  if (pos >= S.CAP) {
+    if ((atomicOr(&S.ctrl->overflow, OVF_BUCKET) & OVF_BUCKET) == 0) S.ctrl->overflow_info = r.dst;
+    return;
+  }
+  S.pool[idx * S.CAP + pos] = r;
+  atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)r.time);
+}
+
+// sgn_rng_*: n draws of one host's Xoshiro256++ stream (the state stays on the device)
+__global__ void k_rng(const DevSim* Sp, uint32_t h, uint32_t n, uint64_t* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  SGN_GLB HostRec* R = Sp->hrec + h;
+  uint64_t s0 = R->rng[0], s1 = R->rng[1], s2 = R->rng[2], s3 = R->rng[3];
+  for (uint32_t i = 0; i < n; i++) {
+    out[i] = rotl64(s0 + s3, 23) + s0;
+    const uint64_t t = s1 << 17;
+    s2 ^= s0;
+    s3 ^= s1;
+    s1 ^= s2;
+    s0 ^= s3;
+    s2 ^= t;
+    s3 = rotl64(s3, 45);
+  }
+  R->rng[0] = s0;
+  R->rng[1] = s1;
+  R->rng[2] = s2;
+  R->rng[3] = s3;
 }
 
 }  // namespace sgn
@@ -1787,6 +1897,7 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow & OVF_SEG) what += " due-event segment buffer";
   if (c.overflow & OVF_EXCHANGE) what += " exchange slot (raise exchange_slot_events)";
   if (c.overflow & OVF_TRACE) what += " trace buffer";
+  if (c.overflow & OVF_DRAIN) what += " drain buffer (raise sgn_drain_enable's capacity or drain more often)";
   return set_error(ctx, SGN_EOVERFLOW,
                    "device capacity exceeded:" + what + " (info " +
                        std::to_string(c.overflow_info) + "); results are invalid");
@@ -1910,6 +2021,9 @@ void free_sim(sgn_ctx* ctx) {
   ctx->graph_pending = false;
   for (void* p : ctx->allocs) hipFree(p);
   ctx->allocs.clear();
+  if (ctx->d_stage) hipFree(ctx->d_stage);
+  ctx->d_stage = nullptr;
+  ctx->stage_cap = 0;
   if (ctx->h_ctrl) {
     hipHostFree(ctx->h_ctrl);
     ctx->h_ctrl = nullptr;
@@ -1932,7 +2046,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!ctx || !cfg || !tr) return SGN_EINVAL;
   if (!ctx->routes_ready) return set_error(ctx, SGN_ESTATE, "sgn_routes_build must precede sgn_sim_init");
   if (!ctx->hosts_ready) return set_error(ctx, SGN_ESTATE, "sgn_hosts_set must precede sgn_sim_init");
-  if (tr->kind != SGN_TRAFFIC_PERIODIC && tr->kind != SGN_TRAFFIC_TGEN)
+  if (tr->kind != SGN_TRAFFIC_PERIODIC && tr->kind != SGN_TRAFFIC_TGEN &&
+      tr->kind != SGN_TRAFFIC_EXTERNAL)
     return set_error(ctx, SGN_EINVAL, "unknown traffic kind");
   if (cfg->out_fifo_cap == 0 || cfg->codel_cap == 0)
     return set_error(ctx, SGN_EINVAL, "out_fifo_cap and codel_cap must be >= 1");
@@ -2108,6 +2223,15 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     if (!S.trace) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
     S.trace_cap = ctx->trace_cap;
   }
+  ctx->handles.clear();
+  ctx->drain_held.clear();
+  ctx->submit_seq.assign(nH, 0u);
+  if (tr->kind == SGN_TRAFFIC_EXTERNAL) {
+    const uint64_t dc = ctx->drain_cap ? ctx->drain_cap : (1ULL << 20);
+    S.drain = (decltype(S.drain))dalloc<sgn_drain_rec>(ctx, dc);
+    if (!S.drain) return set_error(ctx, SGN_ENOMEM, "device allocation failed (drain buffer)");
+    S.drain_cap = dc;
+  }
   // multi-GPU exchange slots
   S.n_ranks = ctx->nranks;
   S.rank = ctx->rank;
@@ -2140,6 +2264,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
   c.remote_min = INVALID;
+  c.prev_we = SIM_START;
   S.ctrl = (decltype(S.ctrl))dalloc<Ctrl>(ctx, 1);
   if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
@@ -2414,6 +2539,183 @@ int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (!ctx->S.stamps || !out) return 0;
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
   SGN_HIP(ctx, hipMemcpy(out, ctx->S.stamps, std::min(cap, waves) * SGN_STAMP_WORDS * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ---- CPU-resident applications (SGN_TRAFFIC_EXTERNAL) ----
+int sgn_drain_enable(sgn_ctx* ctx, uint64_t capacity) {
+  if (!ctx) return SGN_EINVAL;
+  if (ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "sgn_drain_enable must precede sgn_sim_init");
+  if (capacity == 0) return set_error(ctx, SGN_EINVAL, "drain capacity must be >= 1");
+  ctx->drain_cap = capacity;
+  return 0;
+}
+
+int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
+  if (!ctx || !b) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  const DevSim& S = ctx->S;
+  if (S.tkind != SGN_TRAFFIC_EXTERNAL)
+    return set_error(ctx, SGN_ESTATE, "sgn_submit needs SGN_TRAFFIC_EXTERNAL traffic");
+  if (b->n == 0) return 0;
+  if (!b->src_host || !b->dst_ip || !b->payload_len || !b->send_time)
+    return set_error(ctx, SGN_EINVAL, "sgn_submit: missing array");
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  const uint64_t ws = ctx->h_ctrl->ws;
+  // the calendar holds NB buckets of BW ns; the gather walks forward from the window
+  const uint64_t horizon = ws + (uint64_t)(S.NB - 2) * S.BW;
+  if (ctx->handles.size() + b->n > 0x7FFFFFFFULL)
+    return set_error(ctx, SGN_ERANGE, "more than 2^31 submissions on one shard");
+  std::vector<EvRec> recs(b->n);
+  std::vector<uint32_t> seq_add;
+  std::vector<uint32_t> seq = ctx->submit_seq;  // committed only on success
+  for (uint64_t i = 0; i < b->n; i++) {
+    const uint32_t src = b->src_host[i];
+    const uint64_t t = b->send_time[i];
+    const uint32_t pay = b->payload_len[i];
+    if (src < ctx->lo || src >= ctx->hi)
+      return set_error(ctx, SGN_EINVAL, "sgn_submit: source host " + std::to_string(src) + " not owned by this shard");
+    if (t < ws || t >= S.end_time)
+      return set_error(ctx, SGN_EINVAL, "sgn_submit: send_time outside [window start, stop time)");
+    if (t >= horizon)
+      return set_error(ctx, SGN_EINVAL, "sgn_submit: send_time beyond the event calendar's horizon; submit it closer to its window");
+    if (pay > 0xFFFFu) return set_error(ctx, SGN_EINVAL, "sgn_submit: payload_len > 65535");
+    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != pay + SGN_UDP_HEADER_BYTES)
+      return set_error(ctx, SGN_EINVAL, "sgn_submit: wire_len must be payload_len + 28 (UDP/IPv4)");
+    uint32_t& q = seq[src - ctx->lo];
+    if (q == 0xFFFFFFFFu) return set_error(ctx, SGN_ERANGE, "sgn_submit: 2^32 submissions from one host");
+    EvRec& r = recs[i];
+    r.time = t;
+    r.eid = ((uint64_t)q++ << 32) | b->dst_ip[i];  // submission order, then the address
+    r.src = src;
+    r.dst = src;
+    r.pc = pay | (1u << 16);
+    r.tag = SGN_TAG_EXT | (uint32_t)(ctx->handles.size() + i);
+  }
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->stage_cap < b->n) {
+    if (ctx->d_stage) hipFree(ctx->d_stage);
+    ctx->d_stage = nullptr;
+    ctx->stage_cap = 0;
+    SGN_HIP(ctx, hipMalloc(&ctx->d_stage, b->n * sizeof(EvRec)));
+    ctx->stage_cap = b->n;
+  }
+  SGN_HIP(ctx, hipMemcpyAsync(ctx->d_stage, recs.data(), b->n * sizeof(EvRec), hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_inject, dim3((uint32_t)((b->n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     (const DevSim*)ctx->d_S, (const EvRec*)ctx->d_stage, (uint32_t)b->n);
+  SGN_HIP(ctx, hipGetLastError());
+  if ((rc = sync_ctrl(ctx))) return rc;
+  for (uint64_t i = 0; i < b->n; i++) ctx->handles.push_back(b->handle ? b->handle[i] : 0);
+  ctx->submit_seq.swap(seq);
+  return 0;
+}
+
+int sgn_drain(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap, uint64_t* n_out) {
+  if (!ctx || (!out && cap)) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  if (ctx->S.tkind != SGN_TRAFFIC_EXTERNAL)
+    return set_error(ctx, SGN_ESTATE, "sgn_drain needs SGN_TRAFFIC_EXTERNAL traffic");
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  const uint64_t n = ctx->h_ctrl->drain_n;
+  if (n) {
+    const size_t old = ctx->drain_held.size();
+    ctx->drain_held.resize(old + n);
+    SGN_HIP(ctx, hipMemcpy(ctx->drain_held.data() + old, (const void*)ctx->S.drain, n * sizeof(sgn_drain_rec),
+                           hipMemcpyDeviceToHost));
+    const uint64_t zero = 0;
+    SGN_HIP(ctx, hipMemcpy((char*)ctx->S.ctrl + offsetof(Ctrl, drain_n), &zero, 8, hipMemcpyHostToDevice));
+    ctx->h_ctrl->drain_n = 0;
+    for (size_t i = old; i < ctx->drain_held.size(); i++) {
+      sgn_drain_rec& r = ctx->drain_held[i];
+      const uint32_t slot = r.tag & ~SGN_TAG_EXT;
+      // a slot is this shard's when the datagram's source is one of its hosts
+      r.handle = ((r.tag & SGN_TAG_EXT) && r.src_host >= ctx->lo && r.src_host < ctx->hi &&
+                  slot < ctx->handles.size()) ? ctx->handles[slot] : 0;
+    }
+  }
+  std::vector<sgn_drain_rec> sel, keep;
+  for (const sgn_drain_rec& r : ctx->drain_held) (r.host >= lo && r.host < hi ? sel : keep).push_back(r);
+  auto key = [](const sgn_drain_rec& r) {
+    return std::make_tuple(r.host, r.time, r.src_host, r.src_eid, r.tag, r.status);
+  };
+  std::sort(sel.begin(), sel.end(), [&](const sgn_drain_rec& a, const sgn_drain_rec& b) { return key(a) < key(b); });
+  const uint64_t k = std::min<uint64_t>(cap, sel.size());
+  if (k) std::memcpy(out, sel.data(), k * sizeof(sgn_drain_rec));
+  keep.insert(keep.end(), sel.begin() + k, sel.end());
+  ctx->drain_held.swap(keep);
+  if (n_out) *n_out = k;
+  return 0;
+}
+
+int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end) {
+  if (!ctx) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  int rc = sync_ctrl(ctx);
+  if (rc) return rc;
+  Ctrl& c = *ctx->h_ctrl;
+  if (start < c.prev_we) return set_error(ctx, SGN_EINVAL, "sgn_set_window: start before the previous window's end");
+  if (start > c.ws) return set_error(ctx, SGN_EINVAL, "sgn_set_window: start after the device's next event time");
+  if (end <= start) return set_error(ctx, SGN_EINVAL, "sgn_set_window: empty window");
+  if (end - start > ctx->S.BW)
+    return set_error(ctx, SGN_EINVAL, "sgn_set_window: window longer than the runahead the calendar was sized for");
+  end = std::min(end, ctx->S.end_time);
+  if (end <= start) return set_error(ctx, SGN_EINVAL, "sgn_set_window: window at or past the stop time");
+  c.ws = start;
+  c.we = end;
+  c.active = 1;
+  SGN_HIP(ctx, hipMemcpy((void*)ctx->S.ctrl, &c, offsetof(Ctrl, overflow), hipMemcpyHostToDevice));
+  return 0;
+}
+
+namespace {
+int rng_draw(sgn_ctx* ctx, uint32_t host, uint32_t n, uint64_t* out) {
+  if (!ctx || (!out && n)) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  constexpr uint32_t CH = 1u << 16;
+  uint64_t* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, (size_t)std::min(n, CH) * 8 + 8));
+  hipError_t e = hipSuccess;
+  for (uint32_t o = 0; o < n && e == hipSuccess; o += CH) {
+    const uint32_t k = std::min(CH, n - o);
+    hipLaunchKernelGGL(k_rng, dim3(1), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, host - ctx->lo, k, d);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out + o, d, (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  }
+  hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "host rng draw");
+  return 0;
+}
+}  // namespace
+
+int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out) { return rng_draw(ctx, host, 1, out); }
+
+int sgn_rng_double(sgn_ctx* ctx, uint32_t host, double* out) {
+  if (!out) return SGN_EINVAL;
+  uint64_t x = 0;
+  int rc = rng_draw(ctx, host, 1, &x);
+  if (rc == 0) *out = (double)(x >> 11) * 0x1.0p-53;
+  return rc;
+}
+
+int sgn_rng_fill_bytes(sgn_ctx* ctx, uint32_t host, uint8_t* buf, size_t len) {
+  if (!buf && len) return SGN_EINVAL;
+  if (len / 8 + 1 > 0xFFFFFFFFull) return set_error(ctx, SGN_ERANGE, "sgn_rng_fill_bytes: len too large");
+  const size_t full = len / 8, rem = len % 8;
+  std::vector<uint64_t> v(full + (rem ? 1 : 0));
+  int rc = rng_draw(ctx, host, (uint32_t)v.size(), v.data());
+  if (rc) return rc;
+  for (size_t i = 0; i < full; i++)
+    for (int k = 0; k < 8; k++) buf[8 * i + k] = (uint8_t)(v[i] >> (8 * k));
+  if (rem) {
+    // fill_bytes_via_next: 5..7 bytes from next_u64, 1..4 from next_u32 = next_u64 >> 32
+    const uint64_t w = rem > 4 ? v[full] : (v[full] >> 32);
+    for (size_t k = 0; k < rem; k++) buf[8 * full + k] = (uint8_t)(w >> (8 * k));
+  }
   return 0;
 }
 

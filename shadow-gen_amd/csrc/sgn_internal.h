@@ -95,6 +95,8 @@ struct Ctrl {
   uint64_t trace_n;       // trace records produced
   uint64_t remote_min;    // multi-GPU: min over events exported this round
   uint64_t epoch;         // persistent rounds: round edges published (grid barrier)
+  uint64_t prev_we;       // end of the last executed window (sgn_set_window's lower bound)
+  uint64_t drain_n;       // drain records produced since the last sgn_drain
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -108,6 +110,7 @@ enum : uint32_t {
   OVF_EXCHANGE = 16u,
   OVF_TRACE = 32u,
   OVF_TIMEOUT = 64u,  // a persistent grid barrier gave up (grid not resident)
+  OVF_DRAIN = 128u,   // drain buffer full (raise sgn_drain_enable's capacity)
 };
 
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
@@ -264,6 +267,9 @@ struct DevSim {
   // trace
   SGN_GLB sgn_trace_rec* trace;
   uint64_t trace_cap;
+  // EXTERNAL traffic: interface deliveries and drops for the CPU-side applications
+  SGN_GLB sgn_drain_rec* drain;
+  uint64_t drain_cap;
   // multi-GPU exchange: out slot r holds events for rank r
   SGN_GLB EvRec* xout;
   SGN_GLB uint32_t* xout_n;  // [n_ranks]
@@ -317,6 +323,12 @@ struct sgn_ctx {
   std::vector<void*> allocs;
   sgn::Ctrl* h_ctrl = nullptr;  // pinned mirror for reads
   uint64_t trace_cap = 0;
+  uint64_t drain_cap = 0;                 // sgn_drain_enable (EXTERNAL traffic)
+  std::vector<uint64_t> handles;          // sgn_submit handles by slot (tag & ~SGN_TAG_EXT)
+  std::vector<uint32_t> submit_seq;       // per owned host: submissions so far
+  std::vector<sgn_drain_rec> drain_held;  // drained from the device, not yet returned
+  void* d_stage = nullptr;                // sgn_submit staging (device)
+  uint64_t stage_cap = 0;
   uint64_t rounds_enqueued = 0;
 
   // multi-GPU

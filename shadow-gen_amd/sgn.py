@@ -21,6 +21,9 @@ EMUTIME_INVALID = 0xFFFFFFFFFFFFFFFF
 EMUTIME_MAX = 0xFFFFFFFFFFFFFFFE
 TRAFFIC_PERIODIC = 1
 TRAFFIC_TGEN = 2
+TRAFFIC_EXTERNAL = 3  # CPU-resident apps: sgn_submit / sgn_drain
+TAG_EXT = 0x80000000
+DRAIN_DELIVERED, DRAIN_LOCAL, DRAIN_LOSS, DRAIN_UNKNOWN, DRAIN_CODEL, DRAIN_BLOCKED = range(6)
 STAMP_WORDS = 96  # include/sgn.h SGN_STAMP_WORDS
 CREATE_TIME_KERNELS = 1
 
@@ -117,6 +120,35 @@ TRACE_DTYPE = np.dtype([("kind", "<u4"), ("host", "<u4"), ("peer", "<u4"), ("fla
 DIGEST_DTYPE = np.dtype([("tx", "<u8"), ("rx", "<u8"), ("app", "<u8"), ("rng", "<u8", (4,)),
                          ("next_event_id", "<u8"), ("n_sent", "<u8"), ("n_popped", "<u8"),
                          ("n_delivered", "<u8"), ("n_codel_dropped", "<u8")])
+
+
+class PktSoa(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("src_host", u32p), ("dst_ip", u32p), ("payload_len", u32p),
+                ("wire_len", u32p), ("send_time", u64p), ("handle", u64p)]
+
+
+class DrainRec(C.Structure):
+    _fields_ = [("time", C.c_uint64), ("src_eid", C.c_uint64), ("handle", C.c_uint64),
+                ("host", C.c_uint32), ("src_host", C.c_uint32), ("dst_host", C.c_uint32),
+                ("status", C.c_uint32), ("payload_len", C.c_uint32), ("tag", C.c_uint32)]
+
+
+DRAIN_DTYPE = np.dtype([("time", "<u8"), ("src_eid", "<u8"), ("handle", "<u8"), ("host", "<u4"),
+                        ("src_host", "<u4"), ("dst_host", "<u4"), ("status", "<u4"),
+                        ("payload_len", "<u4"), ("tag", "<u4")])
+assert DRAIN_DTYPE.itemsize == C.sizeof(DrainRec)
+
+
+def pkt_soa(src_host, dst_ip, payload_len, send_time, handle=None, wire_len=None):
+    """(PktSoa, keep-alive arrays) for sgn_submit / ora_sim_submit."""
+    a = [np.ascontiguousarray(src_host, dtype=np.uint32), np.ascontiguousarray(dst_ip, dtype=np.uint32),
+         np.ascontiguousarray(payload_len, dtype=np.uint32), np.ascontiguousarray(send_time, dtype=np.uint64)]
+    h = None if handle is None else np.ascontiguousarray(handle, dtype=np.uint64)
+    w = None if wire_len is None else np.ascontiguousarray(wire_len, dtype=np.uint32)
+    b = PktSoa(len(a[0]), ptr(a[0], C.c_uint32), ptr(a[1], C.c_uint32), ptr(a[2], C.c_uint32),
+               ptr(w, C.c_uint32) if w is not None else None, ptr(a[3], C.c_uint64),
+               ptr(h, C.c_uint64) if h is not None else None)
+    return b, (a, h, w)
 assert TRACE_DTYPE.itemsize == C.sizeof(TraceRec)
 assert DIGEST_DTYPE.itemsize == C.sizeof(HostDigest)
 
@@ -190,6 +222,13 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_selftest_codel_law": (C.c_int, [vp, C.c_uint64, u64p]),
         "sgn_debug_stamps": (C.c_int, [vp, u64p, C.c_uint64, u64p]),
         "sgn_debug_rounds": (C.c_int, [vp, u64p]),
+        "sgn_submit": (C.c_int, [vp, C.POINTER(PktSoa)]),
+        "sgn_drain_enable": (C.c_int, [vp, C.c_uint64]),
+        "sgn_drain": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(DrainRec), C.c_uint64, u64p]),
+        "sgn_set_window": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
+        "sgn_rng_next_u64": (C.c_int, [vp, C.c_uint32, u64p]),
+        "sgn_rng_double": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_double)]),
+        "sgn_rng_fill_bytes": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -374,6 +413,38 @@ class Context:
         out = np.zeros(n.value, dtype=TRACE_DTYPE)
         self.check(self.L.sgn_trace_read(self.h, out.ctypes.data_as(C.POINTER(TraceRec)), n.value, C.byref(n)))
         return out
+
+    # ---- CPU-resident applications (TRAFFIC_EXTERNAL) and the host RNG ----
+    def drain_enable(self, cap):
+        self.check(self.L.sgn_drain_enable(self.h, cap))
+
+    def submit(self, src_host, dst_ip, payload_len, send_time, handle=None, wire_len=None):
+        b, keep = pkt_soa(src_host, dst_ip, payload_len, send_time, handle, wire_len)
+        self.check(self.L.sgn_submit(self.h, C.byref(b)))
+
+    def drain(self, lo=0, hi=0xFFFFFFFF, cap=1 << 22):
+        out = np.zeros(cap, dtype=DRAIN_DTYPE)
+        n = C.c_uint64()
+        self.check(self.L.sgn_drain(self.h, lo, hi, out.ctypes.data_as(C.POINTER(DrainRec)), cap, C.byref(n)))
+        return out[: n.value]
+
+    def set_window(self, start, end):
+        self.check(self.L.sgn_set_window(self.h, start, end))
+
+    def rng_next_u64(self, host):
+        v = C.c_uint64()
+        self.check(self.L.sgn_rng_next_u64(self.h, host, C.byref(v)))
+        return v.value
+
+    def rng_double(self, host):
+        v = C.c_double()
+        self.check(self.L.sgn_rng_double(self.h, host, C.byref(v)))
+        return v.value
+
+    def rng_fill_bytes(self, host, n):
+        buf = (C.c_uint8 * max(1, n))()
+        self.check(self.L.sgn_rng_fill_bytes(self.h, host, buf, n))
+        return bytes(buf[:n])
 
     def kernel_times(self):
         k = KernelTimes()

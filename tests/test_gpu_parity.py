@@ -284,3 +284,77 @@ def test_two_shards_one_gpu_match_single(ctxf, oracle, kind, dynamic):
               "delivered", "codel_dropped", "local_events"):
         assert tot[k] == s1[k], k
     assert done.value == s1["rounds"]
+
+
+# ---- CPU-resident applications (SGN_TRAFFIC_EXTERNAL) and the device-held host RNG ----
+def _external_pair(ctxf, oracle, world, drain_cap=1 << 16):
+    g, used, hosts, cfg, tr = world
+    lat, loss = oracle.routes(g, used)
+    o = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=True)
+    c = ctxf()
+    c.routes_build(g, used)
+    c.hosts_set(hosts)
+    c.trace_enable(1 << 20)
+    c.drain_enable(drain_cap)
+    c.sim_init(cfg, tr)
+    return o, c
+
+
+def test_external_apps_submit_drain_rng(ctxf, oracle):
+    from external_common import datagrams, drive, external_world
+    world = external_world()
+    o, c = _external_pair(ctxf, oracle, world)
+    dg = datagrams(world[2])
+    (do, dc), rounds = drive([o, c], dg)
+    assert rounds > 50 and len(do) == len(dg[3])
+    for f in sgn.DRAIN_DTYPE.names:
+        bad = np.nonzero(do[f] != dc[f])[0]
+        assert len(bad) == 0, (f, do[bad[:3]], dc[bad[:3]])
+    st = np.bincount(dc["status"], minlength=6)
+    assert st[sgn.DRAIN_DELIVERED] > 0 and st[sgn.DRAIN_LOSS] > 0 and st[sgn.DRAIN_BLOCKED] > 0
+    assert_same_run(o, c, world[2].n)
+
+
+def test_external_rules_on_device(ctxf, oracle):
+    from external_common import RUNAHEAD, external_world
+    world = external_world(n=10, V=5, stop_ns=10_000_000_000)
+    o, c = _external_pair(ctxf, oracle, world)
+    S = SIM_START
+    ip = world[2].ip
+    c.round()
+    assert c.window()[2] is False
+    with pytest.raises(sgn.SgnError, match="empty window"):
+        c.set_window(S + 10, S + 10)
+    with pytest.raises(sgn.SgnError, match="longer than the runahead"):
+        c.set_window(S + 10, S + 10 + 10 * RUNAHEAD)
+    c.set_window(S + 5_000_000, S + 5_000_000 + RUNAHEAD)
+    with pytest.raises(sgn.SgnError, match="outside"):
+        c.submit([0], [ip[1]], [100], [S + 4_000_000])
+    with pytest.raises(sgn.SgnError, match="horizon"):
+        c.submit([0], [ip[1]], [100], [S + 5_000_000 + 5 * 10 ** 9])
+    with pytest.raises(sgn.SgnError, match="wire_len"):
+        c.submit([0], [ip[1]], [100], [S + 5_500_000], wire_len=[100])
+    with pytest.raises(sgn.SgnError, match="not owned"):
+        c.submit([10], [ip[1]], [100], [S + 5_500_000])
+    c.submit([0], [ip[1]], [100], [S + 5_500_000], handle=[77], wire_len=[128])
+    c.round()
+    ws, we, active = c.window()
+    assert active and ws > S + 5_500_000
+    with pytest.raises(sgn.SgnError, match="after the device"):
+        c.set_window(ws + 1, ws + 2)
+    with pytest.raises(sgn.SgnError, match="previous window"):
+        c.set_window(S + 5_000_000, S + 5_000_001)
+    while c.window()[2]:
+        c.round()
+    d = c.drain()
+    assert len(d) == 1 and d["handle"][0] == 77 and d["payload_len"][0] == 100
+    # the device RNG is the host's Xoshiro256++ stream (seeded as host.rs:234)
+    L = oracle.load()
+    st = np.zeros(4, dtype=np.uint64)
+    L.ora_xoshiro_seed_from_u64(int(world[2].seed[5]), sgn.ptr(st, sgn.C.c_uint64))
+    exp = [int(L.ora_xoshiro_next_u64(sgn.ptr(st, sgn.C.c_uint64))) for _ in range(3)]
+    assert c.rng_next_u64(5) == exp[0]
+    assert c.rng_double(5) == (exp[1] >> 11) * 2.0 ** -53
+    assert c.rng_fill_bytes(5, 3) == (exp[2] >> 32).to_bytes(4, "little")[:3]
+    with pytest.raises(sgn.SgnError):
+        sgn.Context().submit([0], [0], [0], [S])  # no simulation

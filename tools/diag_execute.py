@@ -38,7 +38,7 @@ for r in range(3):
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} runs={runs[i]:4d} max_lane={mx[i]:4d}"
               f" busy_lanes={busy[i]:2d}  cyc/event={cyc[i] / max(ev[i], 1):7.1f} gather={tg[i]} exec={tx[i]}")
         if s[i, 8:24].any():
-            names = ["ro", "ri", "app", "batch", "hdload", "fqload", "tbref", "poprun"]
+            names = ["ro", "ri", "app", "batch", "hdload", "fqload", "rmiss", "poprun"]
             print("      busiest lane: " + " ".join(f"{n}={s[i, 8 + k]}" for k, n in enumerate(names)))
             print("      wave sums:    " + " ".join(f"{n}={s[i, 16 + k]}" for k, n in enumerate(names)))
             tn = ["send", "fwdout", "fwdin", "pop", "app", "load"]
