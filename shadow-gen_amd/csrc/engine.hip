@@ -35,7 +35,14 @@
 #ifdef SGN_DIAG
 #define DG(i) (dg[i]++)
 #define DGT_BEGIN(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define DGT_END(i, v) (dgt[i] += (uint32_t)(__builtin_amdgcn_s_memtime() - (v)))
+// wave time in a section: added by the section's lowest active lane only (the lanes in a
+// section entered it together), so the wave's sum over lanes is the section's wave time
+#define DGT_END(i, v)                                                                  \
+  do {                                                                                 \
+    const uint64_t dgt_t = __builtin_amdgcn_s_memtime();                               \
+    if ((uint32_t)(__ffsll((long long)__ballot(1)) - 1) == (threadIdx.x & 63))         \
+      dgt[i] += (uint32_t)(dgt_t - (v));                                               \
+  } while (0)
 #else
 #define DG(i) ((void)0)
 #define DGT_BEGIN(v) ((void)0)
@@ -112,6 +119,12 @@ __device__ __forceinline__ void min_nr(SGN_GLB uint64_t* p, uint64_t v) {
   (void)__hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a rare per-host counter in the host record: a no-return atomic add, so the lane does not
+// wait for a load of the old value
+__device__ __forceinline__ void cnt_add(SGN_GLB uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // a / b for a divisor below 2^32: u32 division when the dividend fits too
 __device__ __forceinline__ uint64_t div_small(uint64_t a, uint64_t b) {
   if (((a | b) >> 32) == 0) return (uint32_t)a / (uint32_t)b;
@@ -182,13 +195,18 @@ struct Pkt {
 // ------------------------------------------------------------------------------------
 // A lane's LDS slot: the pending digest runs and the digests themselves (touched once per
 // run), and the CoDel queue's cached head and open tail runs.
+// LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
+// pad every lane's slot to a multiple of 16 B and cost a workgroup per CU)
+typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
+typedef FifoEnt FifoEnt8 __attribute__((aligned(8)));
 struct LaneLDS {
   sgn_drun run[3];   // tx, rx, app (sgn_workload.h)
   uint64_t dig[3];   // tx, rx, app digests
-  CodelEnt hd, tl;   // head run being consumed / tail run being extended
+  CodelEnt8 hd, tl;  // head run being consumed / tail run being extended
   uint64_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU)
   uint64_t cq[4];    // CoDel drop state: interval end, drop next, current / previous count
-  FifoEnt fh;        // copy of the send queue's head entry ...
+  uint64_t app_k;    // synthetic app counter
+  FifoEnt8 fh;       // copy of the send queue's head entry ...
   uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
   uint64_t rc_T;
   uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
@@ -282,6 +300,7 @@ struct HostExec {
     L->cq[1] = r.cq_dn;
     L->cq[2] = r.cq_cur;
     L->cq[3] = r.cq_prev;
+    L->app_k = r.app_k;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
@@ -350,6 +369,7 @@ struct HostExec {
     r.cq_dn = L->cq[1];
     r.cq_cur = L->cq[2];
     r.cq_prev = L->cq[3];
+    r.app_k = L->app_k;
     S.nextloc[h] = next_local_time();
     if (hd_valid) *cq_slot(0) = L->hd;
     if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
@@ -600,7 +620,7 @@ struct HostExec {
     return true;
   }
   __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
-    R->n_codel++;
+    cnt_add(&R->n_codel, 1);
     if (external()) drain_rec(SGN_DRAIN_CODEL, p.src, gid, p.eid, p.payload, p.tag);
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
@@ -679,7 +699,6 @@ struct HostExec {
   // the head entry (from the LDS copy when it is current)
   __device__ __forceinline__ FifoEnt fifo_head() {
     if (L->fh_idx == fq_head) return L->fh;
-    DG(DG_FQLOAD);
     const FifoEnt e = *fq_slot(0);
     L->fh = e;
     L->fh_idx = fq_head;
@@ -712,7 +731,8 @@ struct HostExec {
     if (external())
       for (uint32_t k = 0; k < m; k++) drain_rec(SGN_DRAIN_DELIVERED, src, gid, e0 + k, payload, tag);
     if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
-      const uint64_t size = S.file_bytes[tag & 3u];
+      const uint32_t c = tag & 3u;  // the class picks one of three (scalar) sizes
+      const uint64_t size = c == 0 ? S.file_bytes[0] : (c == 1 ? S.file_bytes[1] : S.file_bytes[2]);
       const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
       if (n == 0) return;
       const uint32_t last = (uint32_t)(size - (n - 1) * SGN_TGEN_MSS);
@@ -720,12 +740,12 @@ struct HostExec {
         if (fifo_push(src, SGN_TGEN_MSS, last, (uint32_t)n, SGN_TAG_RESP))
           relay_notify<0>();
         else
-          R->n_blocked++;
+          cnt_add(&R->n_blocked, 1);
       }
     }
   }
   __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
-    R->n_local_deliv++;
+    cnt_add(&R->n_local_deliv, 1);
     if (external()) drain_rec(SGN_DRAIN_LOCAL, gid, gid, 0, p.payload, p.tag);
     sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
     L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
@@ -810,10 +830,14 @@ struct HostExec {
             continue;
           }
         }
-        if (!codel_pop(&p)) {
+        DGT_BEGIN(tz0);
+        const bool gotp = codel_pop(&p);
+        DGT_END(DGT_LOAD, tz0);
+        if (!gotp) {
           set_relay_state<1>(RELAY_IDLE);
           return false;
         }
+        DG(DG_FQLOAD);
       }
       // the source address is the router's (0.0.0.0), never this host's: no local bypass
       if (!boot && !tb_remove<1>((uint64_t)p.payload + SGN_UDP_HEADER_BYTES, dur)) {
@@ -847,7 +871,7 @@ struct HostExec {
     DG(DG_BATCH);
     const bool boot = now < S.boot_end;
     if (dst == NO_HOST) {  // resolve_ip_to_host_id failed: InetDropped (worker.rs:347-357)
-      R->n_unknown += n;
+      cnt_add(&R->n_unknown, n);
       sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (S.trace_on)
         for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
@@ -879,6 +903,7 @@ struct HostExec {
     const uint64_t eid0 = eid;
     const bool can_drop = !boot && payload > 0;
     uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
+    DGT_BEGIN(tr0);
     for (uint32_t j = 0; j < n; j++) {
       const uint64_t x = rng_next() >> 11;
       if (can_drop && x >= T) {
@@ -894,6 +919,7 @@ struct HostExec {
         if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
       }
     }
+    DGT_END(DGT_APP, tr0);
     if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
     const uint32_t nsent = (uint32_t)(eid - eid0);
     if (nsent == 0) return;
@@ -949,41 +975,43 @@ struct HostExec {
   // comforming_remove (which applies the lazy refill) no further refill happens and the
   // number that conform is balance / wire_len; the first that does not is cached exactly
   // like Relay::next_packet.
-  __device__ bool forward_out(uint64_t* dur) {
+  // One step = the cached packet or one send-queue entry. The task runs step by step, one
+  // step per iteration of the wave's event loop (F_RO_CONT: the host stays inside the task,
+  // `now` does not move and none of its other events run until the queue is empty or the
+  // bucket blocks), so lanes forwarding long trains send them side by side instead of one
+  // after another (a train's per-packet loss draws are the serial part of a round).
+  __device__ void forward_out_step() {
+    DGT_BEGIN(tf0);
     const bool boot = now < S.boot_end;
-    set_relay_state<0>(RELAY_FORWARDING);
+    uint64_t dur = 0;
+    bool blocked = false;
     if (fl & F_RO_NEXT) {
       fl &= ~F_RO_NEXT;
       const bool is_local = ro_dst == gid;
-      if (!boot && !is_local) {
-        if (!tb_remove<0>((uint64_t)ro_pay + SGN_UDP_HEADER_BYTES, dur)) {
-          fl |= F_RO_NEXT;
-          set_relay_state<0>(RELAY_IDLE);
-          return true;
-        }
+      if (!boot && !is_local && !tb_remove<0>((uint64_t)ro_pay + SGN_UDP_HEADER_BYTES, &dur)) {
+        fl |= F_RO_NEXT;
+        blocked = true;
+      } else {
+        Pkt p;
+        p.src = gid;
+        p.dst_ip = my_ip;
+        p.payload = ro_pay;
+        p.tag = ro_tag;
+        p.eid = 0;
+        if (is_local)
+          deliver_local(p);
+        else
+          send_batch(ro_dst, ro_pay, ro_tag, 1);
       }
-      Pkt p;
-      p.src = gid;
-      p.dst_ip = my_ip;
-      p.payload = ro_pay;
-      p.tag = ro_tag;
-      p.eid = 0;
-      if (is_local)
-        deliver_local(p);
-      else
-        send_batch(ro_dst, ro_pay, ro_tag, 1);
-    }
-    while (fq_len > 0) {
-      DGT_BEGIN(tq0);
+    } else if (fq_len > 0) {
       const FifoEnt e = fifo_head();
       const uint32_t run = e.count == 1 ? 1u : e.count - 1;
       const uint32_t payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
       const uint64_t wire = (uint64_t)payload + SGN_UDP_HEADER_BYTES;
       const bool is_local = e.dst == gid;
       uint32_t n_ok = run;
-      bool blocked = false;
       if (!boot && !is_local) {
-        if (!tb_remove<0>(wire, dur)) {
+        if (!tb_remove<0>(wire, &dur)) {
           n_ok = 0;
           blocked = true;
         } else if (run > 1) {
@@ -994,11 +1022,10 @@ struct HostExec {
             tbb0 -= more * wire;
             n_ok = 1 + (uint32_t)more;
             blocked = true;
-            tb_remove<0>(wire, dur);  // fails: same `now`, gives the conforming duration
+            tb_remove<0>(wire, &dur);  // fails: same `now`, gives the conforming duration
           }
         }
       }
-      DGT_END(DGT_LOAD, tq0);
       if (is_local) {
         Pkt p;
         p.src = gid;
@@ -1010,7 +1037,6 @@ struct HostExec {
       } else {
         send_batch(e.dst, payload, e.tag, n_ok);
       }
-      DGT_BEGIN(tq1);
       const uint32_t consumed = n_ok + (blocked ? 1u : 0u);
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
@@ -1019,33 +1045,40 @@ struct HostExec {
         fq_slot(0)->count = e.count - consumed;
         L->fh.count = e.count - consumed;
       }
-      DGT_END(DGT_APP, tq1);
       if (blocked) {
         fl |= F_RO_NEXT;
         ro_dst = e.dst;
         ro_pay = payload;
         ro_tag = e.tag;
-        set_relay_state<0>(RELAY_IDLE);
-        return true;
       }
     }
-    set_relay_state<0>(RELAY_IDLE);
-    return false;
+    if (blocked || (fq_len == 0 && !(fl & F_RO_NEXT))) {  // the task returns
+      fl &= ~F_RO_CONT;
+      set_relay_state<0>(RELAY_IDLE);
+      if (blocked) forward_later<0>(dur);
+    }
+    DGT_END(DGT_FWDOUT, tf0);
   }
 
   // run_forward_task + forward_now (relay/mod.rs:166-187)
   template <int W>
   __device__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
+    if (W == 0) {  // forward_out_step continues it in the next iterations
+      set_relay_state<0>(RELAY_FORWARDING);
+      fl |= F_RO_CONT;
+      forward_out_step();
+      return;
+    }
     uint64_t dur;
     DGT_BEGIN(t0);
-    const bool blocked = W == 0 ? forward_out(&dur) : forward_in(&dur);
-    DGT_END(W == 0 ? DGT_FWDOUT : DGT_FWDIN, t0);
+    const bool blocked = forward_in(&dur);
+    DGT_END(DGT_FWDIN, t0);
     if (blocked) forward_later<W>(dur);
   }
 
   __device__ void app_task() {
-    const uint64_t k = R->app_k++;
+    const uint64_t k = L->app_k++;
     uint32_t dst, payload, tag;
     uint64_t next_delay;
     if (S.tkind == SGN_TRAFFIC_PERIODIC) {
@@ -1067,7 +1100,7 @@ struct HostExec {
     if (fifo_push(dst, payload, payload, 1, tag))
       relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
     else
-      R->n_blocked++;
+      cnt_add(&R->n_blocked, 1);
     schedule<SLOT_APP>(now + next_delay);
   }
 
@@ -1082,7 +1115,7 @@ struct HostExec {
     if (fifo_push(dst, payload, payload, 1, e.tag)) {
       relay_notify<0>();
     } else {
-      R->n_blocked++;
+      cnt_add(&R->n_blocked, 1);
       drain_rec(SGN_DRAIN_BLOCKED, gid, NO_HOST, 0, payload, e.tag);
     }
   }
@@ -1110,7 +1143,7 @@ struct HostExec {
       {  // wave-level: iterations, and iterations in which some lane runs each handler;
          // the previous iteration's cycles are added to its handler combination's slot
         const bool ispop = pi < s1 && ev[ord[pi]].time <= lt;
-        const int kind = ispop ? 0 : (lt >= until ? 4 : 1 + ls);
+        const int kind = (fl & F_RO_CONT) ? 1 : ispop ? 0 : (lt >= until ? 4 : 1 + ls);
         const uint64_t act = __ballot(1);
         const uint64_t b0 = __ballot(kind == 0), b1 = __ballot(kind == 1),
                        b2 = __ballot(kind == 2), b3 = __ballot(kind == 3);
@@ -1133,6 +1166,10 @@ struct HostExec {
         it_t = tnow;
       }
 #endif
+      if (fl & F_RO_CONT) {  // inside relay_inet_out's forwarding task (forward_out_step)
+        forward_out_step();
+        continue;
+      }
       if (pi < s1) {
         const EvRec& e = ev[ord[pi]];
         if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
@@ -1556,8 +1593,8 @@ __device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we
     }
     for (int i = 0; i < DGT_N; i++) {
       const uint32_t v = loaded ? ex.dgt[i] : 0u;
-      const uint32_t vb = __shfl(v, bl, 64);
-      if (lane == 0) st[24 + i] = vb;
+      const uint32_t vs = wave_sum_u32(v);  // the wave's time in section i
+      if (lane == 0) st[24 + i] = vs;
     }
     if (lane == 0) {
       st[32] = w_load;

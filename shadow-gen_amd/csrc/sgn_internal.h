@@ -116,7 +116,7 @@ enum : uint32_t {
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
 // A round touches only the hosts with something due (~1 in 8 at the bench workload), so a
 // record per host turns each executed host's state into 3 contiguous cache lines; the hot
-// part (bytes 0..327) is what Host::execute reads and writes every time it runs.
+// part (bytes 0..335) is what Host::execute reads and writes every time it runs.
 struct __attribute__((aligned(128))) HostRec {
   uint64_t rng[4];           // Xoshiro256++ state (host/host.rs:234)
   uint64_t eid;              // next event id (host.rs:259,662-666)
@@ -136,14 +136,14 @@ struct __attribute__((aligned(128))) HostRec {
   uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
   uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
   uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
-  // cold: rare paths only
   uint64_t app_k;                            // synthetic app counter
+  // cold: rare paths only
   uint64_t tseq;                            // trace sequence
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
   uint64_t pad[17];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
-static_assert(offsetof(HostRec, cq_prev) + 8 <= 384, "hot part: three cache lines");
+static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
 
 // per-wave counters (DevSim::w_cnt rows of G)
 enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_N };
@@ -159,6 +159,7 @@ enum : uint32_t {
   F_CODEL_IE = 0x100u,       // CoDel interval_end is Some
   F_CODEL_DN = 0x200u,       // CoDel drop_next is Some
   F_HAS_APP = 0x400u,        // host runs a synthetic app timer
+  F_RO_CONT = 0x800u,        // inside relay_inet_out's forwarding task (never stored)
 };
 
 enum { SLOT_RO = 0, SLOT_RI = 1, SLOT_APP = 2, NSLOT = 3 };
