@@ -777,8 +777,13 @@ struct HostExec {
           // by the first that leaves less; the queued bytes only fall here, so the last pop
           // decides). After the first comforming_remove (which applies the lazy refill)
           // balance / wire more packets conform; the first that does not is cached.
+          // In drop mode before drop_next, pop returns every packet without a drop too
+          // (drop_from_drop_mode's loop does not run, :172-201) and changes nothing until a
+          // pop leaves <= MTU queued (then interval_end and drop mode end).
           const bool standing = sat_sub(now, L->hd.enqueue_ts) >= CODEL_TARGET;
-          if (!standing || !((fl & F_CODEL_IE) && now >= L->cq[0])) {
+          const bool ie_due = (fl & F_CODEL_IE) && now >= L->cq[0];
+          const bool drop_quiet = (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now < L->cq[1];
+          if (!standing || !ie_due || drop_quiet) {
             const uint32_t n = L->hd.count;
             const uint64_t wire = (uint64_t)L->hd.payload + SGN_UDP_HEADER_BYTES;
             uint32_t m = n;
@@ -805,13 +810,15 @@ struct HostExec {
             L->hd.count -= used;
             cq_len -= used;
             cq_bytes = sat_sub(cq_bytes, (uint64_t)used * wire);
-            fl &= ~F_CODEL_DROP;
             if (!standing || cq_bytes <= SGN_CONFIG_MTU) {
-              fl &= ~F_CODEL_IE;
-            } else if (!(fl & F_CODEL_IE)) {
-              fl |= F_CODEL_IE;
-              L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
-            }
+              fl &= ~(F_CODEL_IE | F_CODEL_DROP);
+            } else if (!ie_due) {
+              fl &= ~F_CODEL_DROP;
+              if (!(fl & F_CODEL_IE)) {
+                fl |= F_CODEL_IE;
+                L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
+              }
+            }  // else drop mode before drop_next: unchanged
             if (L->hd.count == 0) {
               hd_valid = false;
               cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
