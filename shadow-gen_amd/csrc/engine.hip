@@ -1,18 +1,22 @@
 // engine.hip — the per-round packet path of Shadow on gfx950.
 //
-// One simulation round (core/manager.rs:541-656) is six launches on one stream:
-//   k_count      count the calendar events due in [ws, we) per destination host
-//   k_scan_*     exclusive scan of the counts -> per-host segment offsets
-//   k_scatter    place due events into their destination's segment; survivors of the
-//                partially consumed bucket move to the spare slab
-//   k_execute    one lane per host: order the segment by (time, src host, src event id)
-//                (core/work/event.rs:84-183), merge it with the host's local events and run
-//                Host::execute (host/host.rs:762-830) — router/CoDel, relays, token
-//                buckets, Worker::send_packet — emitting new events into the calendar
-//   k_finalize   bucket bookkeeping, min next event over queue heads (manager.rs:580-628),
-//                Controller::manager_finished_current_round (controller.rs:88-112)
-// The window lives in device memory (Ctrl), so rounds are enqueued back to back without a
-// host round trip; every kernel returns immediately once the simulation has ended.
+// One wave of 64 lanes per host group (64 consecutive hosts, lane = host). A simulation
+// round (core/manager.rs:541-656) for a group is exec_group():
+//   gather   the group's calendar slabs of the window's buckets -> LDS (device-scope loads);
+//            runs due later in the last bucket move to the spare slab set
+//   order    counting sort of the due event runs by destination lane, rank sort inside each
+//            lane's segment by (time, src host, src event id) (core/work/event.rs:84-183)
+//   execute  every lane runs Host::execute (host/host.rs:762-830) over its segment merged
+//            with its three local event slots: router/CoDel, relays and token buckets,
+//            Worker::send_packet (loss draws from the host's Xoshiro256++), emitting event
+//            runs into the destinations' calendar slabs
+//   edge     minimum next event, bucket bookkeeping, Controller::manager_finished_current_
+//            round (controller.rs:88-112) — run by the last wave to arrive
+// Kernels: k_rounds (single shard, persistent: up to 128 rounds per launch with an atomic
+// grid barrier per round), k_execute (one round per launch: sgn_round, multi-shard) with
+// k_finalize / k_import / k_advance around the RCCL exchange (comm.cpp), k_inject
+// (sgn_submit), k_rng (sgn_rng_*). The window lives in device memory (Ctrl), so rounds run
+// back to back without a host round trip.
 //
 // Bit-exactness notes: all time/byte/event-id arithmetic is u64 integer; the only floating
 // point is (a) reliability = (f64)(1.0f - loss) vs the f64 draw (x >> 11) * 2^-53
@@ -253,7 +257,7 @@ struct HostExec {
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
-  __device__ void load() {
+  __device__ __forceinline__ void load() {
     R = S.hrec + h;
     const HostRec& r = *R;
     gid = S.lo + h;
@@ -324,7 +328,7 @@ struct HostExec {
 #endif
   }
 
-  __device__ void store() {
+  __device__ __forceinline__ void store() {
     HostRec& r = *R;
     r.rng[0] = r0;
     r.rng[1] = r1;
@@ -378,7 +382,7 @@ struct HostExec {
   // rare counters go straight to memory (registers are kept for the per-packet ones)
 
 
-  __device__ uint64_t next_local_time() const {
+  __device__ __forceinline__ uint64_t next_local_time() const {
     uint64_t m = st0;
     m = st1 < m ? st1 : m;
     m = st2 < m ? st2 : m;
@@ -397,11 +401,20 @@ struct HostExec {
     r3 = rotl64(r3, 45);
     return result;
   }
+  __device__ __forceinline__ void rng_skip() {  // rng_next without its output
+    const uint64_t t = r1 << 17;
+    r2 ^= r0;
+    r3 ^= r1;
+    r1 ^= r2;
+    r0 ^= r3;
+    r2 ^= t;
+    r3 = rotl64(r3, 45);
+  }
   __device__ __forceinline__ double rng_f64() {
     return (double)(rng_next() >> 11) * 0x1.0p-53;
   }
 
-  __device__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
+  __device__ __forceinline__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
                         uint64_t c) {
     if (!S.trace_on) return;
     const uint64_t seq = R->tseq++;
@@ -422,12 +435,12 @@ struct HostExec {
     S.trace[pos] = r;
   }
 
-  __device__ void overflow(uint32_t bit) {
+  __device__ __forceinline__ void overflow(uint32_t bit) {
     if ((atomicOr(&C->overflow, bit) & bit) == 0) C->overflow_info = gid;
   }
 
   // EXTERNAL traffic: a datagram's fate for the CPU-side applications (sgn_drain)
-  __device__ void drain_rec(uint32_t status, uint32_t src, uint32_t dst, uint64_t seid,
+  __device__ __forceinline__ void drain_rec(uint32_t status, uint32_t src, uint32_t dst, uint64_t seid,
                             uint32_t payload, uint32_t tag) {
     const uint64_t pos = atomicAdd((unsigned long long*)&C->drain_n, 1ULL);
     if (pos >= S.drain_cap) {
@@ -484,7 +497,7 @@ struct HostExec {
 
   // ---- TokenBucket::comforming_remove (network/relay/token_bucket.rs:65-154) ----
   template <int W>
-  __device__ bool tb_remove(uint64_t dec, uint64_t* dur) {
+  __device__ __forceinline__ bool tb_remove(uint64_t dec, uint64_t* dur) {
     uint64_t& bal = W == 0 ? tbb0 : tbb1;
     uint64_t& last = W == 0 ? tbl0 : tbl1;
     const uint64_t interval = 1000000ULL;  // relay/mod.rs:279
@@ -540,7 +553,7 @@ struct HostExec {
   }
   // Router::route_incoming_packet (router/mod.rs:55-57) -> CoDelQueue::push (:303-317) for a
   // run of n packets arriving at `now`: extends the open tail run when it continues it.
-  __device__ void codel_push_run(uint32_t src, uint64_t eid0, uint32_t payload, uint32_t tag,
+  __device__ __forceinline__ void codel_push_run(uint32_t src, uint64_t eid0, uint32_t payload, uint32_t tag,
                                  uint32_t n) {
     const auto continues = [&](const CodelEnt& r) {
       return r.enqueue_ts == now && r.src == src && r.eid + r.count == eid0 &&
@@ -573,7 +586,7 @@ struct HostExec {
     if (cq_len > c_maxcodel) c_maxcodel = cq_len;
   }
   // process_standing_delay (:231-262)
-  __device__ bool codel_standing(uint64_t sd) {
+  __device__ __forceinline__ bool codel_standing(uint64_t sd) {
     if (sd < CODEL_TARGET || cq_bytes <= SGN_CONFIG_MTU) {
       fl &= ~F_CODEL_IE;
       return false;
@@ -596,7 +609,7 @@ struct HostExec {
     hd_valid = true;
   }
   // codel_pop (:204-227)
-  __device__ bool codel_pop_raw(Pkt* p, bool* ok_to_drop) {
+  __device__ __forceinline__ bool codel_pop_raw(Pkt* p, bool* ok_to_drop) {
     if (cq_len == 0) {
       fl &= ~F_CODEL_IE;
       return false;
@@ -619,18 +632,18 @@ struct HostExec {
     p->eid = e.eid;
     return true;
   }
-  __device__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
+  __device__ __forceinline__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
     cnt_add(&R->n_codel, 1);
     if (external()) drain_rec(SGN_DRAIN_CODEL, p.src, gid, p.eid, p.payload, p.tag);
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
-  __device__ bool codel_was_dropping_recently() const {  // :273-281
+  __device__ __forceinline__ bool codel_was_dropping_recently() const {  // :273-281
     if (!(fl & F_CODEL_DN)) return false;
     return sat_sub(now, L->cq[1]) < CODEL_INTERVAL * 16;
   }
   // CoDelQueue::pop (:125-201)
-  __device__ bool codel_pop(Pkt* out) {
+  __device__ __forceinline__ bool codel_pop(Pkt* out) {
     Pkt p;
     bool okd;
     if (!codel_pop_raw(&p, &okd)) {
@@ -680,7 +693,7 @@ struct HostExec {
     if (idx >= S.fifo_cap) idx -= S.fifo_cap;
     return S.fifo + (size_t)h * S.fifo_cap + idx;
   }
-  __device__ bool fifo_push(uint32_t dst, uint32_t payload, uint32_t last, uint32_t count,
+  __device__ __forceinline__ bool fifo_push(uint32_t dst, uint32_t payload, uint32_t last, uint32_t count,
                             uint32_t tag) {
     if (fq_len >= S.fifo_cap) return false;
     FifoEnt e;
@@ -721,7 +734,7 @@ struct HostExec {
 
   // interface delivery to the synthetic app (NetworkInterface::push -> socket) of m packets
   // from src with consecutive event ids e0.. at `now` (one run-encoded app digest step)
-  __device__ void deliver_run(uint32_t src, uint64_t e0, uint32_t m, uint32_t payload,
+  __device__ __forceinline__ void deliver_run(uint32_t src, uint64_t e0, uint32_t m, uint32_t payload,
                               uint32_t tag) {
     c_deliv += m;
     c_bytes += (uint64_t)m * payload;
@@ -744,7 +757,7 @@ struct HostExec {
       }
     }
   }
-  __device__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
+  __device__ __forceinline__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
     cnt_add(&R->n_local_deliv, 1);
     if (external()) drain_rec(SGN_DRAIN_LOCAL, gid, gid, 0, p.payload, p.tag);
     sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
@@ -753,7 +766,7 @@ struct HostExec {
 
   // ---- Relay::forward_until_blocked (network/relay/mod.rs:201-273) for relay_inet_in:
   //      the router's CoDel queue -> the interface (relay_inet_out uses forward_out) ----
-  __device__ bool forward_in(uint64_t* dur) {
+  __device__ __forceinline__ bool forward_in(uint64_t* dur) {
     const bool boot = now < S.boot_end;
     set_relay_state<1>(RELAY_FORWARDING);
     while (true) {
@@ -867,13 +880,26 @@ struct HostExec {
   // digest takes runs of equal outcomes. Sent packets take consecutive source event ids and
   // share one delivery time, so their events are reserved with one atomic and written as
   // one contiguous run.
-  __device__ void send_batch(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
+  __device__ __forceinline__ void send_batch(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
     DGT_BEGIN(t0);
     send_batch_(dst, payload, tag, n);
     DGT_END(DGT_SEND, t0);
   }
+  // one loss-draw outcome of send_batch_'s record-free path (tx digest runs only)
+  __device__ __forceinline__ void loss_step(bool lost, uint32_t& run, uint32_t& sent, uint32_t dst,
+                                            uint64_t deliver) {
+    if (lost) {
+      c_loss++;
+      if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
+      run = 0;
+      sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
+    } else {
+      run++;
+      sent++;
+    }
+  }
   // dst: the HostId the address resolves to (FifoEnt), NO_HOST: not in the simulation
-  __device__ void send_batch_(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
+  __device__ __forceinline__ void send_batch_(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
     if (n == 0 || now >= S.end_time) return;
     DG(DG_BATCH);
     const bool boot = now < S.boot_end;
@@ -911,20 +937,46 @@ struct HostExec {
     const bool can_drop = !boot && payload > 0;
     uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
     DGT_BEGIN(tr0);
-    for (uint32_t j = 0; j < n; j++) {
-      const uint64_t x = rng_next() >> 11;
-      if (can_drop && x >= T) {
-        c_loss++;
-        if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
-        run = 0;
-        sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
-        if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
-        if (external()) drain_rec(SGN_DRAIN_LOSS, gid, dst, 0, payload, tag);
-      } else {
-        const uint64_t e = eid++;
-        run++;
-        if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+    if (S.trace_on || external()) {  // per-packet records
+      for (uint32_t j = 0; j < n; j++) {
+        const uint64_t x = rng_next() >> 11;
+        if (can_drop && x >= T) {
+          c_loss++;
+          if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
+          run = 0;
+          sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
+          if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+          if (external()) drain_rec(SGN_DRAIN_LOSS, gid, dst, 0, payload, tag);
+        } else {
+          const uint64_t e = eid++;
+          run++;
+          if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+        }
       }
+    } else if (!can_drop || T >= (1ULL << 53)) {
+      // nothing can drop (bootstrapping, empty payload, or a lossless path: chance < 1.0 =
+      // reliability always); the draws still advance the stream (worker.rs:366 draws first)
+      for (uint32_t j = 0; j < n; j++) rng_skip();
+      run = n;
+      eid += n;
+    } else {
+      // x >> 11 >= T  <=>  x >= T << 11 (T < 2^53); four draws per test in the common case
+      const uint64_t Tx = T << 11;
+      uint32_t sent = 0, j = 0;
+      for (; j + 4 <= n; j += 4) {
+        const uint64_t x0 = rng_next(), x1 = rng_next(), x2 = rng_next(), x3 = rng_next();
+        if ((x0 >= Tx) | (x1 >= Tx) | (x2 >= Tx) | (x3 >= Tx)) {
+          loss_step(x0 >= Tx, run, sent, dst, deliver);
+          loss_step(x1 >= Tx, run, sent, dst, deliver);
+          loss_step(x2 >= Tx, run, sent, dst, deliver);
+          loss_step(x3 >= Tx, run, sent, dst, deliver);
+        } else {
+          run += 4;
+          sent += 4;
+        }
+      }
+      for (; j < n; j++) loss_step(rng_next() >= Tx, run, sent, dst, deliver);
+      eid += sent;
     }
     DGT_END(DGT_APP, tr0);
     if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
@@ -987,7 +1039,7 @@ struct HostExec {
   // `now` does not move and none of its other events run until the queue is empty or the
   // bucket blocks), so lanes forwarding long trains send them side by side instead of one
   // after another (a train's per-packet loss draws are the serial part of a round).
-  __device__ void forward_out_step() {
+  __device__ __forceinline__ void forward_out_step() {
     DGT_BEGIN(tf0);
     const bool boot = now < S.boot_end;
     uint64_t dur = 0;
@@ -1069,7 +1121,7 @@ struct HostExec {
 
   // run_forward_task + forward_now (relay/mod.rs:166-187)
   template <int W>
-  __device__ void run_forward_task() {
+  __device__ __forceinline__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
     if (W == 0) {  // forward_out_step continues it in the next iterations
       set_relay_state<0>(RELAY_FORWARDING);
@@ -1084,7 +1136,7 @@ struct HostExec {
     if (blocked) forward_later<W>(dur);
   }
 
-  __device__ void app_task() {
+  __device__ __forceinline__ void app_task() {
     const uint64_t k = L->app_k++;
     uint32_t dst, payload, tag;
     uint64_t next_delay;
@@ -1115,7 +1167,7 @@ struct HostExec {
   // queue and notifies relay_inet_out (Host::notify_socket_has_packets, host.rs:969-983),
   // as app_task does for the synthetic apps. The record carries the destination address in
   // the low half of its event id (the high half is the submission order).
-  __device__ void app_submit(const EvRec& e) {
+  __device__ __forceinline__ void app_submit(const EvRec& e) {
     uint32_t dst;
     if (!dns_lookup((uint32_t)e.eid, &dst)) dst = NO_HOST;
     const uint32_t payload = ev_payload(e);
@@ -1133,7 +1185,7 @@ struct HostExec {
   // time < until. A window is executed as consecutive sub-windows (one per calendar
   // bucket): nothing created inside a window is due in it (packet deliveries are >= the
   // window end, worker.rs:386-390), so this is the same sequence of events.
-  __device__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
+  __device__ __forceinline__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
                       uint64_t until) {
     uint32_t pi = s0;
 #ifdef SGN_DIAG
