@@ -37,7 +37,7 @@
 // Diagnostic build (libsgn_diag.so, -DSGN_DIAG): per-lane counts of the work kinds that
 // carry dependent global-memory round trips, reported through sgn_debug_stamps.
 #ifdef SGN_DIAG
-#define DG(i) (dg[i]++)
+#define DG(i) ((void)0)  // per-lane work counts: off (registers; see DGT sections)
 #define DGT_BEGIN(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 // wave time in a section: added by the section's lowest active lane only (the lanes in a
 // section entered it together), so the wave's sum over lanes is the section's wave time
@@ -247,7 +247,6 @@ struct HostExec {
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint32_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
 #ifdef SGN_DIAG
-  uint32_t dg[DG_N];
   uint32_t dgt[DGT_N];
   uint32_t wk[5];
 #endif
@@ -322,7 +321,6 @@ struct HostExec {
     }
     L->run[0].n = L->run[1].n = L->run[2].n = 0;
 #ifdef SGN_DIAG
-    for (int i = 0; i < DG_N; i++) dg[i] = 0;
     for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
     for (int i = 0; i < 5; i++) wk[i] = 0;
 #endif
@@ -1454,7 +1452,7 @@ struct ExecLDS {
 //  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
 //     segment and local slots, emitting new runs into the calendar / exchange slots;
 //  4. the group's minimum kept-event time and next local event time are returned.
-__device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
+__device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
                            const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out) {
   SGN_GLB Ctrl* C = S.ctrl;
   EvRec* lev = X.lev;
@@ -1642,7 +1640,7 @@ __device__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we
     const uint64_t bm = __ballot(loaded && n_ev == mx);
     const int bl = bm ? __ffsll((long long)bm) - 1 : 0;
     for (int i = 0; i < DG_N; i++) {
-      const uint32_t v = loaded ? ex.dg[i] : 0u;
+      const uint32_t v = 0u;  // (per-lane work counts disabled)
       const uint32_t vb = __shfl(v, bl, 64);
       const uint32_t vs = wave_sum_u32(v);
       if (lane == 0) {

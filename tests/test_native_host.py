@@ -5,6 +5,8 @@ multiply-high and shifts; it must equal x / d for every u64 x."""
 import pathlib
 import subprocess
 
+import pytest
+
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
@@ -17,3 +19,49 @@ def test_udiv64_matches_division(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert " 0 bad" in out.stdout
+
+
+def _kernel_meta(so):
+    """AMDGPU kernel metadata (per kernel: private segment, VGPRs, spills) of every gfx950
+    code object bundled into a built library."""
+    import re
+    import tempfile
+    d = pathlib.Path(tempfile.mkdtemp())
+    fb = d / "fb.bin"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", str(so), str(fb)], check=True)
+    data = fb.read_bytes()
+    offs = [m.start() for m in re.finditer(re.escape(b"__CLANG_OFFLOAD_BUNDLE__"), data)]
+    out = {}
+    llvm = pathlib.Path("/opt/rocm/lib/llvm/bin")
+    for i, o in enumerate(offs):
+        b, co = d / f"b{i}.bin", d / f"b{i}.co"
+        b.write_bytes(data[o:offs[i + 1] if i + 1 < len(offs) else len(data)])
+        r = subprocess.run([str(llvm / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+        if r.returncode:
+            continue
+        notes = subprocess.run([str(llvm / "llvm-readelf"), "--notes", str(co)], capture_output=True,
+                               text=True, check=True).stdout
+        cur = None
+        for line in notes.splitlines():
+            m = re.match(r"\s+\.name:\s+(\S+)", line)
+            if m:
+                cur = m.group(1)
+                out[cur] = {}
+            m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_count|vgpr_spill_count):\s+(\d+)", line)
+            if m and cur:
+                out[cur][m.group(1)] = int(m.group(2))
+    return out
+
+
+@pytest.mark.skipif(not pathlib.Path("/opt/rocm/lib/llvm/bin/clang-offload-bundler").exists(),
+                    reason="ROCm LLVM tools absent")
+def test_round_kernels_have_no_scratch():
+    # the round kernels must keep every host's state in registers/LDS: a non-inlined helper
+    # or a spill puts it in scratch memory and costs ~2x (seen when send_batch was outlined)
+    meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
+    for k in ("k_rounds", "k_execute"):
+        (name,) = [n for n in meta if k in n]
+        m = meta[name]
+        assert m["private_segment_fixed_size"] == 0, (k, m)
+        assert m["vgpr_spill_count"] == 0 and m["vgpr_count"] <= 256, (k, m)
