@@ -199,6 +199,17 @@ struct Pkt {
 // ------------------------------------------------------------------------------------
 // A lane's LDS slot: the pending digest runs and the digests themselves (touched once per
 // run), and the CoDel queue's cached head and open tail runs.
+// The wave's outbox: event records for this shard's calendar, placed after the event loop
+// by all 64 lanes at once (one round trip for all the slab reservations of the wave instead
+// of one per send in the sending lane's serial path). A full outbox falls back to placing
+// the record at once.
+constexpr uint32_t OBOX = 24;
+struct Outbox {
+  EvRec rec[OBOX];
+  uint32_t idx[OBOX];  // (slab set, group) slab index
+  uint32_t n;          // records appended (may exceed OBOX: those were placed directly)
+};
+
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
 // pad every lane's slot to a multiple of 16 B and cost a workgroup per CU)
 typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
@@ -246,14 +257,15 @@ struct HostExec {
   LaneLDS* L;
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint32_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
+  Outbox* ob;             // the wave's outbox (LDS)
 #ifdef SGN_DIAG
   uint32_t dgt[DGT_N];
   uint32_t wk[5];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS* l, const uint32_t* bs)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs) {}
+                      LaneLDS* l, const uint32_t* bs, Outbox* o)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ __forceinline__ void load() {
@@ -848,9 +860,7 @@ struct HostExec {
             continue;
           }
         }
-        DGT_BEGIN(tz0);
         const bool gotp = codel_pop(&p);
-        DGT_END(DGT_LOAD, tz0);
         if (!gotp) {
           set_relay_state<1>(RELAY_IDLE);
           return false;
@@ -995,8 +1005,22 @@ struct HostExec {
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
-      pos = atomicAdd(&S.slab_n[idx], nrec);
       min_nr(b == b1 ? &C->keep_min : &S.bucket_min[b], deliver);
+      if (nrec == 1) {
+        const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
+        if (k < OBOX) {
+          EvRec& r = ob->rec[k];
+          r.time = deliver;
+          r.eid = eid0;
+          r.src = gid;
+          r.dst = dst;
+          r.pc = payload | (nsent << 16);
+          r.tag = tag;
+          ob->idx[k] = (uint32_t)idx;
+          return;
+        }
+      }
+      pos = atomicAdd(&S.slab_n[idx], nrec);
       dstp = S.pool + idx * S.CAP;
       cap = S.CAP;
     } else {
@@ -1211,13 +1235,8 @@ struct HostExec {
           wk[2] += b1 != 0;
           wk[3] += b2 != 0;
           wk[4] += b3 != 0;
-          if (S.stamps) {
-            SGN_GLB uint64_t* st = S.stamps + SGN_STAMP_WORDS * (size_t)(h >> S.gsh);
-            if (it_mask < 16) {
-              st[48 + it_mask] += tnow - it_t;
-              st[64 + it_mask] += 1;
-            }
-          }
+          // (per-combination cycles: off — a global read-modify-write per iteration would
+          // add a dependent round trip to every iteration of the diag build)
         }
         it_mask = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u) | (b3 ? 8u : 0u);
         it_t = tnow;
@@ -1271,7 +1290,7 @@ struct HostExec {
         DG(DG_APP);
         DGT_BEGIN(t0);
         app_task();
-        DGT_END(DGT_APP, t0);
+        DGT_END(DGT_LOAD, t0);
       }
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
@@ -1441,6 +1460,7 @@ struct ExecLDS {
   uint32_t* lcur;
   LaneLDS* lslot;     // the lanes' LDS slots
   uint32_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB)
+  Outbox* ob;         // the wave's outbox
 };
 
 // One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
@@ -1481,7 +1501,10 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 
   uint64_t lmin = INVALID;
   if (valid) lmin = S.nextloc[h];
-  HostExec ex(S, h, we, be, ks, lslot + lane, lbs);
+  Outbox* ob = X.ob;
+  if (lane == 0) ob->n = 0;
+  __syncthreads();
+  HostExec ex(S, h, we, be, ks, lslot + lane, lbs, ob);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -1598,6 +1621,19 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     }
   }
 
+  // the outbox's records into their slabs, all lanes at once (the arrival's vmcnt(0)
+  // completes them before the round edge)
+  {
+    const uint32_t no = min(ob->n, OBOX);
+    for (uint32_t i = lane; i < no; i += 64) {
+      const uint32_t idx = ob->idx[i];
+      const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+      if (pos < S.CAP)
+        st_dev_rec(S.pool + (size_t)idx * S.CAP + pos, ob->rec[i]);
+      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+        C->overflow_info = ob->rec[i].dst;
+    }
+  }
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
   uint32_t n_ev = 0;
 #ifdef SGN_DIAG
@@ -1694,6 +1730,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   __shared__ uint32_t lcnt_[64], lstart_[64], lcur_[64];                             \
   __shared__ LaneLDS lslot_[64];                                                     \
   __shared__ uint32_t lbs_[LDS_BSLAB];                                               \
+  __shared__ Outbox ob_;                                                             \
   ExecLDS X;                                                                         \
   X.lev = (EvRec*)lds_dyn;                                                           \
   X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \
@@ -1702,7 +1739,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.lstart = lstart_;                                                                \
   X.lcur = lcur_;                                                                    \
   X.lslot = lslot_;                                                                  \
-  X.lbs = lbs_;
+  X.lbs = lbs_;                                                                      \
+  X.ob = &ob_;
 
 // Arrival of one workgroup at the end of a round: its minima go into its chunk's slots with
 // returning device-scope atomics, then it counts itself in (64 workgroups per chunk counter,
@@ -1991,6 +2029,7 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow & OVF_SEG) what += " due-event segment buffer";
   if (c.overflow & OVF_EXCHANGE) what += " exchange slot (raise exchange_slot_events)";
   if (c.overflow & OVF_TRACE) what += " trace buffer";
+  if (c.overflow & OVF_TIMEOUT) what += " persistent grid barrier timed out (grid not resident)";
   if (c.overflow & OVF_DRAIN) what += " drain buffer (raise sgn_drain_enable's capacity or drain more often)";
   return set_error(ctx, SGN_EOVERFLOW,
                    "device capacity exceeded:" + what + " (info " +
@@ -2375,7 +2414,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_rounds, 64, dyn) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
         hipFuncGetAttributes(&fa, (const void*)k_rounds) == hipSuccess && occ > 0 && ncu > 0) {
-      const int lds_occ = (int)((160u * 1024u) / (fa.sharedSizeBytes + dyn));
+      // LDS is allocated per workgroup in 512-byte granules (a 23184-byte workgroup fits 6
+      // per CU, not 7: a grid sized for 7 was not resident and its barrier timed out)
+      const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
+      const int lds_occ = (int)((160u * 1024u) / lds_wg);
       occ = std::min(occ, lds_occ);
       ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, (uint64_t)occ * (uint64_t)ncu);
     }

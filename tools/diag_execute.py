@@ -37,11 +37,8 @@ for r in range(3):
     for i in order[:12]:
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} runs={runs[i]:4d} max_lane={mx[i]:4d}"
               f" busy_lanes={busy[i]:2d}  cyc/event={cyc[i] / max(ev[i], 1):7.1f} gather={tg[i]} exec={tx[i]}")
-        if s[i, 8:24].any():
-            names = ["ro", "ri", "app", "batch", "hdload", "slowpkt", "rmiss", "poprun"]
-            print("      busiest lane: " + " ".join(f"{n}={s[i, 8 + k]}" for k, n in enumerate(names)))
-            print("      wave sums:    " + " ".join(f"{n}={s[i, 16 + k]}" for k, n in enumerate(names)))
-            tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "codelpop"]
+        if s[i, 24:30].any():
+            tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app"]
             print("      wave cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
     if s[:, 32:35].any():
