@@ -40,6 +40,9 @@ for r in range(3):
         if s[i, 24:30].any():
             tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app"]
             print("      wave cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
+            sec = s[i, 25] + s[i, 26] + s[i, 27] + s[i, 29]
+            print(f"      load={s[i, 32]} run={s[i, 33]} store={s[i, 34]} run-outside-handlers={s[i, 33] - sec}"
+                  f" iterations={s[i, 35]}")
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
     if s[:, 32:35].any():
         wl, wr, ws_ = s[:, 32], s[:, 33], s[:, 34]
