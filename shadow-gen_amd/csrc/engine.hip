@@ -212,6 +212,9 @@ struct Outbox {
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
 // pad every lane's slot to a multiple of 16 B and cost a workgroup per CU)
+// (copies between them and the 16-byte-aligned global entries are compiled as 8-byte LDS
+// pairs, ds_write2_b64 / ds_read2_b64; clang's align-mismatch note on them is expected)
+#pragma clang diagnostic ignored "-Walign-mismatch"
 typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
 typedef FifoEnt FifoEnt8 __attribute__((aligned(8)));
 struct LaneLDS {
@@ -1145,12 +1148,6 @@ struct HostExec {
   template <int W>
   __device__ __forceinline__ void run_forward_task() {
     set_relay_state<W>(RELAY_IDLE);
-    if (W == 0) {  // forward_out_step continues it in the next iterations
-      set_relay_state<0>(RELAY_FORWARDING);
-      fl |= F_RO_CONT;
-      forward_out_step();
-      return;
-    }
     uint64_t dur;
     DGT_BEGIN(t0);
     const bool blocked = forward_in(&dur);
@@ -1210,9 +1207,8 @@ struct HostExec {
   __device__ __forceinline__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
                       uint64_t until) {
     uint32_t pi = s0;
+    uint64_t pt = pi < s1 ? ev[ord[pi]].time : INVALID;  // next due packet run's time
 #ifdef SGN_DIAG
-    uint32_t it_mask = 99;
-    uint64_t it_t = 0;
 #endif
     while (true) {
       // earliest local event by (time, event id)
@@ -1238,18 +1234,16 @@ struct HostExec {
           // (per-combination cycles: off — a global read-modify-write per iteration would
           // add a dependent round trip to every iteration of the diag build)
         }
-        it_mask = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u) | (b3 ? 8u : 0u);
-        it_t = tnow;
+        (void)tnow;
       }
 #endif
-      if (fl & F_RO_CONT) {  // inside relay_inet_out's forwarding task (forward_out_step)
-        forward_out_step();
-        continue;
-      }
-      if (pi < s1) {
-        const EvRec& e = ev[ord[pi]];
-        if (e.time <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+      // inside relay_inet_out's forwarding task: its next step (the one call site of
+      // forward_out_step below), no other event of the host
+      if (!(fl & F_RO_CONT)) {
+        if (pi < s1 && pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
+          const EvRec& e = ev[ord[pi]];
           pi++;
+          pt = pi < s1 ? ev[ord[pi]].time : INVALID;  // the next run's time, ahead of need
           now = e.time;
           if (external() && e.src == gid) {  // a CPU application's datagram (sgn_submit)
             app_submit(e);
@@ -1273,25 +1267,27 @@ struct HostExec {
           DGT_END(DGT_POP, t0);
           continue;
         }
-      }
-      if (lt >= until) break;
-      now = lt;
-      c_localev++;
-      if (ls == 0) {
+        if (lt >= until) break;
+        now = lt;
+        c_localev++;
+        if (ls == 1) {
+          st1 = INVALID;
+          run_forward_task<1>();
+          continue;
+        }
+        if (ls == 2) {
+          st2 = INVALID;
+          DGT_BEGIN(t0);
+          app_task();
+          DGT_END(DGT_LOAD, t0);
+          continue;
+        }
+        // run_forward_task for relay_inet_out (relay/mod.rs:166-187): Idle, then Forwarding
         st0 = INVALID;
-        DG(DG_RO);
-        run_forward_task<0>();
-      } else if (ls == 1) {
-        st1 = INVALID;
-        DG(DG_RI);
-        run_forward_task<1>();
-      } else {
-        st2 = INVALID;
-        DG(DG_APP);
-        DGT_BEGIN(t0);
-        app_task();
-        DGT_END(DGT_LOAD, t0);
+        set_relay_state<0>(RELAY_FORWARDING);
+        fl |= F_RO_CONT;
       }
+      forward_out_step();
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
     sgn_drun_flush_same(&L->dig[0], &L->run[0]);
