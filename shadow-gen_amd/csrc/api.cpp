@@ -257,6 +257,7 @@ int sgn_route_get(sgn_ctx* ctx, uint32_t src, uint32_t dst, uint64_t* lat, float
     if (ctx->used_ids[i] == dst) di = (int)i;
   }
   if (si < 0 || di < 0) return SGN_ENOENT;
+  if (int rc = sgn::ensure_host_routes(ctx)) return rc;
   const size_t k = (size_t)si * ctx->U + di;
   if (lat) *lat = ctx->h_lat[k];
   if (loss) *loss = ctx->h_loss[k];
@@ -266,6 +267,7 @@ int sgn_route_get(sgn_ctx* ctx, uint32_t src, uint32_t dst, uint64_t* lat, float
 int sgn_routes_copy(sgn_ctx* ctx, uint64_t* lat, float* loss) {
   if (!ctx) return SGN_EINVAL;
   if (!ctx->routes_ready) return set_error(ctx, SGN_ESTATE, "no route table");
+  if (int rc = sgn::ensure_host_routes(ctx)) return rc;
   if (lat) std::memcpy(lat, ctx->h_lat.data(), ctx->h_lat.size() * 8);
   if (loss) std::memcpy(loss, ctx->h_loss.data(), ctx->h_loss.size() * 4);
   return 0;
@@ -274,7 +276,7 @@ int sgn_routes_copy(sgn_ctx* ctx, uint64_t* lat, float* loss) {
 int sgn_min_latency(sgn_ctx* ctx, uint64_t* out) {
   if (!ctx || !out) return SGN_EINVAL;
   if (!ctx->routes_ready) return set_error(ctx, SGN_ESTATE, "no route table");
-  *out = *std::min_element(ctx->h_lat.begin(), ctx->h_lat.end());
+  *out = ctx->lat_min;  // over every entry incl. self-loops (graph/mod.rs:472)
   return 0;
 }
 
@@ -295,6 +297,7 @@ static int route_index(sgn_ctx* ctx, uint32_t src_be, uint32_t dst_be, size_t* k
 uint64_t sgn_worker_get_latency(sgn_ctx* ctx, uint32_t src_be, uint32_t dst_be) {
   size_t k;
   if (!ctx || !ctx->hosts_ready || route_index(ctx, src_be, dst_be, &k)) return SGN_EMUTIME_INVALID;
+  if (sgn::ensure_host_routes(ctx)) return SGN_EMUTIME_INVALID;
   return ctx->h_lat[k];
 }
 

@@ -2213,11 +2213,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.period_jitter = tr->period_jitter_ns;
   for (int i = 0; i < 3; i++) S.file_bytes[i] = tr->file_bytes[i];
 
-  uint64_t min_possible = ~0ULL, max_lat = 0;
-  for (uint64_t v : ctx->h_lat) {
-    min_possible = std::min(min_possible, v);
-    max_lat = std::max(max_lat, v);
-  }
+  const uint64_t min_possible = ctx->lat_min, max_lat = ctx->lat_max;
   S.min_possible = min_possible;
   if (min_possible == 0) return set_error(ctx, SGN_EINVAL, "route latency 0 (Runahead::new asserts)");
 

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 
@@ -150,59 +151,145 @@ __global__ __launch_bounds__(256) void fw_phase3(uint64_t* D, uint32_t Vp, int k
       D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b] = c[a][b];
 }
 
-// Tight-arc loss fold, one workgroup per used source. LDS: D row (u64) + loss row (f32).
-__global__ __launch_bounds__(256) void loss_pass(const uint64_t* D, uint32_t Vp,
-                                                 const uint32_t* usrc, const uint32_t* au,
-                                                 const uint32_t* av, const uint64_t* al,
-                                                 const float* ap, uint32_t E2, float* Lout,
-                                                 uint32_t* iters) {
+// Tight-arc loss fold, one workgroup per used source. The arcs that are tight for the
+// source (d[s][u] + lat(u,v) == d[s][v]) are found in ONE sweep over the arc list and kept in
+// LDS (packed u | v << 16 and the arc's loss); the fixed point then iterates over that short
+// list only. A source with more tight arcs than the LDS list holds falls back to sweeping the
+// global arc list each iteration. The fixed point is the same in any order (min of an isotone
+// fold), so the LDS list order (atomic appends) does not matter.
+// LDS: D row (u64 x Vp), loss row (f32 x Vp), tight list (2 x u32 x cap), 3 counters.
+__global__ __launch_bounds__(512) void loss_pass(const uint64_t* D, uint32_t Vp,
+                                                 const uint32_t* usrc, const uint32_t* auv,
+                                                 const uint64_t* al, const float* ap, uint32_t E2,
+                                                 uint32_t cap, float* Lout, uint32_t* iters) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* Dr = (uint64_t*)smem;
   float* L = (float*)(Dr + Vp);
-  int& changed = *(int*)(L + Vp);  // in the dynamic region: no static LDS ahead of it
+  uint32_t* tuv = (uint32_t*)(L + Vp);
+  float* tp = (float*)(tuv + cap);
+  uint32_t* ctl = (uint32_t*)(tp + cap);  // [0] tight count, [1] changed
   const uint32_t s = usrc[blockIdx.x];
   for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) {
     Dr[v] = D[(uint64_t)s * Vp + v];
     L[v] = 2.0f;  // "no path yet": larger than any loss in [0, 1]
   }
+  if (threadIdx.x == 0) ctl[0] = 0;
   __syncthreads();
   if (threadIdx.x == 0) L[s] = 0.0f;  // the source's score is PathProperties::default()
+  // one sweep: the source's tight arcs into LDS. Four arcs per thread per step with 16-byte
+  // loads, two steps in flight: the sweep is bound by how many loads each thread keeps
+  // outstanding, not by bytes.
+  auto tight = [&](uint32_t uv, uint64_t l, uint32_t e) {
+    const uint64_t du = Dr[uv & 0xFFFFu];
+    if (du >= FW_INF || du + l != Dr[uv >> 16]) return;
+    const uint32_t k = atomicAdd(&ctl[0], 1u);
+    if (k < cap) {
+      tuv[k] = uv;
+      tp[k] = ap[e];
+    }
+  };
+  const uint32_t E4 = E2 / 4;
+  const uint4* auv4 = (const uint4*)auv;
+  const ulonglong2* al2 = (const ulonglong2*)al;
+  for (uint32_t q = threadIdx.x; q < E4; q += 2 * blockDim.x) {
+    const uint32_t q2 = q + blockDim.x;
+    const bool two = q2 < E4;
+    const uint4 a = auv4[q];
+    const ulonglong2 l0 = al2[2 * q], l1 = al2[2 * q + 1];
+    uint4 b = make_uint4(0, 0, 0, 0);
+    ulonglong2 m0 = make_ulonglong2(0, 0), m1 = make_ulonglong2(0, 0);
+    if (two) {
+      b = auv4[q2];
+      m0 = al2[2 * q2];
+      m1 = al2[2 * q2 + 1];
+    }
+    tight(a.x, l0.x, 4 * q);
+    tight(a.y, l0.y, 4 * q + 1);
+    tight(a.z, l1.x, 4 * q + 2);
+    tight(a.w, l1.y, 4 * q + 3);
+    if (two) {
+      tight(b.x, m0.x, 4 * q2);
+      tight(b.y, m0.y, 4 * q2 + 1);
+      tight(b.z, m1.x, 4 * q2 + 2);
+      tight(b.w, m1.y, 4 * q2 + 3);
+    }
+  }
+  for (uint32_t e = 4 * E4 + threadIdx.x; e < E2; e += blockDim.x) tight(auv[e], al[e], e);
+  __syncthreads();
+  const uint32_t nt = ctl[0];
+  const bool in_lds = nt <= cap;
   uint32_t it = 0;
   while (true) {
     __syncthreads();
-    if (threadIdx.x == 0) changed = 0;
+    if (threadIdx.x == 0) ctl[1] = 0;
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < E2; e += blockDim.x) {
-      const uint32_t u = au[e];
-      const uint64_t du = Dr[u];
-      if (du >= FW_INF) continue;
-      const uint32_t v = av[e];
-      if (du + al[e] != Dr[v]) continue;  // not on a shortest-latency path
-      const float lu = L[u];
+    const uint32_t n = in_lds ? nt : E2;
+    for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+      uint32_t uv;
+      float pe;
+      if (in_lds) {
+        uv = tuv[e];
+        pe = tp[e];
+      } else {
+        uv = auv[e];
+        const uint64_t du = Dr[uv & 0xFFFFu];
+        if (du >= FW_INF || du + al[e] != Dr[uv >> 16]) continue;
+        pe = ap[e];
+      }
+      const float lu = L[uv & 0xFFFFu];
       if (lu > 1.0f) continue;
-      const float cand = __fsub_rn(1.0f, __fmul_rn(__fsub_rn(1.0f, lu), __fsub_rn(1.0f, ap[e])));
+      const float cand = __fsub_rn(1.0f, __fmul_rn(__fsub_rn(1.0f, lu), __fsub_rn(1.0f, pe)));
       const uint32_t cb = __float_as_uint(cand);
-      if (cb < __float_as_uint(L[v])) {
-        const uint32_t old = atomicMin((unsigned int*)&L[v], cb);
-        if (cb < old) changed = 1;
+      float* lv = &L[uv >> 16];
+      if (cb < __float_as_uint(*lv)) {
+        const uint32_t old = atomicMin((unsigned int*)lv, cb);
+        if (cb < old) ctl[1] = 1;
       }
     }
     __syncthreads();
     it++;
-    if (!changed) break;
+    if (!ctl[1]) break;
   }
   for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) Lout[(uint64_t)blockIdx.x * Vp + v] = L[v];
-  if (threadIdx.x == 0) iters[blockIdx.x] = it;
+  if (threadIdx.x == 0) iters[blockIdx.x] = it | (in_lds ? 0u : 0x80000000u);
 }
 
+// The U x U table straight into the engine's device buffers: latency from D, loss from the
+// loss rows, each used node's (n,n) entry replaced by its single self-loop edge
+// (graph/mod.rs:209-215); res = {first disconnected pair index, min latency, max latency}.
 __global__ void extract(const uint64_t* D, uint32_t Vp, const float* Lrows, const uint32_t* uidx,
-                        uint32_t U, uint64_t* lat, float* loss) {
+                        uint32_t U, const uint64_t* self_lat, const float* self_loss,
+                        uint64_t* lat, float* loss, unsigned long long* res) {
   const uint64_t n = (uint64_t)U * U;
+  uint64_t mn = ~0ULL, mx = 0, bad = ~0ULL;
   for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n;
        x += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t i = (uint32_t)(x / U), j = (uint32_t)(x % U);
-    lat[x] = D[(uint64_t)uidx[i] * Vp + uidx[j]];
-    loss[x] = Lrows[(uint64_t)i * Vp + uidx[j]];
+    uint64_t l;
+    float p;
+    if (i == j) {
+      l = self_lat[i];
+      p = self_loss[i];
+    } else {
+      l = D[(uint64_t)uidx[i] * Vp + uidx[j]];
+      p = Lrows[(uint64_t)i * Vp + uidx[j]];
+      if (l >= FW_INF && x < bad) bad = x;
+    }
+    lat[x] = l;
+    loss[x] = p;
+    mn = l < mn ? l : mn;
+    mx = l > mx ? l : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64), c = __shfl_xor(bad, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+    bad = c < bad ? c : bad;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bad != ~0ULL) atomicMin(&res[0], (unsigned long long)bad);
+    atomicMin(&res[1], (unsigned long long)mn);
+    atomicMax(&res[2], (unsigned long long)mx);
   }
 }
 
@@ -227,6 +314,19 @@ int upload(sgn_ctx* ctx, DevBuf& b, const T* src, size_t n) {
 }
 
 }  // namespace
+
+// The host mirror of the device table, copied on first use by a CPU-side consumer
+// (sgn_route_get, sgn_routes_copy, worker_getLatency); the engine never needs it.
+int sgn::ensure_host_routes(sgn_ctx* ctx) {
+  if (ctx->h_routes) return 0;
+  const size_t n = (size_t)ctx->U * ctx->U;
+  ctx->h_lat.resize(n);
+  ctx->h_loss.resize(n);
+  SGN_HIP(ctx, hipMemcpy(ctx->h_lat.data(), ctx->d_lat, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemcpy(ctx->h_loss.data(), ctx->d_loss, n * 4, hipMemcpyDeviceToHost));
+  ctx->h_routes = true;
+  return 0;
+}
 
 extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t* used,
                                 uint32_t U, int32_t use_shortest_path) {
@@ -280,8 +380,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     return std::string(c == 0 ? "No edge connecting node " : "More than one edge connecting node ") +
            std::to_string(g->node_id[a]) + " to " + std::to_string(g->node_id[b]);
   };
-  std::vector<uint64_t> lat((size_t)U * U);
-  std::vector<float> loss((size_t)U * U);
+  std::vector<uint64_t> lat;  // direct paths only (the shortest-path table stays on the device)
+  std::vector<float> loss;
   hipEvent_t e0, e1, e2, e3;
   SGN_HIP(ctx, hipEventCreate(&e0));
   SGN_HIP(ctx, hipEventCreate(&e1));
@@ -298,6 +398,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
   sgn_routes_timing tm{};
   tm.tile = FW_T;
   if (!use_shortest_path) {
+    lat.resize((size_t)U * U);
+    loss.resize((size_t)U * U);
     for (uint32_t i = 0; i < U; i++)
       for (uint32_t j = 0; j < U; j++) {
         auto it = pairs.find(key(uidx[i], uidx[j]));
@@ -316,31 +418,52 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     const size_t lds = (size_t)Vp * 12 + 16;
     if (lds > 160 * 1024)
       return set_error(ctx, SGN_ERANGE, "graph too large for the LDS loss pass (V > 13632)");
-    // directed arcs (undirected edges both ways), self-loops excluded
-    std::vector<uint32_t> au, av;
+    // directed arcs (undirected edges both ways), self-loops excluded; u | v << 16 packed
+    // (V <= 13632 here: the LDS bound above)
+    std::vector<uint32_t> auv;
     std::vector<uint64_t> al;
     std::vector<float> ap;
-    au.reserve(2 * (size_t)E);
+    auv.reserve(2 * (size_t)E);
     for (uint32_t k = 0; k < E; k++) {
       if (es[k] == ed[k]) continue;
-      au.push_back(es[k]); av.push_back(ed[k]); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
+      auv.push_back(es[k] | (ed[k] << 16)); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
       if (!g->directed) {
-        au.push_back(ed[k]); av.push_back(es[k]); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
+        auv.push_back(ed[k] | (es[k] << 16)); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
       }
     }
-    const uint32_t E2 = (uint32_t)au.size();
-    DevBuf dD, deu, dev, del, dau, dav, dal, dap, dus, dL, dit, dlat, dloss;
+    const uint32_t E2 = (uint32_t)auv.size();
+    std::vector<uint64_t> sl(U);
+    std::vector<float> sp(U);
+    for (uint32_t i = 0; i < U; i++) {
+      sl[i] = g->edge_latency_ns[self_edge[uidx[i]]];
+      sp[i] = g->edge_loss[self_edge[uidx[i]]];
+    }
+    // tight-arc list capacity: 4 per node (a source's tight arcs are its shortest-path DAG:
+    // about one per node plus ties), at least 4 k, within what LDS holds next to the rows
+    const uint32_t cap = (uint32_t)std::min<size_t>(std::max<size_t>(4096, 4 * (size_t)Vp),
+                                                    (160 * 1024 - lds - 16) / 8);
+    const size_t lds2 = lds + (size_t)cap * 8 + 16;
+    DevBuf dD, deu, dev, del, dauv, dal, dap, dus, dL, dit, dsl, dsp, dres;
     int rc;
     if ((rc = upload(ctx, deu, es.data(), E)) || (rc = upload(ctx, dev, ed.data(), E)) ||
-        (rc = upload(ctx, del, g->edge_latency_ns, E)) || (rc = upload(ctx, dau, au.data(), E2)) ||
-        (rc = upload(ctx, dav, av.data(), E2)) || (rc = upload(ctx, dal, al.data(), E2)) ||
-        (rc = upload(ctx, dap, ap.data(), E2)) || (rc = upload(ctx, dus, uidx.data(), U)))
+        (rc = upload(ctx, del, g->edge_latency_ns, E)) || (rc = upload(ctx, dauv, auv.data(), E2)) ||
+        (rc = upload(ctx, dal, al.data(), E2)) || (rc = upload(ctx, dap, ap.data(), E2)) ||
+        (rc = upload(ctx, dus, uidx.data(), U)) || (rc = upload(ctx, dsl, sl.data(), U)) ||
+        (rc = upload(ctx, dsp, sp.data(), U)))
       return rc;
+    const unsigned long long res0[3] = {~0ULL, ~0ULL, 0ULL};
+    if ((rc = upload(ctx, dres, res0, 3))) return rc;
     SGN_HIP(ctx, hipMalloc(&dD.p, (size_t)Vp * Vp * 8));
     SGN_HIP(ctx, hipMalloc(&dL.p, (size_t)U * Vp * 4));
     SGN_HIP(ctx, hipMalloc(&dit.p, (size_t)U * 4));
-    SGN_HIP(ctx, hipMalloc(&dlat.p, (size_t)U * U * 8));
-    SGN_HIP(ctx, hipMalloc(&dloss.p, (size_t)U * U * 4));
+    // the engine's table (replaces any previous one)
+    if (ctx->d_lat) hipFree(ctx->d_lat);
+    if (ctx->d_loss) hipFree(ctx->d_loss);
+    ctx->d_lat = nullptr;
+    ctx->d_loss = nullptr;
+    ctx->routes_ready = false;
+    SGN_HIP(ctx, hipMalloc(&ctx->d_lat, (size_t)U * U * 8));
+    SGN_HIP(ctx, hipMalloc(&ctx->d_loss, (size_t)U * U * 4));
     hipStream_t st = ctx->stream;
     uint64_t* D = (uint64_t*)dD.p;
     SGN_HIP(ctx, hipEventRecord(e0, st));
@@ -357,19 +480,20 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipEventRecord(e1, st));
-    hipLaunchKernelGGL(loss_pass, dim3(U), dim3(256), lds, st, D, Vp, (const uint32_t*)dus.p,
-                       (const uint32_t*)dau.p, (const uint32_t*)dav.p, (const uint64_t*)dal.p,
-                       (const float*)dap.p, E2, (float*)dL.p, (uint32_t*)dit.p);
+    hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
+                       (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
+                       (float*)dL.p, (uint32_t*)dit.p);
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipEventRecord(e2, st));
     hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
-                       (const uint32_t*)dus.p, U, (uint64_t*)dlat.p, (float*)dloss.p);
+                       (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p, (const float*)dsp.p,
+                       ctx->d_lat, ctx->d_loss, (unsigned long long*)dres.p);
     SGN_HIP(ctx, hipGetLastError());
-    SGN_HIP(ctx, hipMemcpyAsync(lat.data(), dlat.p, (size_t)U * U * 8, hipMemcpyDeviceToHost, st));
-    SGN_HIP(ctx, hipMemcpyAsync(loss.data(), dloss.p, (size_t)U * U * 4, hipMemcpyDeviceToHost, st));
+    unsigned long long res[3];
+    SGN_HIP(ctx, hipMemcpyAsync(res, dres.p, sizeof(res), hipMemcpyDeviceToHost, st));
+    SGN_HIP(ctx, hipEventRecord(e3, st));
     std::vector<uint32_t> its(U);
     SGN_HIP(ctx, hipMemcpyAsync(its.data(), dit.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
-    SGN_HIP(ctx, hipEventRecord(e3, st));
     SGN_HIP(ctx, hipStreamSynchronize(st));
     float ms_fw = 0, ms_loss = 0, ms_total = 0;
     hipEventElapsedTime(&ms_fw, e0, e1);
@@ -378,21 +502,37 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     tm.latency_ms = ms_fw;
     tm.loss_ms = ms_loss;
     tm.total_ms = ms_total;
-    tm.loss_iters = its.empty() ? 0 : *std::max_element(its.begin(), its.end());
-    tm.n_tight_edges = E2;
-    for (uint32_t i = 0; i < U; i++)
-      for (uint32_t j = 0; j < U; j++)
-        if (lat[(size_t)i * U + j] >= FW_INF)
-          return set_error(ctx, SGN_EINVAL, "used nodes " + std::to_string(used[i]) + " -> " +
-                                                std::to_string(used[j]) + " are not connected");
-    // the single self-loop replaces the zero-length path (graph/mod.rs:209-215)
-    for (uint32_t i = 0; i < U; i++) {
-      const uint32_t k = self_edge[uidx[i]];
-      lat[(size_t)i * U + i] = g->edge_latency_ns[k];
-      loss[(size_t)i * U + i] = g->edge_loss[k];
+    uint32_t mi = 0, n_global = 0;
+    for (uint32_t v : its) {
+      mi = std::max(mi, v & 0x7FFFFFFFu);
+      n_global += v >> 31;
     }
+    tm.loss_iters = mi;
+    tm.n_tight_edges = E2;
+    if (n_global)
+      fprintf(stderr, "libsgn: %u sources had more tight arcs than the LDS list (%u): global sweeps\n",
+              n_global, cap);
+    if (res[0] != ~0ULL) {
+      const uint64_t i = res[0] / U, j = res[0] % U;
+      return set_error(ctx, SGN_EINVAL, "used nodes " + std::to_string(used[i]) + " -> " +
+                                            std::to_string(used[j]) + " are not connected");
+    }
+    ctx->lat_min = res[1];
+    ctx->lat_max = res[2];
+    ctx->h_lat.clear();
+    ctx->h_loss.clear();
+    ctx->h_routes = false;  // host mirror made on demand (sgn_route_get & co.)
+    ctx->U = U;
+    ctx->used_ids.assign(used, used + U);
+    ctx->rt_timing = tm;
+    ctx->routes_ready = true;
+    ctx->hosts_ready = false;  // hosts map onto used nodes: re-register
+    return 0;
   }
-  // device copy for the engine
+  // direct paths (use_shortest_path: false): the host table, uploaded for the engine
+  ctx->lat_min = *std::min_element(lat.begin(), lat.end());
+  ctx->lat_max = *std::max_element(lat.begin(), lat.end());
+  ctx->h_routes = true;
   if (ctx->d_lat) hipFree(ctx->d_lat);
   if (ctx->d_loss) hipFree(ctx->d_loss);
   ctx->d_lat = nullptr;

@@ -304,6 +304,8 @@ struct sgn_ctx {
   std::vector<uint32_t> used_ids;
   std::vector<uint64_t> h_lat;  // host copy of the table (CPU-side consumers)
   std::vector<float> h_loss;
+  uint64_t lat_min = 0, lat_max = 0;  // over the U x U table (Runahead seed, calendar size)
+  bool h_routes = false;               // h_lat / h_loss hold the table (ensure_host_routes)
   uint64_t* d_lat = nullptr;
   float* d_loss = nullptr;
   sgn_routes_timing rt_timing{};
@@ -367,6 +369,7 @@ int set_error(sgn_ctx* ctx, int code, const std::string& msg);
 int hip_fail(sgn_ctx* ctx, hipError_t e, const char* what);
 void* dev_alloc(sgn_ctx* ctx, size_t bytes, bool zero = true);
 void free_sim(sgn_ctx* ctx);
+int ensure_host_routes(sgn_ctx* ctx);
 // timing helpers around a launch
 void time_begin(sgn_ctx* ctx, int kernel);
 void time_end(sgn_ctx* ctx);
