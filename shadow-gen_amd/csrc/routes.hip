@@ -58,57 +58,91 @@ __global__ void fw_edges(uint64_t* D, uint32_t Vp, const uint32_t* eu, const uin
       dst[ty + 16 * a][tx + 16 * b] =                                              \
           D[(uint64_t)((bi) * FW_T + ty + 16 * a) * Vp + (bj) * FW_T + tx + 16 * b];
 
-__global__ __launch_bounds__(256) void fw_phase1(uint64_t* D, uint32_t Vp, int kb) {
-  __shared__ uint64_t P[FW_T][FW_T + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  FW_LOAD_TILE(P, kb, kb);
-  __syncthreads();
+// The dependent tiles (pivot, panels) run as 1024-thread workgroups, 2x2 entries per thread
+// in registers (thread (ty, tx) of 32x32 owns rows ty + 32a, columns tx + 32b): at step k the
+// owners of the tile's row k / column k publish them to a double-buffered LDS row / column
+// (one barrier per step) and every thread updates its entries from the published values.
+// Row k and column k do not change at step k (the pivot's diagonal is 0), so the published
+// values are exactly those the in-place algorithm would read. 16 waves per workgroup keep
+// the SIMDs busy through each step's dependent chain.
+__global__ __launch_bounds__(1024) void fw_phase1(uint64_t* D, uint32_t Vp, int kb) {
+  __shared__ uint64_t rowb[2][FW_T], colb[2][FW_T];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  uint64_t c[2][2];
+  for (int a = 0; a < 2; a++)
+    for (int b = 0; b < 2; b++)
+      c[a][b] = D[(uint64_t)(kb * FW_T + ty + 32 * a) * Vp + kb * FW_T + tx + 32 * b];
   for (int k = 0; k < FW_T; k++) {
-    for (int a = 0; a < 4; a++) {
-      const uint64_t pik = P[ty + 16 * a][k];
-      for (int b = 0; b < 4; b++) {
-        const uint64_t s = pik + P[k][tx + 16 * b];
-        uint64_t& c = P[ty + 16 * a][tx + 16 * b];
-        c = s < c ? s : c;
-      }
-    }
+    const int h = k & 1;
+    if (ty == (k & 31))
+#pragma unroll
+      for (int b = 0; b < 2; b++) rowb[h][tx + 32 * b] = c[k >> 5][b];
+    if (tx == (k & 31))
+#pragma unroll
+      for (int a = 0; a < 2; a++) colb[h][ty + 32 * a] = c[a][k >> 5];
     __syncthreads();
+    const uint64_t u0 = rowb[h][tx], u1 = rowb[h][tx + 32];
+    const uint64_t l0 = colb[h][ty], l1 = colb[h][ty + 32];
+    c[0][0] = min(c[0][0], l0 + u0);
+    c[0][1] = min(c[0][1], l0 + u1);
+    c[1][0] = min(c[1][0], l1 + u0);
+    c[1][1] = min(c[1][1], l1 + u1);
   }
-  for (int a = 0; a < 4; a++)
-    for (int b = 0; b < 4; b++)
-      D[(uint64_t)(kb * FW_T + ty + 16 * a) * Vp + kb * FW_T + tx + 16 * b] =
-          P[ty + 16 * a][tx + 16 * b];
+  for (int a = 0; a < 2; a++)
+    for (int b = 0; b < 2; b++)
+      D[(uint64_t)(kb * FW_T + ty + 32 * a) * Vp + kb * FW_T + tx + 32 * b] = c[a][b];
 }
 
 // row panel (kb, j) and column panel (i, kb) against the finished pivot tile
-__global__ __launch_bounds__(256) void fw_phase2(uint64_t* D, uint32_t Vp, int kb, int nb) {
+// ROW: C[i][j] = min(C, P[i][k] + C[k][j]) publishes its row k each step;
+// column: C[i][j] = min(C, C[i][k] + P[k][j]) publishes its column k
+template <bool ROW>
+__device__ __forceinline__ void fw_panel(uint64_t (&c)[2][2], uint64_t (*P)[FW_T + 1],
+                                         uint64_t (*pub)[FW_T], int tx, int ty) {
+  for (int k = 0; k < FW_T; k++) {
+    const int h = k & 1;
+    if (ROW) {
+      if (ty == (k & 31))
+#pragma unroll
+        for (int b = 0; b < 2; b++) pub[h][tx + 32 * b] = c[k >> 5][b];
+    } else if (tx == (k & 31)) {
+#pragma unroll
+      for (int a = 0; a < 2; a++) pub[h][ty + 32 * a] = c[a][k >> 5];
+    }
+    __syncthreads();
+    const uint64_t u0 = ROW ? pub[h][tx] : P[k][tx], u1 = ROW ? pub[h][tx + 32] : P[k][tx + 32];
+    const uint64_t l0 = ROW ? P[ty][k] : pub[h][ty], l1 = ROW ? P[ty + 32][k] : pub[h][ty + 32];
+    c[0][0] = min(c[0][0], l0 + u0);
+    c[0][1] = min(c[0][1], l0 + u1);
+    c[1][0] = min(c[1][0], l1 + u0);
+    c[1][1] = min(c[1][1], l1 + u1);
+  }
+}
+
+__global__ __launch_bounds__(1024) void fw_phase2(uint64_t* D, uint32_t Vp, int kb, int nb) {
   __shared__ uint64_t P[FW_T][FW_T + 1];
-  __shared__ uint64_t Q[FW_T][FW_T + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  __shared__ uint64_t pub[2][FW_T];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   int idx = blockIdx.x;
   const bool row = idx < nb - 1;
   if (!row) idx -= nb - 1;
   const int other = idx < kb ? idx : idx + 1;
   const int bi = row ? kb : other, bj = row ? other : kb;
-  FW_LOAD_TILE(P, kb, kb);
-  FW_LOAD_TILE(Q, bi, bj);
+  for (int a = 0; a < 2; a++)
+    for (int b = 0; b < 2; b++)
+      P[ty + 32 * a][tx + 32 * b] = D[(uint64_t)(kb * FW_T + ty + 32 * a) * Vp + kb * FW_T + tx + 32 * b];
+  uint64_t c[2][2];
+  for (int a = 0; a < 2; a++)
+    for (int b = 0; b < 2; b++)
+      c[a][b] = D[(uint64_t)(bi * FW_T + ty + 32 * a) * Vp + bj * FW_T + tx + 32 * b];
   __syncthreads();
-  for (int k = 0; k < FW_T; k++) {
-    for (int a = 0; a < 4; a++) {
-      const uint64_t left = row ? P[ty + 16 * a][k] : Q[ty + 16 * a][k];
-      for (int b = 0; b < 4; b++) {
-        const uint64_t up = row ? Q[k][tx + 16 * b] : P[k][tx + 16 * b];
-        const uint64_t s = left + up;
-        uint64_t& c = Q[ty + 16 * a][tx + 16 * b];
-        c = s < c ? s : c;
-      }
-    }
-    __syncthreads();
-  }
-  for (int a = 0; a < 4; a++)
-    for (int b = 0; b < 4; b++)
-      D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b] =
-          Q[ty + 16 * a][tx + 16 * b];
+  if (row)
+    fw_panel<true>(c, P, pub, tx, ty);
+  else
+    fw_panel<false>(c, P, pub, tx, ty);
+  for (int a = 0; a < 2; a++)
+    for (int b = 0; b < 2; b++)
+      D[(uint64_t)(bi * FW_T + ty + 32 * a) * Vp + bj * FW_T + tx + 32 * b] = c[a][b];
 }
 
 // all remaining tiles: C = min(C, A (bi,kb) (+) B (kb,bj)), k order irrelevant
@@ -472,9 +506,9 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
                        D, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
                        (int)g->directed);
     for (uint32_t kb = 0; kb < nb; kb++) {
-      hipLaunchKernelGGL(fw_phase1, dim3(1), dim3(256), 0, st, D, Vp, (int)kb);
+      hipLaunchKernelGGL(fw_phase1, dim3(1), dim3(1024), 0, st, D, Vp, (int)kb);
       if (nb > 1) {
-        hipLaunchKernelGGL(fw_phase2, dim3(2 * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
+        hipLaunchKernelGGL(fw_phase2, dim3(2 * (nb - 1)), dim3(1024), 0, st, D, Vp, (int)kb, (int)nb);
         hipLaunchKernelGGL(fw_phase3, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
       }
     }
