@@ -65,7 +65,9 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, budget_s):
     import oracle_py
 
     threads = max(1, min(16, os.cpu_count() or 1))
-    lat, loss = oracle_py.routes(g, used)
+    t_apsp = time.perf_counter()
+    lat, loss = oracle_py.routes(g, used)  # per-source Dijkstra (graph/mod.rs:181-226), 1 thread
+    apsp_s = time.perf_counter() - t_apsp
     sim = oracle_py.Sim(used, lat, loss, hosts, cfg, tr, threads=threads)
     sim.run(args.warmup * args.rounds_per_step)
 
@@ -90,6 +92,8 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, budget_s):
                   f"workload and the same rounds the GPU timed (rounds "
                   f"{args.warmup * args.rounds_per_step}..{args.warmup * args.rounds_per_step + rounds}"
                   f", {ev} packet events, {el:.1f} s wall; warm-up rounds untimed)",
+        "apsp_ms": round(apsp_s * 1e3, 1),
+        "apsp_sample": "the oracle's per-source Dijkstra over the same graph (1 thread)",
         "single_core": {"value": ev1 / el1, "cores": 1,
                         "sample": f"the next {rounds1} rounds on 1 thread ({ev1} packet events, {el1:.1f} s)"},
     }
