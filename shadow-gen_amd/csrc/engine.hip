@@ -1468,8 +1468,13 @@ struct ExecLDS {
 //  3. execute: every lane runs Host::execute (host.rs:762-830) for its host over its
 //     segment and local slots, emitting new runs into the calendar / exchange slots;
 //  4. the group's minimum kept-event time and next local event time are returned.
+// at_end(kmin, next) runs once the group's cross-workgroup data (calendar records, slab
+// fills, minima) is issued and before the host records are written back: the round's
+// arrival goes there, so its wait covers only what other workgroups read.
+template <typename AtEnd>
 __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
-                           const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out) {
+                           const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out,
+                           AtEnd&& at_end) {
   SGN_GLB Ctrl* C = S.ctrl;
   EvRec* lev = X.lev;
   uint16_t* lb = X.lb;
@@ -1631,12 +1636,21 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     }
   }
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
+  if (loaded) my_min = ex.next_local_time();
+  kmin = wave_min_u64(kmin);
+  const uint64_t m = wave_min_u64(my_min);
+  *kmin_out = kmin;
+  *next_out = m;
+  if (lane == 0) {
+    S.w_keep[g] = kmin;
+    S.w_next[g] = m;
+  }
+  at_end(kmin, m);
   uint32_t n_ev = 0;
 #ifdef SGN_DIAG
   const uint64_t td = __builtin_amdgcn_s_memtime();
 #endif
   if (loaded) {
-    my_min = ex.next_local_time();
     ex.store();
     n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_deliv + ex.c_localev;
   }
@@ -1644,7 +1658,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   const uint64_t w_store = __builtin_amdgcn_s_memtime() - td;
 #endif
-  kmin = wave_min_u64(kmin);
   if (S.stamps) {
     // per-wave diagnostics: shader cycles, total and max events over the wave's lanes
     const uint64_t clk1 = __builtin_amdgcn_s_memtime();
@@ -1668,18 +1681,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       st[30] = __builtin_amdgcn_s_memrealtime();
     }
 #ifdef SGN_DIAG
-    // the busiest lane's work counts (words 8..15) and the wave's sums (16..23)
-    const uint64_t bm = __ballot(loaded && n_ev == mx);
-    const int bl = bm ? __ffsll((long long)bm) - 1 : 0;
-    for (int i = 0; i < DG_N; i++) {
-      const uint32_t v = 0u;  // (per-lane work counts disabled)
-      const uint32_t vb = __shfl(v, bl, 64);
-      const uint32_t vs = wave_sum_u32(v);
-      if (lane == 0) {
-        st[8 + i] = vb;
-        st[16 + i] = vs;
-      }
-    }
     for (int i = 0; i < DGT_N; i++) {
       const uint32_t v = loaded ? ex.dgt[i] : 0u;
       const uint32_t vs = wave_sum_u32(v);  // the wave's time in section i
@@ -1696,28 +1697,22 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     }
 #endif
   }
-  // ---- 4. hosts that ran (roofline accounting) and the group's next event ----
+  // ---- 4. hosts that ran (roofline accounting): per-wave counters, no-return adds ----
   const uint64_t ex_mask = __ballot(loaded);
   const uint32_t n_sorted = wave_sum_u32(sorted);
-  const uint64_t m = wave_min_u64(my_min);
-  *kmin_out = kmin;
-  *next_out = m;
-  // counters only ever summed over hosts: accumulated per wave
   const uint32_t w_loss = wave_sum_u32(loaded ? ex.c_loss : 0u);
   const uint32_t w_lev = wave_sum_u32(loaded ? ex.c_localev : 0u);
   uint64_t w_bytes = loaded ? ex.c_bytes : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) w_bytes += shfl_xor64(w_bytes, off);
   if (lane == 0) {
-    S.w_keep[g] = kmin;
-    S.w_next[g] = m;
     const size_t G = S.G;
-    if (ex_mask) S.w_cnt[W_EXEC * G + g] += (uint64_t)__popcll(ex_mask);
-    if (N_all) S.w_cnt[W_RUNS * G + g] += N_all;
-    if (n_sorted) S.w_cnt[W_SORTED * G + g] += n_sorted;
-    if (w_loss) S.w_cnt[W_LOSS * G + g] += w_loss;
-    if (w_lev) S.w_cnt[W_LOCAL_EV * G + g] += w_lev;
-    if (w_bytes) S.w_cnt[W_BYTES * G + g] += w_bytes;
+    if (ex_mask) cnt_add(&S.w_cnt[W_EXEC * G + g], (uint64_t)__popcll(ex_mask));
+    if (N_all) cnt_add(&S.w_cnt[W_RUNS * G + g], N_all);
+    if (n_sorted) cnt_add(&S.w_cnt[W_SORTED * G + g], n_sorted);
+    if (w_loss) cnt_add(&S.w_cnt[W_LOSS * G + g], w_loss);
+    if (w_lev) cnt_add(&S.w_cnt[W_LOCAL_EV * G + g], w_lev);
+    if (w_bytes) cnt_add(&S.w_cnt[W_BYTES * G + g], w_bytes);
   }
 }
 
@@ -1782,9 +1777,11 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = S.bucket_slab[i];
   __syncthreads();
   uint64_t kmin, m;
-  exec_group(S, blockIdx.x, ws, we, ks, X, &kmin, &m);
-  if (!S.fuse_finalize) return;
-  if (!arrive(S, blockIdx.x, gridDim.x, kmin, m)) return;
+  bool last = false;
+  exec_group(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+    if (S.fuse_finalize) last = arrive(S, blockIdx.x, gridDim.x, k, n);
+  });
+  if (!last) return;
   const uint32_t b1 = bucket_of(S, we - 1);
   finalize_fused(S, threadIdx.x, (gridDim.x + 63) >> 6, ws, we, ks,
                  S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]));
@@ -1820,19 +1817,25 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       __hip_atomic_fetch_min(rd, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t kall = INVALID, mall = INVALID;
+    bool last = false;
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
-      exec_group(S, g, ws, we, ks, X, &kmin, &m);
-      kall = kmin < kall ? kmin : kall;
-      mall = m < mall ? m : mall;
+      const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
+      exec_group(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+        kall = k < kall ? k : kall;
+        mall = n < mall ? n : mall;
+        if (lastg) {
+          if (rd && threadIdx.x == 0)
+            __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = arrive(S, w, P, kall, mall);
+        }
+      });
       __syncthreads();
     }
     const uint32_t b1 = bucket_of(S, we - 1);
     const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
-    if (rd && threadIdx.x == 0)
-      __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrive(S, w, P, kall, mall)) {
+    if (last) {
       finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks, slab_b1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) {
