@@ -2415,6 +2415,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       const int lds_occ = (int)((160u * 1024u) / lds_wg);
       occ = std::min(occ, lds_occ);
       ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, (uint64_t)occ * (uint64_t)ncu);
+      // test hook: a smaller grid makes every workgroup serve several groups per round
+      if (const char* e = getenv("SGN_PERSIST_GRID"))
+        ctx->persist_grid = std::max<uint32_t>(1, std::min<uint32_t>(ctx->persist_grid, (uint32_t)atoi(e)));
     }
   }
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);

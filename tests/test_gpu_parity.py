@@ -218,6 +218,19 @@ def test_engine_large_digests(ctxf, oracle):
     assert_same_run(o, c, n, trace=False)
 
 
+@pytest.mark.parametrize("grid", [1, 7])
+def test_persistent_grid_smaller_than_groups(ctxf, oracle, monkeypatch, grid):
+    # every workgroup of the persistent round kernel serves several host groups per round
+    # (as at 1 M hosts, where the groups outnumber the resident workgroups)
+    monkeypatch.setenv("SGN_PERSIST_GRID", str(grid))
+    n = 2000
+    args = scenario(n=n, V=100, kind=sgn.TRAFFIC_TGEN, stop_ns=400_000_000, tor=True,
+                    bw=np.where(np.arange(n) % 10 == 0, 100_000_000, 10_000_000).astype(np.uint64))
+    o, c = run_both(ctxf, oracle, args, trace=False)
+    assert c.stats()["packets_sent"] > 1000
+    assert_same_run(o, c, n, trace=False)
+
+
 def test_worker_exports(ctxf, oracle):
     g, used, hosts, cfg, tr = scenario(n=20, V=10)
     c = ctxf()
