@@ -1522,35 +1522,49 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
     const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
-    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
+    // the slab's fill and its first 64 records in ONE round trip: the records are loaded
+    // before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
+    // appends to a bucket's slab while its window runs (new runs for the window's last
+    // bucket go to the spare slab set)
     SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
+    EvRec r0 = ld_dev_rec(pb + lane);
+    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
     lcnt[lane] = 0;
     uint32_t N = 0;
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
       const uint32_t j = j0 + lane;
-      EvRec r;
-      if (j < n) r = ld_dev_rec(pb + j);
+      EvRec r = r0;
+      if (j0 > 0 && j < n) r = ld_dev_rec(pb + j);
       const bool due = j < n && (!last || r.time < we);
       const bool keep = j < n && !due;
       const uint64_t dm = __ballot(due), km = __ballot(keep);
       if (due) lev[N + lanes_below(dm)] = r;
       N += (uint32_t)__popcll(dm);
       if (km) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&S.slab_n[ik], (uint32_t)__popcll(km));
-        base = __shfl(base, 0, 64) + lanes_below(km);
+        // the last bucket's later runs move to the spare slab set: through the outbox
+        // (placed with the sends after the event loop), or at once when it is full
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&ob->n, (uint32_t)__popcll(km));
+        k = __shfl(k, 0, 64) + lanes_below(km);
         if (keep) {
-          if (base < S.CAP)
-            st_dev_rec(pk + base, r);
-          else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-            C->overflow_info = r.dst;
           kmin = r.time < kmin ? r.time : kmin;
+          if (k < OBOX) {
+            ob->rec[k] = r;
+            ob->idx[k] = (uint32_t)ik;
+          } else {
+            const uint32_t base = atomicAdd(&S.slab_n[ik], 1u);
+            if (base < S.CAP)
+              st_dev_rec(pk + base, r);
+            else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+              C->overflow_info = r.dst;
+          }
         }
       }
     }
     if (lane == 0) {
       st_dev(&S.slab_n[ib], 0u);  // consumed (or moved); nobody appends to it this round
-      if (n > ld_dev(&C->max_bucket)) atomicMax((unsigned long long*)&C->max_bucket, (unsigned long long)n);
+      if (n) __hip_atomic_fetch_max(&S.w_cnt[W_MAXFILL * S.G + g], (uint64_t)n, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
     }
     N_all += N;
     __syncthreads();
@@ -2548,14 +2562,16 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   s.rounds = ctx->h_ctrl->rounds;
   s.min_used_latency_ns = ctx->h_ctrl->min_used;
   s.max_codel_len = mc;
-  s.max_pending_events = ctx->h_ctrl->max_bucket;
+
   {
     const size_t G = ctx->S.G;
     std::vector<uint64_t> wc(W_N * G);
     SGN_HIP(ctx, hipMemcpy(wc.data(), (const void*)ctx->S.w_cnt, wc.size() * 8, hipMemcpyDeviceToHost));
     uint64_t acc[W_N] = {};
     for (int k = 0; k < W_N; k++)
-      for (size_t g = 0; g < G; g++) acc[k] += wc[k * G + g];
+      for (size_t g = 0; g < G; g++)
+        acc[k] = k == W_MAXFILL ? std::max(acc[k], wc[k * G + g]) : acc[k] + wc[k * G + g];
+    s.max_pending_events = acc[W_MAXFILL];
     s.host_executions = acc[W_EXEC];
     s.event_runs = acc[W_RUNS];
     s.sched_sorted_segments = acc[W_SORTED];

@@ -146,7 +146,7 @@ static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
 
 // per-wave counters (DevSim::w_cnt rows of G)
-enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_N };
+enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_MAXFILL, W_N };  // W_MAXFILL: max, not sum
 
 // host flag bits
 enum : uint32_t {
