@@ -4,10 +4,13 @@
 // Mutex<EventQueue> pushes between threads (core/worker.rs:603-613) and the round minimum
 // is a per-thread reduction (core/manager.rs:623-628). With hosts sharded over GPUs, the
 // same two steps become, per round and entirely stream-ordered (no host round trip):
-//   1. grouped ncclSend/ncclRecv of each peer's fixed-size event slot + its count,
-//   2. k_import files received events into the local calendar,
-//   3. k_finalize(local) computes {min next event, min used latency} for this shard,
-//   4. ncclAllReduce(min, uint64, 2) in place, then k_advance moves the window.
+//   1. k_execute's last wave does the local round edge (bucket bookkeeping) and writes one
+//      32-byte message per peer: {runs sent to it, this shard's min next event including
+//      the runs it exported, its min used latency},
+//   2. ONE grouped ncclSend/ncclRecv moves each peer's fixed-size run slot and message,
+//   3. k_import files the received runs into the local calendar,
+//   4. k_advance reduces the n messages (the global min: what an all-reduce would give)
+//      and moves the window — every shard computes the same window.
 // Every produced event has time >= the window end (worker.rs:386-390), so nothing needs
 // to cross shards inside a round.
 
@@ -22,9 +25,8 @@
 
 namespace sgn {
 void launch_execute(sgn_ctx* ctx);
-void launch_finalize_local(sgn_ctx* ctx);
 void launch_import(sgn_ctx* ctx);
-void launch_advance(sgn_ctx* ctx, const uint64_t* red);
+void launch_advance(sgn_ctx* ctx);
 }  // namespace sgn
 
 using namespace sgn;
@@ -73,6 +75,10 @@ int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES], uint64_t sl
 
 namespace sgn {
 int comm_round_exchange(sgn_ctx* ctx) {
+  // k_execute's last wave has already done the local round edge and written this shard's
+  // message for every peer (run count, local min next event incl. exported runs, local min
+  // used latency): ONE grouped send/recv moves runs and messages, then every shard imports
+  // and reduces the messages itself (no all-reduce, no memsets).
   DevSim& S = ctx->S;
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   hipStream_t st = ctx->stream;
@@ -83,23 +89,15 @@ int comm_round_exchange(sgn_ctx* ctx) {
     r = ncclSend(S.xout + (size_t)p * S.xslot, slot_bytes, ncclUint8, (int)p, comm, st);
     if (r == ncclSuccess)
       r = ncclRecv(S.xin + (size_t)p * S.xslot, slot_bytes, ncclUint8, (int)p, comm, st);
-    if (r == ncclSuccess) r = ncclSend(S.xout_n + p, 1, ncclUint32, (int)p, comm, st);
-    if (r == ncclSuccess) r = ncclRecv(S.xin_n + p, 1, ncclUint32, (int)p, comm, st);
+    if (r == ncclSuccess) r = ncclSend(S.xmsg_out + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
+    if (r == ncclSuccess) r = ncclRecv(S.xmsg_in + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
   }
   ncclResult_t r2 = ncclGroupEnd();
   if (r != ncclSuccess || r2 != ncclSuccess)
     return set_error(ctx, SGN_EDEVICE, std::string("RCCL exchange: ") +
                                            ncclGetErrorString(r != ncclSuccess ? r : r2));
-  SGN_HIP(ctx, hipMemsetAsync(S.xin_n + S.rank, 0, 4, st));
   launch_import(ctx);
-  SGN_HIP(ctx, hipMemsetAsync(S.xout_n, 0, (size_t)S.n_ranks * 4, st));
-  launch_finalize_local(ctx);
-  // {round_min, min_used} are adjacent u64 fields of Ctrl: reduce both in place
-  uint64_t* red = &S.ctrl->round_min;
-  r = ncclAllReduce(red, red, 2, ncclUint64, ncclMin, comm, st);
-  if (r != ncclSuccess)
-    return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-reduce: ") + ncclGetErrorString(r));
-  launch_advance(ctx, red);
+  launch_advance(ctx);
   return 0;
 }
 
@@ -138,7 +136,6 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
     if (!ctxs[i] || !ctxs[i]->sim_ready || !ctxs[i]->comm_local || ctxs[i]->group.size() != n)
       return ctxs[i] ? set_error(ctxs[i], SGN_ESTATE, "not a local shard group") : SGN_EINVAL;
   uint64_t done = 0;
-  std::vector<uint32_t> cnt(n);
   for (; done < max_rounds; done++) {
     Ctrl h{};
     SGN_HIP(ctxs[0], hipMemcpy(&h, (const void*)ctxs[0]->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
@@ -148,43 +145,29 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       launch_execute(ctxs[i]);
     }
     for (uint32_t i = 0; i < n; i++) SGN_HIP(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
-    // the all-to-all: shard b's receive slot a <- shard a's send slot b
+    // the all-to-all: shard b's receive slot and message a <- shard a's send slot and
+    // message b (what comm_round_exchange's grouped send/recv does)
     for (uint32_t a = 0; a < n; a++) {
       sgn_ctx* A = ctxs[a];
-      SGN_HIP(A, hipMemcpy(cnt.data(), (const void*)A->S.xout_n, n * 4, hipMemcpyDeviceToHost));
+      std::vector<uint64_t> msg((size_t)n * 4);
+      SGN_HIP(A, hipMemcpy(msg.data(), (const void*)A->S.xmsg_out, msg.size() * 8, hipMemcpyDeviceToHost));
       for (uint32_t b = 0; b < n; b++) {
         if (b == a) continue;
         sgn_ctx* B = ctxs[b];
-        const uint32_t k = std::min<uint32_t>(cnt[b], (uint32_t)A->xslot);
+        const uint64_t k = std::min<uint64_t>(msg[4 * (size_t)b], A->xslot);
         if (k)
           SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * B->S.xslot),
                                (const void*)(A->S.xout + (size_t)b * A->S.xslot),
                                (size_t)k * sizeof(EvRec), hipMemcpyDefault));
-        SGN_HIP(B, hipMemcpy((void*)(B->S.xin_n + a), &cnt[b], 4, hipMemcpyHostToDevice));
+        SGN_HIP(B, hipMemcpy((void*)(B->S.xmsg_in + 4 * (size_t)a), &msg[4 * (size_t)b], 32,
+                             hipMemcpyHostToDevice));
       }
     }
     for (uint32_t i = 0; i < n; i++) {
       sgn_ctx* c = ctxs[i];
       SGN_HIP(c, hipSetDevice(c->device));
-      SGN_HIP(c, hipMemsetAsync((void*)(c->S.xin_n + c->S.rank), 0, 4, c->stream));
       launch_import(c);
-      SGN_HIP(c, hipMemsetAsync((void*)c->S.xout_n, 0, (size_t)c->S.n_ranks * 4, c->stream));
-      launch_finalize_local(c);
-    }
-    // all-reduce(min) of {round_min, min_used}
-    uint64_t red[2] = {~0ULL, ~0ULL};
-    for (uint32_t i = 0; i < n; i++) {
-      sgn_ctx* c = ctxs[i];
-      SGN_HIP(c, hipStreamSynchronize(c->stream));
-      uint64_t v[2];
-      SGN_HIP(c, hipMemcpy(v, (const void*)&c->S.ctrl->round_min, 16, hipMemcpyDeviceToHost));
-      red[0] = std::min(red[0], v[0]);
-      red[1] = std::min(red[1], v[1]);
-    }
-    for (uint32_t i = 0; i < n; i++) {
-      sgn_ctx* c = ctxs[i];
-      SGN_HIP(c, hipMemcpy((void*)&c->S.ctrl->round_min, red, 16, hipMemcpyHostToDevice));
-      launch_advance(c, (const uint64_t*)&c->S.ctrl->round_min);
+      launch_advance(c);
       SGN_HIP(c, hipStreamSynchronize(c->stream));
     }
   }

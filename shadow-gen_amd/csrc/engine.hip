@@ -208,6 +208,7 @@ struct Outbox {
   EvRec rec[OBOX];
   uint32_t idx[OBOX];  // (slab set, group) slab index
   uint32_t n;          // records appended (may exceed OBOX: those were placed directly)
+  uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
 };
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
@@ -1032,6 +1033,7 @@ struct HostExec {
         const uint32_t mid = (lo + hi) >> 1;
         if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
       }
+      atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
       pos = atomicAdd(&S.xout_n[lo], nrec);
       dstp = S.xout + (size_t)lo * S.xslot;
       cap = S.xslot;
@@ -1369,8 +1371,11 @@ __device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
 // finalize_round for the fused single-shard path, run by the last wave of k_execute: the
 // waves' minima come from the chunk slots; every value another wave changed during this
 // launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
+// local != 0 (multi-shard): instead of moving the window, the shard's {min next event, min
+// used latency} and its per-peer run counts go into the round-edge messages (comm.cpp sends
+// them with the runs; k_advance reduces them on every shard).
 __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uint64_t ws,
-                               uint64_t we, uint32_t ks, uint32_t slab_b1) {
+                               uint64_t we, uint32_t ks, uint32_t slab_b1, int local = 0) {
   SGN_GLB Ctrl* C = S.ctrl;
   const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
   // one round trip: every value to read (chunk minima, spare-slab minimum, bucket minima,
@@ -1413,6 +1418,17 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     st_dev(&S.bucket_min[b1], nb1);
     m = nb1 < m ? nb1 : m;
     m = wn < m ? wn : m;
+    if (local) {
+      for (uint32_t p = 0; p < S.n_ranks; p++) {
+        const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
+        SGN_GLB uint64_t* o = (p == S.rank ? S.xmsg_in : S.xmsg_out) + 4 * (size_t)p;
+        st_dev(o, cnt);
+        st_dev(o + 1, m);
+        st_dev(o + 2, mu);
+        st_dev(o + 3, (uint64_t)0);
+      }
+      return;
+    }
     const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
     st_dev(&C->last_min_next, min_next);
     // Runahead::get (runahead.rs:44-57)
@@ -1503,7 +1519,10 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint64_t lmin = INVALID;
   if (valid) lmin = S.nextloc[h];
   Outbox* ob = X.ob;
-  if (lane == 0) ob->n = 0;
+  if (lane == 0) {
+    ob->n = 0;
+    ob->xmin = INVALID;
+  }
   __syncthreads();
   HostExec ex(S, h, we, be, ks, lslot + lane, lbs, ob);
   bool loaded = false;
@@ -1652,7 +1671,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
   if (loaded) my_min = ex.next_local_time();
   kmin = wave_min_u64(kmin);
-  const uint64_t m = wave_min_u64(my_min);
+  uint64_t m = wave_min_u64(my_min);
+  m = ob->xmin < m ? ob->xmin : m;  // runs exported to other shards are pending events too
   *kmin_out = kmin;
   *next_out = m;
   if (lane == 0) {
@@ -1793,12 +1813,13 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   uint64_t kmin, m;
   bool last = false;
   exec_group(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
-    if (S.fuse_finalize) last = arrive(S, blockIdx.x, gridDim.x, k, n);
+    last = arrive(S, blockIdx.x, gridDim.x, k, n);
   });
   if (!last) return;
   const uint32_t b1 = bucket_of(S, we - 1);
+  // single shard: the round edge; multi-shard: the local part of it (comm.cpp finishes it)
   finalize_fused(S, threadIdx.x, (gridDim.x + 63) >> 6, ws, we, ks,
-                 S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]));
+                 S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]), S.fuse_finalize ? 0 : 1);
 }
 
 // Persistent rounds (single shard): the grid stays resident and runs up to max_rounds
@@ -1885,11 +1906,18 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 // Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
 // window; multi-shard runs reduce C->round_min/min_used across ranks first.
 // Multi-shard: window advance from the all-reduced {min_next, min_used}.
-__global__ void k_advance(DevSim S, const uint64_t* red) {
+// the global {min next event, min used latency} from every shard's round-edge message
+__global__ void k_advance(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active || threadIdx.x != 0) return;
-  const uint64_t m = red[0];
-  if (S.dynamic && red[1] != INVALID && red[1] < C->min_used) C->min_used = red[1];
+  uint64_t m = INVALID, mu = INVALID;
+  for (uint32_t p = 0; p < S.n_ranks; p++) {
+    const uint64_t a = S.xmsg_in[4 * (size_t)p + 1], b = S.xmsg_in[4 * (size_t)p + 2];
+    m = a < m ? a : m;
+    mu = b < mu ? b : mu;
+    S.xout_n[p] = 0;  // the next round's sends count from zero
+  }
+  if (S.dynamic && mu != INVALID && mu < C->min_used) C->min_used = mu;
   const uint64_t min_next = m == INVALID ? EMU_MAX : m;
   C->last_min_next = min_next;
   uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
@@ -1908,22 +1936,22 @@ __global__ void k_advance(DevSim S, const uint64_t* red) {
 
 // Multi-shard: file received runs into the local calendar (after k_execute, so runs for
 // the window's last bucket go to the spare slab like local sends).
+// Multi-shard: the runs other shards sent this round into the calendar. Runs at or after
+// this round's window end: the bucket bookkeeping of the round edge already ran (k_execute's
+// last wave), so every run goes to its bucket's current slab set.
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
-  const uint32_t b1 = bucket_of(S, C->we - 1);
-  const uint32_t ks = C->keep_slab;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
-    const uint32_t n = min(S.xin_n[r], S.xslot);
+    if (r == S.rank) continue;
+    const uint32_t n = (uint32_t)min(S.xmsg_in[4 * (size_t)r], (uint64_t)S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
       const EvRec e = S.xin[(size_t)r * S.xslot + i];
       const uint32_t b = bucket_of(S, e.time);
-      const uint32_t slab = b == b1 ? ks : S.bucket_slab[b];
-      const size_t idx = (size_t)slab * S.G + ((e.dst - S.lo) >> S.gsh);
+      const size_t idx = (size_t)S.bucket_slab[b] * S.G + ((e.dst - S.lo) >> S.gsh);
       const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
-      atomicMin((unsigned long long*)(b == b1 ? &C->keep_min : &S.bucket_min[b]),
-                (unsigned long long)e.time);
+      atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)e.time);
       if (pos < S.CAP)
         S.pool[idx * S.CAP + pos] = e;
       else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
@@ -2394,6 +2422,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
     S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    S.xmsg_out = (decltype(S.xmsg_out))dalloc<uint64_t>(ctx, ctx->nranks * 4);
+    S.xmsg_in = (decltype(S.xmsg_in))dalloc<uint64_t>(ctx, ctx->nranks * 4);
+    if (!S.xmsg_out || !S.xmsg_in) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
   }
   Ctrl c{};
@@ -2891,13 +2922,10 @@ void launch_execute(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_execute, dim3(ctx->S.G), dim3(64), exec_lds_bytes(ctx->S.CAP), ctx->stream,
                      (const DevSim*)ctx->d_S);
 }
-void launch_finalize_local(sgn_ctx* ctx) {
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->S, 0);
-}
 void launch_import(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_import, dim3(256), dim3(256), 0, ctx->stream, ctx->S);
 }
-void launch_advance(sgn_ctx* ctx, const uint64_t* red) {
-  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, ctx->stream, ctx->S, red);
+void launch_advance(sgn_ctx* ctx) {
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, ctx->stream, ctx->S);
 }
 }  // namespace sgn

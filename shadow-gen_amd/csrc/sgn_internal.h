@@ -276,6 +276,10 @@ struct DevSim {
   SGN_GLB uint32_t* xout_n;  // [n_ranks]
   SGN_GLB EvRec* xin;
   SGN_GLB uint32_t* xin_n;   // [n_ranks] (received counts)
+  // round-edge messages, 4 u64 per peer: {runs sent to it, local min next event (incl. the
+  // runs exported this round), local min used latency, 0}; xmsg_in[rank] is this shard's own
+  SGN_GLB uint64_t* xmsg_out;  // [n_ranks * 4]
+  SGN_GLB uint64_t* xmsg_in;   // [n_ranks * 4]
   uint32_t xslot;    // events per slot
   uint32_t rank;
   SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
