@@ -199,6 +199,7 @@ struct Pkt {
 // ------------------------------------------------------------------------------------
 // A lane's LDS slot: the pending digest runs and the digests themselves (touched once per
 // run), and the CoDel queue's cached head and open tail runs.
+constexpr uint32_t GATHER_SPEC = 16;  // slab slots a gather loads before the fill is known
 // The wave's outbox: event records for this shard's calendar, placed after the event loop
 // by all 64 lanes at once (one round trip for all the slab reservations of the wave instead
 // of one per send in the sending lane's serial path). A full outbox falls back to placing
@@ -1541,19 +1542,22 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
     const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
-    // the slab's fill and its first 64 records in ONE round trip: the records are loaded
-    // before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
+    // the slab's fill and its first GATHER_SPEC records in ONE round trip: the records are
+    // loaded before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
     // appends to a bucket's slab while its window runs (new runs for the window's last
-    // bucket go to the spare slab set)
+    // bucket go to the spare slab set). Only GATHER_SPEC lanes load speculatively: a slab
+    // holds ~4 runs on average, and loading all 64 slots pulled 2 KB of cold HBM lines per
+    // slab (PMC fetch 58 -> 342 MB per launch); fuller slabs load the rest below.
     SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
-    EvRec r0 = ld_dev_rec(pb + lane);
+    EvRec r0{};
+    if (lane < GATHER_SPEC) r0 = ld_dev_rec(pb + lane);
     const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
     lcnt[lane] = 0;
     uint32_t N = 0;
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
       const uint32_t j = j0 + lane;
       EvRec r = r0;
-      if (j0 > 0 && j < n) r = ld_dev_rec(pb + j);
+      if ((j0 > 0 || lane >= GATHER_SPEC) && j < n) r = ld_dev_rec(pb + j);
       const bool due = j < n && (!last || r.time < we);
       const bool keep = j < n && !due;
       const uint64_t dm = __ballot(due), km = __ballot(keep);
