@@ -170,7 +170,7 @@ def main():
         ev = int(e.item())
     d = {k: st1[k] - st0[k] for k in st1}
     rounds = d["rounds"]
-    # roofline of the dominant kernel (k_execute): algorithmic bytes per launch
+    # roofline of the dominant kernel (k_rounds on one shard, k_execute multi-shard): algorithmic bytes per launch
     # = SURVEY.md §8(d)'s packet-path model, 128 B per packet (send record, DNS, node
     # indices, route entry, event record write, sort/merge, pop read) + 96 B per active
     # host-round (RNG state, event-id counter, queue head), over the units one launch
