@@ -56,47 +56,139 @@ def events_of(st):
     return st["packets_sent"] + st["packets_loss_dropped"] + st["packet_events_popped"]
 
 
-def cpu_baseline(g, used, hosts, cfg, tr, args, budget_s):
-    """The oracle (CPU restatement of the reference's round loop, with the reference's own
-    parallel structure: worker threads over host chunks, per-host queue locks, a barrier per
-    round) on the same workload and the SAME rounds the GPU timed: warm-up rounds untimed,
-    then the timed rounds (bounded by budget_s), then a single-thread sample."""
+def cpu_share():
+    """Host cores this process may use: the cgroup CPU quota when one is set (the GPU box
+    grants a share of a larger machine), else the affinity mask; plus what the OS shows."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = visible
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            share = max(1, min(visible, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the box pins pools to its share
+        share = max(1, min(share, int(os.environ["OMP_NUM_THREADS"])))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return share, visible, model
+
+
+STAT_KEYS = ("rounds", "packets_sent", "packets_loss_dropped", "packets_unknown_dst", "packet_events_popped",
+             "codel_dropped", "delivered", "local_delivered", "app_blocked", "local_events", "bytes_delivered",
+             "min_used_latency_ns", "max_codel_len", "host_executions")
+DIGEST_KEYS = ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered", "n_codel_dropped")
+
+
+def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
+    """The CPU restatement of the reference's hot path (oracle/, a C++ port: the Rust
+    reference cannot be built here), timed on this box's host cores, and the parity check of
+    the GPU run.
+
+    1. Parity: the oracle (CPU-optimised data structures, all cores) runs the same workload
+       through exactly the rounds the GPU ran (warm-up untimed, then the GPU's timed rounds,
+       timed); its stats, final window and every host's digests must equal the GPU's.
+    2. Then, on the next rounds of the same simulation, each of {reference-faithful,
+       CPU-optimised} x {all cores, 1 core} for a bounded sample (SURVEY.md §8(d),
+       BASELINE.md). Faithful = the reference's hash-map lookups per packet, the global
+       packet-counter write lock (worker.rs:379, graph/mod.rs:450-458), heap packet copies
+       and a lock per queue operation; a persistent worker pool with a rendezvous per round
+       either way.
+    3. APSP: compute_shortest_paths restated both ways, at all cores (rayon) and 1 core."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle_py
 
-    threads = max(1, min(16, os.cpu_count() or 1))
-    t_apsp = time.perf_counter()
-    lat, loss = oracle_py.routes(g, used)  # per-source Dijkstra (graph/mod.rs:181-226), 1 thread
-    apsp_s = time.perf_counter() - t_apsp
-    sim = oracle_py.Sim(used, lat, loss, hosts, cfg, tr, threads=threads)
-    sim.run(args.warmup * args.rounds_per_step)
+    cores, visible, model = cpu_share()
+    apsp = {}
+    for faithful in (True, False):
+        for th in (cores, 1):
+            t0 = time.perf_counter()
+            lat, loss = oracle_py.routes(g, used, faithful=faithful, threads=th)
+            apsp[f"{'faithful' if faithful else 'optimised'}_{th}c_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    sim = oracle_py.Sim(used, lat, loss, hosts, cfg, tr, threads=cores)
+    warm = args.warmup * args.rounds_per_step
+    assert sim.run(warm) == warm
+    st0 = sim.stats()
+    t0 = time.perf_counter()
+    timed_rounds = sim.run(gpu["rounds_timed"])
+    el = time.perf_counter() - t0
+    ev = events_of(sim.stats()) - events_of(st0)
+    # parity with the GPU run: same rounds, same counters, same window, same digests
+    so = sim.stats()
+    mism = [k for k in STAT_KEYS if so[k] != gpu["stats"][k]]
+    if sim.window() != gpu["window"]:
+        mism.append("window")
+    do = sim.digests(0, hosts.n)
+    for f in DIGEST_KEYS:
+        bad = np.nonzero(do[f] != gpu["digests"][f])[0] if do[f].ndim == 1 else \
+            np.nonzero((do[f] != gpu["digests"][f]).any(1))[0]
+        if len(bad):
+            mism.append(f"digest {f}: {len(bad)} hosts (first {bad[:3].tolist()})")
+    parity = {"ok": not mism and timed_rounds == gpu["rounds_timed"], "mismatches": mism[:8],
+              "rounds_compared": warm + timed_rounds, "hosts_compared": int(hosts.n),
+              "fields": list(STAT_KEYS) + ["window"] + [f"digest.{f}" for f in DIGEST_KEYS]}
+    modes = {"optimised_all": {"value": ev / el, "cores": cores, "rounds": timed_rounds, "events": ev,
+                               "wall_s": round(el, 2), "sample": "the GPU's timed rounds"}}
 
-    def timed(rounds_max, budget):
-        st0 = sim.stats()
-        t0 = time.perf_counter()
-        done = 0
-        while done < rounds_max and time.perf_counter() - t0 < budget:
-            done += sim.run(min(50, rounds_max - done))
-        el = time.perf_counter() - t0
-        return events_of(sim.stats()) - events_of(st0), el, done
+    def sample(name, faithful, th, budget):
+        sim.set_faithful(faithful)
+        sim.set_threads(th)
+        s0 = events_of(sim.stats())
+        t1 = time.perf_counter()
+        r = 0
+        while time.perf_counter() - t1 < budget and sim.window()[2]:
+            r += sim.run(20)
+        e1 = time.perf_counter() - t1
+        e = events_of(sim.stats()) - s0
+        modes[name] = {"value": e / e1, "cores": th, "rounds": r, "events": e, "wall_s": round(e1, 2),
+                       "sample": "the next rounds of the same simulation"}
 
-    ev, el, rounds = timed(args.steps * args.rounds_per_step, budget_s)
-    sim.L.ora_sim_set_threads(sim.h, 1)
-    ev1, el1, rounds1 = timed(args.steps * args.rounds_per_step, budget_s / 3)
+    b = args.cpu_budget_s
+    sample("faithful_all", True, cores, b / 4)
+    sample("faithful_1", True, 1, b / 4)
+    sample("optimised_1", False, 1, b / 4)
+    f = modes["faithful_all"]
     return {
-        "value": ev / el,
+        "value": f["value"],
         "unit": "packet events/s",
-        "cores": threads,
+        "cores": cores,
         "kind": "port",
-        "sample": f"oracle round loop ({threads} worker threads) over the same {hosts.n}-host "
-                  f"workload and the same rounds the GPU timed (rounds "
-                  f"{args.warmup * args.rounds_per_step}..{args.warmup * args.rounds_per_step + rounds}"
-                  f", {ev} packet events, {el:.1f} s wall; warm-up rounds untimed)",
-        "apsp_ms": round(apsp_s * 1e3, 1),
-        "apsp_sample": "the oracle's per-source Dijkstra over the same graph (1 thread)",
-        "single_core": {"value": ev1 / el1, "cores": 1,
-                        "sample": f"the next {rounds1} rounds on 1 thread ({ev1} packet events, {el1:.1f} s)"},
-    }
+        "sample": f"reference-faithful C++ restatement (oracle/) of the round loop on {cores} worker threads, "
+                  f"{f['rounds']} rounds of the same {hosts.n}-host workload right after the GPU's timed rounds "
+                  f"({f['events']} packet events, {f['wall_s']} s); the CPU-optimised restatement over the GPU's "
+                  f"exact timed rounds reached {modes['optimised_all']['value'] / 1e6:.1f} M/s",
+        "cpu_model": model, "cpus_visible": visible,
+        "modes": {k: {kk: (round(vv, 1) if isinstance(vv, float) else vv) for kk, vv in m.items()}
+                  for k, m in modes.items()},
+        "apsp_ms": apsp,
+        "apsp_sample": "compute_shortest_paths restated (per-source Dijkstra over the same graph): "
+                       "faithful = hash-map scores, O(U) contains filter, hashed U^2 output + to_ids "
+                       "re-collect; optimised = dense arrays; sources over N threads like rayon",
+    }, parity
+
+
+def apsp_roofline(apsp, V, U):
+    """the blocked min-plus latency phase streams the V x V u64 matrix once
+    per k-block (B_fw = 16 V^3 / T); the loss phase reads, per sweep and source, the tight arcs
+    (20 B each) and the V-entry distance row (12 B each): B_loss = U H (20 E_tight + 12 V)."""
+    T = apsp["tile"] or 64
+    b_fw = 16.0 * V ** 3 / T
+    b_loss = float(U) * max(1, apsp["loss_iters"]) * (20.0 * apsp["n_tight_edges"] / max(1, U) + 12.0 * V)
+    out = {}
+    for name, b, ms in (("latency_phase", b_fw, apsp["latency_ms"]), ("loss_phase", b_loss, apsp["loss_ms"])):
+        gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        out[name] = {"bound": "hbm", "alg_bytes": int(b), "ms": round(ms, 3), "achieved": round(gbs, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5)}
+    out["relaxations_per_s"] = round(V ** 3 / (apsp["latency_ms"] * 1e-3), 1) if apsp["latency_ms"] > 0 else None
+    out["note"] = ("the latency phase is a chain of V dependent pivot steps (64 per k-block), "
+                   "bounded by that chain's latency, not by bytes")
+    return out
 
 
 def main():
@@ -107,7 +199,8 @@ def main():
     ap.add_argument("--hosts", type=int, default=100_000, help="hosts per GPU")
     ap.add_argument("--nodes", type=int, default=1000)
     ap.add_argument("--rounds-per-step", type=int, default=100)
-    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0,
+                    help="wall budget of the CPU mode samples after the parity run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -184,22 +277,32 @@ def main():
     if launches and exec_ms > 0:
         avg_s = exec_ms / launches / 1e3
         achieved = alg_bytes / launches / avg_s / 1e9
+        rpl = rounds / launches
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                 "kernel": rk, "avg_launch_us": round(avg_s * 1e6, 2),
                 "alg_bytes_per_launch": int(alg_bytes / launches),
                 "units_per_launch": {"packets": round(n_pkt / launches, 1),
-                                     "active_host_rounds": round(host_exec / launches, 1)}}
+                                     "active_host_rounds": round(host_exec / launches, 1),
+                                     "rounds": round(rpl, 2)},
+                "latency_bound": {
+                    "round_us": round(avg_s * 1e6 / rpl, 2),
+                    "note": "the round is a chain: per-host serial event loops (RNG stream and event "
+                            "ids force in-order work inside a host) with dependent memory round trips, "
+                            "then a grid-wide barrier; HBM bytes are not what bounds it"}}
         # HBM bytes per launch measured by PMC (tools/pmc_traffic.sh: FETCH_SIZE x2 +
-        # WRITE_SIZE over the same default run's timed dispatches), when it matches this run
+        # WRITE_SIZE, separate passes) for this workload; per launch of the same number of
+        # rounds, so independent of --steps / --warmup
         tf = ROOT / "profiles" / "round_kernel_traffic.json"
-        default_run = (args.hosts, args.nodes, args.rounds_per_step, args.steps, args.warmup,
-                       world) == (100_000, 1000, 100, 10, 5, 1)
-        if tf.exists() and default_run:
+        if tf.exists():
             t = json.loads(tf.read_text())
-            roof["traffic"] = t["traffic_bytes_per_launch"]
-            roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
-            roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
+            wl = t.get("workload", {})
+            if (wl.get("hosts_per_gpu"), wl.get("graph_nodes"), wl.get("rounds_per_launch"), wl.get("n_gpus"),
+                    t.get("kernel")) == (args.hosts, args.nodes, round(rpl), world, rk):
+                roof["traffic"] = t["traffic_bytes_per_launch"]
+                roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
+                roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
+    info = ctx.engine_info()
     out = {
         "metric": METRIC,
         "value": ev / el,
@@ -222,23 +325,37 @@ def main():
         "apsp_build_ms": round(apsp["total_ms"], 3),
         "apsp": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in apsp.items()},
         "apsp_first_build_ms": round(apsp_first["total_ms"], 3),
+        "apsp_roofline": apsp_roofline(apsp, args.nodes, len(used)),
         "sim_ms_per_step": None,
         "rounds_timed": rounds,
         "packet_events_timed": ev,
         "roofline": roof,
         "cpu_baseline": None,
+        "parity": None,
         "max_slab_fill": st1["max_pending_events"],
+        "hbm_footprint_bytes": info["device_bytes"],
+        "engine": {k: info[k] for k in ("calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity",
+                                        "persistent_grid", "persistent_fallbacks")},
     }
-    ws, _, _ = ctx.window()
+    ws, we, act = ctx.window()
     out["sim_time_reached_ms"] = (ws - sgn.SIMULATION_START) / 1e6
     out["sim_ms_per_step"] = out["sim_time_reached_ms"] / (args.steps + args.warmup)
+    ok = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(g, used, hosts, cfg, tr, args, args.cpu_budget_s)
+        gpu = {"rounds_timed": rounds, "stats": st1, "window": (ws, we, act),
+               "digests": ctx.digests(0, hosts.n)}
+        out["cpu_baseline"], par = cpu_baseline(g, used, hosts, cfg, tr, args, gpu)
+        out["parity"] = par["ok"]
+        out["parity_detail"] = par
+        ok = par["ok"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
+    if not ok:
+        print("bench: GPU results differ from the oracle (parity false)", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

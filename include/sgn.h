@@ -242,6 +242,10 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, sgn_host_
 /* Host::next_event_time (host.rs:832): backs worker_maxEventRunaheadTime (worker.rs:774).
  * SGN_EMUTIME_INVALID when the queue is empty. Only valid between rounds. */
 int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t);
+/* The same for every owned host in [host_lo, host_hi) at once (out[host - host_lo]): one
+ * device pass over the host records and the calendar, one copy. A CPU controller reads its
+ * hosts' worker_maxEventRunaheadTime inputs with one call per round, not one per host. */
+int sgn_hosts_next_event_time(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, uint64_t* out);
 
 /* Per-packet trace (for bit-exact comparison at small sizes). Enable before sim_init. */
 #define SGN_TRACE_SEND 1u   /* a = now, b = deliver time (0 if dropped/unknown), c = event id */
@@ -288,6 +292,23 @@ typedef struct sgn_pkt_soa {
 } sgn_pkt_soa;
 int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* batch);
 
+/* Per-thread staging: Shadow calls Worker::send_packet from every worker thread
+ * at once (router/mod.rs:70-73, worker.rs:330). Each CPU worker thread owns one stage and
+ * appends to it with sgn_stage_push — safe concurrently on DISTINCT stages, no device work;
+ * the controller thread then submits every stage with one sgn_stage_flush between rounds.
+ * A flush is exactly one sgn_submit of the stages' datagrams concatenated in stage-creation
+ * order (each stage in push order); on failure nothing is queued and the stages keep their
+ * datagrams. Create and destroy stages only while no flush runs. */
+typedef struct sgn_stage sgn_stage;
+int sgn_stage_create(sgn_ctx* ctx, sgn_stage** out);
+void sgn_stage_destroy(sgn_stage* stage);
+/* Copies the batch into the stage (checks array presence and payload/wire sizes only; the
+ * window and horizon rules are checked at flush). */
+int sgn_stage_push(sgn_stage* stage, const sgn_pkt_soa* batch);
+/* Datagrams waiting in a stage. */
+uint64_t sgn_stage_pending(const sgn_stage* stage);
+int sgn_stage_flush(sgn_ctx* ctx);
+
 /* Packet egress: one record per datagram that left the network core, on the host where it
  * happened. Every submitted datagram yields exactly one record (delivered or dropped) once
  * its fate is decided; datagrams sent to EXTERNAL hosts are all submitted ones. */
@@ -327,12 +348,29 @@ int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end);
  * of host_rngDouble / host_rngNextNBytes (host/host.rs:1324-1336) and raw next_u64. They
  * advance the same Xoshiro256++ stream the loss draws use. Between rounds only. */
 int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out);
+/* counts[i] draws from each of n DISTINCT owned hosts in one device pass, concatenated in
+ * order into out (sum(counts) entries): the batched form of sgn_rng_next_u64. */
+int sgn_rng_next_u64_batch(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint32_t n,
+                           uint64_t* out);
 /* rand 0.9 StandardUniform f64: (next_u64 >> 11) * 2^-53 */
 int sgn_rng_double(sgn_ctx* ctx, uint32_t host, double* out);
 /* rand_core 0.9 fill_bytes_via_next: little-endian next_u64 per 8 bytes; a tail of 5..7
  * bytes takes the low bytes of one more next_u64, a tail of 1..4 those of next_u32 (the
  * upper half of next_u64, rand_xoshiro 0.7). */
 int sgn_rng_fill_bytes(sgn_ctx* ctx, uint32_t host, uint8_t* buf, size_t len);
+
+/* Engine layout and execution mode chosen by sgn_sim_init (capacity planning, tests). */
+typedef struct sgn_engine_info {
+  uint64_t calendar_buckets;    /* NB: time buckets of the event calendar (a power of two) */
+  uint64_t bucket_width_ns;     /* BW = max(min route latency, configured runahead) */
+  uint64_t host_groups;         /* G: groups of hosts_per_wave consecutive hosts */
+  uint64_t slab_capacity;       /* event runs per (bucket, group) slab */
+  uint64_t hosts_per_wave;
+  uint64_t persistent_grid;     /* workgroups of the persistent round kernel (0: per-round) */
+  uint64_t persistent_fallbacks;/* persistent launches refused by the residency census */
+  uint64_t device_bytes;        /* device memory held by the simulation */
+} sgn_engine_info;
+int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 
 /* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS). */
 typedef struct sgn_kernel_times {

@@ -21,7 +21,10 @@
 #include <atomic>
 #include <map>
 #include <memory>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <queue>
 #include <string>
@@ -530,8 +533,26 @@ struct Adj {
   uint32_t edge;
 };
 
-int routes(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, uint64_t* lat_out,
-           float* loss_out, char* err, size_t err_len) {
+// Runs fn(t) for t in [0, threads) on threads (t = 0 on the caller) and joins them.
+template <typename F>
+void par_for_threads(int threads, F&& fn) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; t++) th.emplace_back(fn, t);
+  fn(0);
+  for (auto& x : th) x.join();
+}
+
+// compute_shortest_paths (graph/mod.rs:181-226) / get_direct_paths (:228-250) into a dense
+// U x U table. Two restatements with identical results:
+//  - faithful != 0: the reference's own data structures — per-source Dijkstra whose scores
+//    are a hash map (petgraph 0.8.3 algo::dijkstra returns HashMap<NodeIndex, K>), the
+//    `nodes.contains(dst)` linear filter, a HashMap<(src, dst), PathProperties> of U^2
+//    entries per source merged into one (rayon flat_map + collect), the self-loop override,
+//    and the to_ids re-collect into HashMap<(u32, u32), _> (core/sim_config.rs:423-445);
+//  - faithful == 0: the same searches over dense arrays (CPU-optimised).
+// Sources run on `threads` worker threads (rayon's into_par_iter over the used nodes).
+int routes_mode(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, int faithful,
+                int threads, uint64_t* lat_out, float* loss_out, char* err, size_t err_len) {
   const uint32_t V = g->n_nodes;
   std::unordered_map<uint32_t, uint32_t> idx;  // GML id -> NodeIndex (last wins, mod.rs:159)
   for (uint32_t i = 0; i < V; i++) idx[g->node_id[i]] = i;
@@ -549,14 +570,20 @@ int routes(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, u
     es[k] = a->second;
     ed[k] = b->second;
   }
-  // get_edge_weight: exactly one edge connecting a -> b (undirected: either orientation,
-  // a self-loop counted once; petgraph Graph::edges_connecting)
+  // adjacency as petgraph iterates it: directed -> outgoing; undirected -> both, with
+  // self-loops once
+  std::vector<std::vector<Adj>> adj(V);
+  for (uint32_t k = 0; k < g->n_edges; k++) {
+    adj[es[k]].push_back({ed[k], k});
+    if (!g->directed && es[k] != ed[k]) adj[ed[k]].push_back({es[k], k});
+  }
+  // get_edge_weight (:254-287): exactly one edge connecting a -> b (petgraph
+  // Graph::edges_connecting walks a's edges; undirected: either orientation, a self-loop once)
   auto edge_weight = [&](uint32_t a, uint32_t b, PathProp* out) -> int {
     int count = 0;
     uint32_t found = 0;
-    for (uint32_t k = 0; k < g->n_edges; k++) {
-      bool m = (es[k] == a && ed[k] == b) || (!g->directed && es[k] == b && ed[k] == a);
-      if (m) { if (count == 0) found = k; count++; }
+    for (const Adj& x : adj[a]) {
+      if (x.to == b) { if (count == 0) found = x.edge; count++; }
     }
     if (count == 0) return -1;
     if (count > 1) return -2;
@@ -581,71 +608,156 @@ int routes(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, u
       }
     return 0;
   }
-  // adjacency as petgraph iterates it: directed -> outgoing; undirected -> both, with
-  // self-loops once
-  std::vector<std::vector<Adj>> adj(V);
-  for (uint32_t k = 0; k < g->n_edges; k++) {
-    adj[es[k]].push_back({ed[k], k});
-    if (!g->directed && es[k] != ed[k]) adj[ed[k]].push_back({es[k], k});
-  }
-  std::vector<PathProp> score(V);
-  std::vector<char> has(V), visited(V);
+  threads = std::max(1, std::min<int>(threads, (int)std::max<uint32_t>(1, U)));
   struct HeapEnt {
     PathProp s;
     uint32_t node;
   };
   auto cmp = [](const HeapEnt& a, const HeapEnt& b) { return path_less(b.s, a.s); };
-  for (uint32_t si = 0; si < U; si++) {
-    uint32_t src = uidx[si];
-    std::fill(has.begin(), has.end(), 0);
-    std::fill(visited.begin(), visited.end(), 0);
-    std::priority_queue<HeapEnt, std::vector<HeapEnt>, decltype(cmp)> heap(cmp);
-    score[src] = {0, 0.0f};
-    has[src] = 1;
-    heap.push({score[src], src});
-    while (!heap.empty()) {
-      HeapEnt top = heap.top();
-      heap.pop();
-      uint32_t node = top.node;
-      if (visited[node]) continue;
-      for (const Adj& a : adj[node]) {
-        uint32_t next = a.to;
-        if (visited[next]) continue;
-        PathProp ew{g->edge_latency_ns[a.edge], g->edge_loss[a.edge]};
-        PathProp ns = path_add(top.s, ew);
-        if (has[next]) {
-          if (path_less(ns, score[next])) {
-            score[next] = ns;
-            heap.push({ns, next});
+  std::atomic<uint32_t> next_src{0};
+  std::atomic<int> disconnected{-1};  // a source with an unreachable used node
+  std::mutex merge_mu;
+  std::unordered_map<uint64_t, PathProp> paths;  // faithful: (src NodeIndex, dst NodeIndex)
+  if (faithful) paths.reserve((size_t)U * U);
+  auto worker = [&](int) {
+    // dense per-thread buffers (CPU-optimised form)
+    std::vector<PathProp> score(faithful ? 0 : V);
+    std::vector<char> has(faithful ? 0 : V), visited(V);
+    while (true) {
+      const uint32_t si = next_src.fetch_add(1);
+      if (si >= U || disconnected.load() >= 0) break;
+      const uint32_t src = uidx[si];
+      std::fill(visited.begin(), visited.end(), 0);
+      std::priority_queue<HeapEnt, std::vector<HeapEnt>, decltype(cmp)> heap(cmp);
+      if (faithful) {
+        // petgraph::algo::dijkstra: scores in a HashMap, visited in a bit set
+        std::unordered_map<uint32_t, PathProp> sc;
+        sc[src] = {0, 0.0f};
+        heap.push({{0, 0.0f}, src});
+        while (!heap.empty()) {
+          HeapEnt top = heap.top();
+          heap.pop();
+          const uint32_t node = top.node;
+          if (visited[node]) continue;
+          for (const Adj& a : adj[node]) {
+            const uint32_t nx = a.to;
+            if (visited[nx]) continue;
+            const PathProp ns = path_add(top.s, {g->edge_latency_ns[a.edge], g->edge_loss[a.edge]});
+            auto it = sc.find(nx);
+            if (it != sc.end()) {
+              if (path_less(ns, it->second)) {
+                it->second = ns;
+                heap.push({ns, nx});
+              }
+            } else {
+              sc.emplace(nx, ns);
+              heap.push({ns, nx});
+            }
           }
-        } else {
-          has[next] = 1;
-          score[next] = ns;
-          heap.push({ns, next});
+          visited[node] = 1;
         }
+        // .filter(|(dst, _)| nodes.contains(dst)).map(...).collect::<HashMap<_, _>>()
+        std::unordered_map<uint64_t, PathProp> mine;
+        for (const auto& kv : sc)
+          if (std::find(uidx.begin(), uidx.end(), kv.first) != uidx.end())
+            mine.emplace(((uint64_t)src << 32) | kv.first, kv.second);
+        std::lock_guard<std::mutex> lk(merge_mu);  // rayon's collect of the flat_map
+        paths.insert(mine.begin(), mine.end());
+        continue;
       }
-      visited[node] = 1;
-    }
-    for (uint32_t dj = 0; dj < U; dj++) {
-      uint32_t dst = uidx[dj];
-      if (!has[dst]) {
-        set_err(err, err_len, "used nodes " + std::to_string(used[si]) + " -> " +
-                                  std::to_string(used[dj]) + " are not connected");
-        return SGN_EINVAL;
+      score[src] = {0, 0.0f};
+      std::fill(has.begin(), has.end(), 0);
+      has[src] = 1;
+      heap.push({score[src], src});
+      while (!heap.empty()) {
+        HeapEnt top = heap.top();
+        heap.pop();
+        const uint32_t node = top.node;
+        if (visited[node]) continue;
+        for (const Adj& a : adj[node]) {
+          const uint32_t nx = a.to;
+          if (visited[nx]) continue;
+          const PathProp ns = path_add(top.s, {g->edge_latency_ns[a.edge], g->edge_loss[a.edge]});
+          if (has[nx]) {
+            if (path_less(ns, score[nx])) {
+              score[nx] = ns;
+              heap.push({ns, nx});
+            }
+          } else {
+            has[nx] = 1;
+            score[nx] = ns;
+            heap.push({ns, nx});
+          }
+        }
+        visited[node] = 1;
       }
-      lat_out[(size_t)si * U + dj] = score[dst].lat;
-      loss_out[(size_t)si * U + dj] = score[dst].loss;
+      for (uint32_t dj = 0; dj < U; dj++) {
+        const uint32_t dst = uidx[dj];
+        if (!has[dst]) {
+          int expect = -1;
+          disconnected.compare_exchange_strong(expect, (int)si);
+          break;
+        }
+        lat_out[(size_t)si * U + dj] = score[dst].lat;
+        loss_out[(size_t)si * U + dj] = score[dst].loss;
+      }
     }
+  };
+  par_for_threads(threads, worker);
+  // assert_eq!(paths.len(), nodes.len().pow(2)) fails for a disconnected graph
+  if (disconnected.load() >= 0 || (faithful && paths.size() != (size_t)U * U)) {
+    // cold path: name the first (source, destination) pair in used-node order that has no path
+    for (uint32_t si = 0; si < U; si++) {
+      std::vector<char> seen(V, 0);
+      std::vector<uint32_t> st{uidx[si]};
+      seen[uidx[si]] = 1;
+      while (!st.empty()) {
+        const uint32_t x = st.back();
+        st.pop_back();
+        for (const Adj& e : adj[x])
+          if (!seen[e.to]) { seen[e.to] = 1; st.push_back(e.to); }
+      }
+      for (uint32_t dj = 0; dj < U; dj++)
+        if (!seen[uidx[dj]]) {
+          set_err(err, err_len, "used nodes " + std::to_string(used[si]) + " -> " +
+                                    std::to_string(used[dj]) + " are not connected");
+          return SGN_EINVAL;
+        }
+    }
+    set_err(err, err_len, "used nodes are not connected");
+    return SGN_EINVAL;
   }
   // the self-loop replaces the zero-length path (graph/mod.rs:209-215)
+  std::vector<PathProp> self(U);
   for (uint32_t i = 0; i < U; i++) {
-    PathProp p;
-    int rc = edge_weight(uidx[i], uidx[i], &p);
+    int rc = edge_weight(uidx[i], uidx[i], &self[i]);
     if (rc) return edge_err(rc, uidx[i], uidx[i]);
-    lat_out[(size_t)i * U + i] = p.lat;
-    loss_out[(size_t)i * U + i] = p.loss;
+  }
+  if (faithful) {
+    for (uint32_t i = 0; i < U; i++) paths[((uint64_t)uidx[i] << 32) | uidx[i]] = self[i];
+    // to_ids: NodeIndex -> GML id, re-collected (core/sim_config.rs:423-445)
+    std::unordered_map<uint64_t, PathProp> by_id;
+    by_id.reserve(paths.size());
+    for (const auto& kv : paths)
+      by_id.emplace(((uint64_t)g->node_id[kv.first >> 32] << 32) | g->node_id[(uint32_t)kv.first], kv.second);
+    for (uint32_t i = 0; i < U; i++)
+      for (uint32_t j = 0; j < U; j++) {
+        const PathProp& p = by_id.at(((uint64_t)used[i] << 32) | used[j]);
+        lat_out[(size_t)i * U + j] = p.lat;
+        loss_out[(size_t)i * U + j] = p.loss;
+      }
+    return 0;
+  }
+  for (uint32_t i = 0; i < U; i++) {
+    lat_out[(size_t)i * U + i] = self[i].lat;
+    loss_out[(size_t)i * U + i] = self[i].loss;
   }
   return 0;
+}
+
+int routes(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, uint64_t* lat_out,
+           float* loss_out, char* err, size_t err_len) {
+  return routes_mode(g, used, U, shortest, 0, 1, lat_out, loss_out, err, err_len);
 }
 
 // ------------------------------------------------------------------------------------
@@ -856,6 +968,9 @@ struct Event {
   uint64_t eid;       // packets: src host's event id; locals: own event id
   int task;
   Pkt pkt;
+  // reference-faithful mode: the destination's own heap copy of the packet
+  // (PacketRc::new_copy_inner, worker.rs:397-398); unused by the optimised mode
+  std::shared_ptr<Pkt> copy;
 };
 
 // Event ordering: time, then Packet < Local, then (src host, src event id) for packets or
@@ -905,6 +1020,60 @@ struct Host {
 
 }  // namespace
 
+// A persistent worker pool with one start/finish rendezvous per round, as the reference's
+// thread-per-core scheduler (lib/scheduler/src/thread_per_core.rs:29-74,159-212: threads live
+// for the whole simulation, spin briefly and then park between rounds). run(f) calls f(t)
+// on every thread t (t = 0 on the caller) and returns when all have finished.
+struct Pool {
+  int n = 1;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<int> pending{0};
+  std::atomic<bool> stop{false};
+  std::function<void(int)> job;
+
+  explicit Pool(int nt) : n(nt) {
+    for (int t = 1; t < n; t++) th.emplace_back([this, t] { loop(t); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+      gen++;
+    }
+    cv.notify_all();
+    for (auto& x : th) x.join();
+  }
+  void loop(int t) {
+    uint64_t seen = 0;
+    while (true) {
+      for (int spin = 0; spin < 20000 && gen.load(std::memory_order_acquire) == seen; spin++)
+        __builtin_ia32_pause();
+      if (gen.load(std::memory_order_acquire) == seen) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return gen.load() != seen; });
+      }
+      seen = gen.load(std::memory_order_acquire);
+      if (stop.load()) return;
+      job(t);
+      pending.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  void run(const std::function<void(int)>& f) {
+    job = f;
+    pending.store(n - 1);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    cv.notify_all();
+    f(0);
+    while (pending.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+  }
+};
+
 // Per-thread worker state, as the reference's thread-local Worker (core/worker.rs): the
 // current time, this round's counters, trace records and exports, and the lowest used
 // latency seen (Worker::update_lowest_used_latency); merged at the round barrier.
@@ -916,6 +1085,9 @@ struct Wk {
   std::vector<sgn_drain_rec> dr;  // EXTERNAL: datagram fates for the CPU-side apps
   bool min_set = false;
   uint64_t min_used = 0;
+  // this round's minimum over the executed hosts' next event times and the deliveries this
+  // thread produced (core/manager.rs:580-599, Worker::update_next_event_time)
+  uint64_t next_min = EMU_INVALID;
 };
 static thread_local Wk* tl_wk = nullptr;
 
@@ -942,6 +1114,21 @@ struct ora_sim {
   int nthreads = 1;
   std::vector<Wk> wks = std::vector<Wk>(1);
   std::unique_ptr<std::mutex[]> qmu;
+  std::unique_ptr<Pool> pool;
+  uint64_t round_next_min = EMU_INVALID;  // min next event time after the last round
+  // reference-faithful mode (CPU baseline): the reference's hash-map lookups per packet
+  // (IpAssignment::get_node x6, RoutingInfo::path x2, Dns, the event-queue map), the global
+  // packet-counter write lock (RoutingInfo::increment_packet_count, graph/mod.rs:450-458,
+  // worker.rs:379), a heap copy of every packet and a lock around every queue operation.
+  // Results are identical to the optimised mode (tests/test_oracle_threads.py).
+  bool faithful = false;
+  std::unordered_map<uint32_t, uint32_t> ip_node;         // IpAddr -> GML node id
+  std::unordered_map<uint64_t, PathProp> route_map;       // (src node, dst node) -> path
+  std::unordered_map<uint64_t, uint64_t> packet_counters; // (src node, dst node) -> packets
+  std::shared_mutex counters_mu;
+  std::unordered_map<uint32_t, std::mutex*> queue_map;    // HostId -> its queue's lock
+  bool locked() const { return nthreads > 1 || faithful; }
+  std::mutex& qlock(uint32_t host) { return faithful ? *queue_map.at(host) : qmu[host]; }
   Wk& W() { return *tl_wk; }
   sgn_stats st;
   bool trace = false;
@@ -1008,8 +1195,8 @@ struct ora_sim {
     ev.eid = h.eid_ctr++;
     ev.task = task;
     if (t >= end_time) return;
-    if (nthreads > 1) {
-      std::lock_guard<std::mutex> g(qmu[h.id]);
+    if (locked()) {
+      std::lock_guard<std::mutex> g(qlock(h.id));
       h.q.push(ev);
     } else {
       h.q.push(ev);
@@ -1074,7 +1261,13 @@ struct ora_sim {
     uint32_t dst = it->second;
     size_t ri = (size_t)h.unode * U + hosts[dst].unode;
     // reliability = 1.0f32 - loss, widened to f64 (:363-365, :532-537)
-    float rel32 = 1.0f - loss[ri];
+    float rel32;
+    if (faithful) {  // WorkerShared::reliability: get_node x2 + RoutingInfo::path
+      const uint32_t a = ip_node.at(h.ip), b = ip_node.at(p.dst_ip);
+      rel32 = 1.0f - route_map.at(((uint64_t)a << 32) | b).loss;
+    } else {
+      rel32 = 1.0f - loss[ri];
+    }
     double reliability = (double)rel32;
     double chance = h.rng.next_f64();  // :366
     if (!bootstrapping && chance >= reliability && p.payload > 0) {  // :371
@@ -1084,7 +1277,19 @@ struct ora_sim {
       if (external()) drain_rec(h, SGN_DRAIN_LOSS, h.id, dst, 0, p.payload, p.tag);
       return;
     }
-    uint64_t delay = lat[ri];  // :376
+    uint64_t delay;
+    if (faithful) {
+      // WorkerShared::latency (:376): get_node x2 + path; increment_packet_count (:379):
+      // get_node x2 + the global write lock (graph/mod.rs:450-458)
+      const uint32_t a = ip_node.at(h.ip), b = ip_node.at(p.dst_ip);
+      delay = route_map.at(((uint64_t)a << 32) | b).lat;
+      const uint32_t c = ip_node.at(h.ip), d = ip_node.at(p.dst_ip);
+      std::unique_lock<std::shared_mutex> g(counters_mu);
+      uint64_t& cnt = packet_counters[((uint64_t)c << 32) | d];
+      cnt = cnt == ~0ULL ? cnt : cnt + 1;
+    } else {
+      delay = lat[ri];  // :376
+    }
     // Worker::update_lowest_used_latency -> Runahead (runahead.rs:61-107), dynamic only
     if (cfg.use_dynamic_runahead && (!W().min_set || delay < W().min_used)) {
       W().min_set = true;
@@ -1094,6 +1299,7 @@ struct ora_sim {
     h.n_sent++;
     uint64_t deliver = W().now + delay;  // :387-390
     if (deliver < round_end) deliver = round_end;
+    W().next_min = std::min(W().next_min, deliver);  // Worker::update_next_event_time (:394)
     // push_packet_to_host (:603-613): Event::new_packet consumes the SOURCE host's id
     Event ev;
     ev.time = deliver;
@@ -1107,7 +1313,12 @@ struct ora_sim {
     trace_rec(h, SGN_TRACE_SEND, dst, 0, W().now, deliver, ev.eid);
     if (owned(dst)) {
       Host& d = hosts[dst];
-      if (nthreads > 1) {
+      if (faithful) {
+        ev.copy = std::make_shared<Pkt>(p);  // PacketRc::new_copy_inner (:397-398)
+        std::lock_guard<std::mutex> g(*queue_map.at(dst));  // event_queues.get(dst).lock()
+        if (ev.time < d.last_popped) std::abort();  // event_queue.rs:59
+        d.q.push(std::move(ev));
+      } else if (nthreads > 1) {
         std::lock_guard<std::mutex> g(qmu[dst]);
         if (ev.time < d.last_popped) std::abort();  // event_queue.rs:59
         d.q.push(ev);
@@ -1247,7 +1458,7 @@ struct ora_sim {
     // (pop under the host's own queue lock in threaded mode: other hosts push into it)
     auto pop_due = [&](Event* out) {
       std::unique_lock<std::mutex> g;
-      if (nthreads > 1) g = std::unique_lock<std::mutex>(qmu[h.id]);
+      if (locked()) g = std::unique_lock<std::mutex>(qlock(h.id));
       if (h.q.empty() || h.q.top().time >= until) return false;
       *out = h.q.top();
       h.q.pop();
@@ -1310,26 +1521,38 @@ struct ora_sim {
     st.rounds++;
   }
 
+  // Host::next_event_time (host.rs:832-834), under the queue's lock when others may push
+  uint64_t host_next(Host& h) {
+    std::unique_lock<std::mutex> g;
+    if (locked()) g = std::unique_lock<std::mutex>(qlock(h.id));
+    return h.q.empty() ? EMU_INVALID : h.q.top().time;
+  }
+
+  // One round on the worker threads (core/manager.rs:568-601): each thread executes hosts
+  // (taken in chunks from a shared counter) and keeps the minimum of their next event times
+  // and of the deliveries it produced; the minima are reduced after the barrier (:623-628).
   void execute_round() {
     round_end = we;  // Worker::set_round_end_time (manager.rs:578)
-    if (nthreads <= 1) {
-      tl_wk = &wks[0];
-      for (uint32_t i = lo; i < hi; i++) execute(hosts[i], we);
-    } else {
-      std::atomic<uint32_t> next{lo};
-      auto worker = [&](int t) {
-        tl_wk = &wks[t];
-        while (true) {
-          const uint32_t a = next.fetch_add(256);
-          if (a >= hi) break;
-          const uint32_t e = std::min<uint32_t>(hi, a + 256);
-          for (uint32_t i = a; i < e; i++) execute(hosts[i], we);
+    std::atomic<uint32_t> next{lo};
+    auto worker = [&](int t) {
+      tl_wk = &wks[t];
+      Wk& w = wks[t];
+      w.next_min = EMU_INVALID;  // Worker::reset_next_event_time (worker.rs:310)
+      while (true) {
+        const uint32_t a = next.fetch_add(256);
+        if (a >= hi) break;
+        const uint32_t e = std::min<uint32_t>(hi, a + 256);
+        for (uint32_t i = a; i < e; i++) {
+          execute(hosts[i], we);
+          w.next_min = std::min(w.next_min, host_next(hosts[i]));
         }
-      };
-      std::vector<std::thread> th;
-      for (int t = 1; t < nthreads; t++) th.emplace_back(worker, t);
+      }
+    };
+    if (nthreads <= 1) {
       worker(0);
-      for (auto& x : th) x.join();
+    } else {
+      if (!pool || pool->n != nthreads) pool.reset(new Pool(nthreads));
+      pool->run(worker);
       tl_wk = &wks[0];
     }
     merge_workers();
@@ -1337,7 +1560,9 @@ struct ora_sim {
 
   // the round barrier (manager.rs:623-628): fold the workers' counters and minima
   void merge_workers() {
+    round_next_min = EMU_INVALID;
     for (Wk& w : wks) {
+      round_next_min = std::min(round_next_min, w.next_min);
       st.packets_sent += w.st.packets_sent;
       st.packets_loss_dropped += w.st.packets_loss_dropped;
       st.packets_unknown_dst += w.st.packets_unknown_dst;
@@ -1693,8 +1918,33 @@ int ora_sim_set_threads(ora_sim* s, int n) {
   if (n < 1 || n > 1024) return SGN_EINVAL;
   s->nthreads = n;
   s->wks.assign(n, Wk());
+  s->pool.reset();
   if (n > 1 && !s->qmu) s->qmu.reset(new std::mutex[s->hosts.size()]);
   return 0;
+}
+
+// Reference-faithful (1) or CPU-optimised (0) data structures; results are identical.
+int ora_sim_set_faithful(ora_sim* s, int on) {
+  s->faithful = on != 0;
+  if (!s->faithful) return 0;
+  if (!s->qmu) s->qmu.reset(new std::mutex[s->hosts.size()]);
+  s->ip_node.clear();
+  s->route_map.clear();
+  s->queue_map.clear();
+  for (const Host& h : s->hosts) {
+    s->ip_node[h.ip] = s->used[h.unode];            // IpAssignment (graph/mod.rs:348-418)
+    s->queue_map[h.id] = &s->qmu[h.id];             // WorkerShared::event_queues
+  }
+  for (uint32_t i = 0; i < s->U; i++)              // RoutingInfo::paths (graph/mod.rs:430)
+    for (uint32_t j = 0; j < s->U; j++)
+      s->route_map[((uint64_t)s->used[i] << 32) | s->used[j]] = {s->lat[(size_t)i * s->U + j],
+                                                                s->loss[(size_t)i * s->U + j]};
+  return 0;
+}
+
+int ora_routes_mode(const sgn_graph* g, const uint32_t* used, uint32_t U, int shortest, int faithful,
+                    int threads, uint64_t* lat, float* loss, char* err, size_t err_len) {
+  return routes_mode(g, used, U, shortest, faithful, threads, lat, loss, err, err_len);
 }
 
 int ora_sim_window(const ora_sim* s, uint64_t* start, uint64_t* end, int32_t* active) {
@@ -1707,7 +1957,8 @@ int ora_sim_window(const ora_sim* s, uint64_t* start, uint64_t* end, int32_t* ac
 int ora_sim_round(ora_sim* s, uint64_t* min_next) {
   if (!s->active) return SGN_ESTATE;
   s->execute_round();
-  uint64_t m = s->local_min_next();
+  // the threads' minima (manager.rs:623-628); sharded runs use the shard protocol instead
+  uint64_t m = s->round_next_min;
   if (m == EMU_INVALID) m = EMU_MAX;  // unwrap_or(EmulatedTime::MAX) (manager.rs:628)
   if (min_next) *min_next = m;
   s->advance(m);

@@ -81,6 +81,13 @@ int ora_routes(const sgn_graph* g, const uint32_t* used_node_ids, uint32_t n_use
                int use_shortest_path, uint64_t* lat_out, float* loss_out, char* err,
                size_t err_len);
 
+/* The same with the reference's data structures (faithful != 0: hash-map scores, the O(U)
+ * contains filter, hashed U^2 output and re-collect) or dense arrays (0), on `threads` worker
+ * threads (rayon over sources). Identical results. */
+int ora_routes_mode(const sgn_graph* g, const uint32_t* used_node_ids, uint32_t n_used,
+                    int use_shortest_path, int faithful, int threads, uint64_t* lat_out,
+                    float* loss_out, char* err, size_t err_len);
+
 /* ---- the round loop (core/manager.rs:541-656 and everything it calls) ---- */
 typedef struct ora_sim ora_sim;
 /* route table as produced by ora_routes for used_node_ids (U x U) */
@@ -89,6 +96,10 @@ int ora_sim_create(const uint32_t* used_node_ids, uint32_t n_used, const uint64_
                    const sgn_traffic* traffic, int trace, ora_sim** out, char* err,
                    size_t err_len);
 void ora_sim_free(ora_sim* s);
+/* Worker threads of the round loop (a persistent pool, one rendezvous per round). */
+int ora_sim_set_threads(ora_sim* s, int n);
+/* Reference-faithful per-packet data structures (1) or the CPU-optimised ones (0). */
+int ora_sim_set_faithful(ora_sim* s, int on);
 int ora_sim_window(const ora_sim* s, uint64_t* start, uint64_t* end, int32_t* active);
 int ora_sim_round(ora_sim* s, uint64_t* min_next);
 int ora_sim_run(ora_sim* s, uint64_t max_rounds, uint64_t* rounds_done);

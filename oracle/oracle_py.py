@@ -67,6 +67,9 @@ def load():
                                      C.POINTER(vp), C.c_char_p, C.c_size_t]),
         "ora_sim_free": (None, [vp]),
         "ora_sim_set_threads": (C.c_int, [vp, C.c_int]),
+        "ora_sim_set_faithful": (C.c_int, [vp, C.c_int]),
+        "ora_routes_mode": (C.c_int, [C.POINTER(sgn.Graph), u32p, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                      u64p, f32p, C.c_char_p, C.c_size_t]),
         "ora_sim_window": (C.c_int, [vp, u64p, u64p, C.POINTER(C.c_int32)]),
         "ora_sim_round": (C.c_int, [vp, u64p]),
         "ora_sim_run": (C.c_int, [vp, C.c_uint64, u64p]),
@@ -108,7 +111,10 @@ class CodelState(C.Structure):
                                           "dropped_total")]
 
 
-def routes(g: sgn.GraphArrays, used, shortest=True):
+def routes(g: sgn.GraphArrays, used, shortest=True, faithful=False, threads=1):
+    """compute_shortest_paths / get_direct_paths (network/graph/mod.rs:181-250) -> dense U x U
+    (latency u64, loss f32). faithful: the reference's hash-map data structures; threads:
+    sources in parallel (rayon). Identical results in every mode."""
     L = load()
     used = np.ascontiguousarray(used, dtype=np.uint32)
     U = len(used)
@@ -116,8 +122,9 @@ def routes(g: sgn.GraphArrays, used, shortest=True):
     loss = np.zeros(U * U, dtype=np.float32)
     err = C.create_string_buffer(512)
     gs = g.struct()
-    rc = L.ora_routes(C.byref(gs), sgn.ptr(used, C.c_uint32), U, 1 if shortest else 0,
-                      sgn.ptr(lat, C.c_uint64), sgn.ptr(loss, C.c_float), err, 512)
+    rc = L.ora_routes_mode(C.byref(gs), sgn.ptr(used, C.c_uint32), U, 1 if shortest else 0,
+                           1 if faithful else 0, threads, sgn.ptr(lat, C.c_uint64),
+                           sgn.ptr(loss, C.c_float), err, 512)
     if rc != 0:
         raise sgn.SgnError(rc, err.value.decode())
     return lat.reshape(U, U), loss.reshape(U, U)
@@ -162,7 +169,8 @@ def host_seeds(sim_seed, names):
 class Sim:
     """The reference-structured round loop (core/manager.rs:541-656) on the CPU."""
 
-    def __init__(self, used, lat, loss, hosts: sgn.HostArrays, cfg, traffic, trace=False, threads=1):
+    def __init__(self, used, lat, loss, hosts: sgn.HostArrays, cfg, traffic, trace=False, threads=1,
+                 faithful=False):
         self.L = load()
         used = np.ascontiguousarray(used, dtype=np.uint32)
         lat = np.ascontiguousarray(lat, dtype=np.uint64).ravel()
@@ -179,6 +187,14 @@ class Sim:
         self.n = hosts.n
         if threads != 1:
             assert self.L.ora_sim_set_threads(self.h, threads) == 0
+        if faithful:
+            assert self.L.ora_sim_set_faithful(self.h, 1) == 0
+
+    def set_threads(self, n):
+        assert self.L.ora_sim_set_threads(self.h, n) == 0
+
+    def set_faithful(self, on):
+        assert self.L.ora_sim_set_faithful(self.h, 1 if on else 0) == 0
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -39,12 +39,14 @@ void* dev_alloc(sgn_ctx* ctx, size_t bytes, bool zero) {
     return nullptr;
   }
   ctx->allocs.push_back(p);
+  ctx->sim_bytes += bytes;
   return p;
 }
 
 }  // namespace sgn
 
 sgn_ctx::~sgn_ctx() {
+  for (sgn_stage* st : stages) st->ctx = nullptr;  // the caller still owns (and destroys) them
   sgn::free_sim(this);
   if (d_lat) hipFree(d_lat);
   if (d_loss) hipFree(d_loss);

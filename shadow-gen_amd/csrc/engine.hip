@@ -14,7 +14,7 @@
 //            round (controller.rs:88-112) — run by the last wave to arrive
 // Kernels: k_rounds (single shard, persistent: up to 128 rounds per launch with an atomic
 // grid barrier per round), k_execute (one round per launch: sgn_round, multi-shard) with
-// k_finalize / k_import / k_advance around the RCCL exchange (comm.cpp), k_inject
+// k_import / k_advance around the RCCL exchange (comm.cpp), k_inject
 // (sgn_submit), k_rng (sgn_rng_*). The window lives in device memory (Ctrl), so rounds run
 // back to back without a host round trip.
 //
@@ -210,6 +210,7 @@ struct Outbox {
   uint32_t idx[OBOX];  // (slab set, group) slab index
   uint32_t n;          // records appended (may exceed OBOX: those were placed directly)
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
+  uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
 };
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
@@ -1007,6 +1008,10 @@ struct HostExec {
     uint32_t pos;
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
+      if (deliver >= ob->hz) {  // past the calendar's horizon (sim_init sizes NB so it cannot be)
+        overflow(OVF_HORIZON);
+        return;
+      }
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
@@ -1314,61 +1319,6 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return (uint32_t)__popcll(lane ? (m & ((~0ULL) >> (64 - lane))) : 0ULL);
 }
 
-// Round edge on one workgroup (any multiple of 64 threads): bucket bookkeeping, the local
-// minimum next event time over the waves' slots and the calendar, and (advance != 0, single
-// shard) Controller::manager_finished_current_round. sh: LDS scratch of >= 16 u64.
-__device__ void finalize_round(const DevSim& S, uint64_t* sh, int advance) {
-  Ctrl* C = S.ctrl;
-  // the waves' minima: events kept in the spare slab, and next local events
-  uint64_t kk = INVALID, wn = INVALID;
-  for (uint32_t g = threadIdx.x; g < S.G; g += blockDim.x) {
-    const uint64_t a = S.w_keep[g], b = S.w_next[g];
-    kk = a < kk ? a : kk;
-    wn = b < wn ? b : wn;
-  }
-  kk = block_min_u64(kk, sh);
-  wn = block_min_u64(wn, sh);
-  if (threadIdx.x == 0) {
-    const uint32_t b0 = bucket_of(S, C->ws), b1 = bucket_of(S, C->we - 1);
-    for (uint32_t b = b0; b != b1; b = (b + 1) & (S.NB - 1)) S.bucket_min[b] = INVALID;  // consumed
-    // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
-    const uint32_t old = S.bucket_slab[b1];
-    S.bucket_slab[b1] = C->keep_slab;
-    C->keep_slab = old;
-    S.bucket_min[b1] = C->keep_min < kk ? C->keep_min : kk;
-    C->keep_min = INVALID;
-  }
-  __syncthreads();
-  uint64_t m = INVALID;
-  for (uint32_t b = threadIdx.x; b < S.NB; b += blockDim.x) {
-    const uint64_t bm = S.bucket_min[b];
-    m = bm < m ? bm : m;
-  }
-  m = block_min_u64(m, sh);
-  if (threadIdx.x == 0) {
-    m = wn < m ? wn : m;
-    m = C->round_min < m ? C->round_min : m;
-    C->round_min = m;  // local minimum (reduced across shards when advance == 0)
-    if (advance) {
-      const uint64_t min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
-      C->last_min_next = min_next;
-      // Runahead::get (runahead.rs:44-57)
-      uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
-      ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
-      // Controller::manager_finished_current_round (controller.rs:88-112)
-      uint64_t ne = min_next + ra;
-      if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
-      ne = ne < S.end_time ? ne : S.end_time;
-      C->active = min_next < ne ? 1u : 0u;
-      C->prev_we = C->we;
-      C->ws = min_next;
-      C->we = ne;
-      C->round_min = INVALID;
-      C->rounds++;
-    }
-  }
-}
-
 // finalize_round for the fused single-shard path, run by the last wave of k_execute: the
 // waves' minima come from the chunk slots; every value another wave changed during this
 // launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
@@ -1448,12 +1398,6 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
   }
 }
 
-__global__ __launch_bounds__(1024) void k_finalize(DevSim S, int advance) {
-  if (!S.ctrl->active) return;
-  __shared__ uint64_t sh[16];
-  finalize_round(S, sh, advance);
-}
-
 // One wave per host group (GROUP consecutive hosts), lane = host. A round is:
 //  1. gather: the group's slabs of the window's buckets are read; runs due in the window go
 //     to LDS, the last bucket's later runs move to the spare slab (Ctrl::keep_slab);
@@ -1523,6 +1467,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   if (lane == 0) {
     ob->n = 0;
     ob->xmin = INVALID;
+    ob->hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
   }
   __syncthreads();
   HostExec ex(S, h, we, be, ks, lslot + lane, lbs, ob);
@@ -1679,10 +1624,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   m = ob->xmin < m ? ob->xmin : m;  // runs exported to other shards are pending events too
   *kmin_out = kmin;
   *next_out = m;
-  if (lane == 0) {
-    S.w_keep[g] = kmin;
-    S.w_next[g] = m;
-  }
   at_end(kmin, m);
   uint32_t n_ev = 0;
 #ifdef SGN_DIAG
@@ -1838,6 +1779,36 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   SGN_GLB Ctrl* C = S.ctrl;
   SGN_EXEC_LDS(X)
   const uint32_t w = blockIdx.x, P = gridDim.x;
+  // Residency census before any simulation state is touched: the grid barrier below needs
+  // every workgroup on the chip at once. Each workgroup counts itself in and waits (bounded)
+  // for the rest; the first to see the whole grid, or to give up, sets the verdict with a
+  // compare-and-swap, so all workgroups act on the same one. A grid that is not resident
+  // leaves untouched and the host runs the rounds with per-round launches instead.
+  {
+    __shared__ uint32_t verdict;
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(&C->res_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t v = 0, spins = 0;
+      while ((v = ld_dev(&C->res_verdict)) == 0) {
+        if (ld_dev(&C->res_arrive) >= P) {
+          v = 1;
+        } else if (++spins > (1u << 14)) {
+          v = 2;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        uint32_t expect = 0;
+        __hip_atomic_compare_exchange_strong(&C->res_verdict, &expect, v, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = ld_dev(&C->res_verdict);
+        break;
+      }
+      verdict = v;
+    }
+    __syncthreads();
+    if (verdict != 1) return;
+  }
   const uint64_t e0 = ld_dev(&C->epoch);
   // the spare slab and the bucket -> slab table change by one swap per round, the same on
   // every workgroup: each keeps its own copy (LDS) and applies the swap itself
@@ -1934,7 +1905,6 @@ __global__ void k_advance(DevSim S) {
   C->ws = min_next;
   C->we = ne;
   C->round_min = INVALID;
-  C->remote_min = INVALID;
   C->rounds++;
 }
 
@@ -1946,12 +1916,18 @@ __global__ void k_advance(DevSim S) {
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
   if (!C->active) return;
+  // the window that just ran is still C->ws (k_advance follows): the same horizon as sends
+  const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
     if (r == S.rank) continue;
     const uint32_t n = (uint32_t)min(S.xmsg_in[4 * (size_t)r], (uint64_t)S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
       const EvRec e = S.xin[(size_t)r * S.xslot + i];
+      if (e.time >= hz) {
+        if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = e.dst;
+        continue;
+      }
       const uint32_t b = bucket_of(S, e.time);
       const size_t idx = (size_t)S.bucket_slab[b] * S.G + ((e.dst - S.lo) >> S.gsh);
       const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
@@ -1990,13 +1966,18 @@ __global__ void k_inject(const DevSim* Sp, const EvRec* recs, uint32_t n) {
   atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)r.time);
 }
 
-// sgn_rng_*: n draws of one host's Xoshiro256++ stream (the state stays on the device)
-__global__ void k_rng(const DevSim* Sp, uint32_t h, uint32_t n, uint64_t* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  SGN_GLB HostRec* R = Sp->hrec + h;
+// sgn_rng_*: draws of host Xoshiro256++ streams (the state stays on the device). One thread
+// per requested host (hosts distinct, checked on the host): its count[i] draws go to
+// out[off[i] ..), in stream order.
+__global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* count,
+                      const uint64_t* off, uint32_t n, uint64_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  SGN_GLB HostRec* R = Sp->hrec + hosts[i];
   uint64_t s0 = R->rng[0], s1 = R->rng[1], s2 = R->rng[2], s3 = R->rng[3];
-  for (uint32_t i = 0; i < n; i++) {
-    out[i] = rotl64(s0 + s3, 23) + s0;
+  uint64_t* o = out + off[i];
+  for (uint32_t k = 0; k < count[i]; k++) {
+    o[k] = rotl64(s0 + s3, 23) + s0;
     const uint64_t t = s1 << 17;
     s2 ^= s0;
     s3 ^= s1;
@@ -2009,6 +1990,34 @@ __global__ void k_rng(const DevSim* Sp, uint32_t h, uint32_t n, uint64_t* out) {
   R->rng[1] = s1;
   R->rng[2] = s2;
   R->rng[3] = s3;
+}
+
+// Host::next_event_time (host.rs:832-834) for the owned hosts [lo, lo + n) (local indices),
+// between rounds: the earliest local event (the host record's slots) ...
+__global__ void k_next_local(const DevSim* Sp, uint32_t lo, uint32_t n, uint64_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const HostRec& r = Sp->hrec[lo + i];
+  uint64_t m = r.slot_t[0];
+  m = r.slot_t[1] < m ? r.slot_t[1] : m;
+  m = r.slot_t[2] < m ? r.slot_t[2] : m;
+  out[i] = m;
+}
+// ... and the earliest pending packet event: one wave per (bucket, host group) slab that
+// overlaps the range, atomicMin into the destination's slot. Between rounds every pending
+// event is in a bucket's slab (the spare slab set is empty).
+__global__ void k_next_packet(const DevSim* Sp, uint32_t lo, uint32_t n, uint32_t g0, uint32_t ng,
+                              uint64_t* out) {
+  const DevSim& S = *Sp;
+  const uint32_t w = blockIdx.x;  // (bucket, group) pair
+  const uint32_t b = w / ng, g = g0 + w % ng;
+  const size_t idx = (size_t)S.bucket_slab[b] * S.G + g;
+  const uint32_t fill = min(S.slab_n[idx], S.CAP);
+  for (uint32_t j = threadIdx.x; j < fill; j += blockDim.x) {
+    const EvRec& e = S.pool[idx * S.CAP + j];
+    const uint32_t d = e.dst - S.lo;
+    if (d >= lo && d < lo + n) atomicMin((unsigned long long*)&out[d - lo], (unsigned long long)e.time);
+  }
 }
 
 }  // namespace sgn
@@ -2033,8 +2042,8 @@ T* dalloc(sgn_ctx* ctx, size_t n) {
   return (T*)dev_alloc(ctx, n * sizeof(T));
 }
 
-enum { K_EXECUTE = 0, K_FINALIZE, K_IMPORT, K_ADVANCE, K_NUM };
-const char* kKernelNames[K_NUM] = {"k_execute", "k_finalize", "k_import", "k_advance"};
+enum { K_EXECUTE = 0, K_IMPORT, K_ADVANCE, K_NUM };
+const char* kKernelNames[K_NUM] = {"k_execute", "k_import", "k_advance"};
 
 int launch_round(sgn_ctx* ctx);
 
@@ -2049,6 +2058,9 @@ namespace {
 
 int launch_round(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
+  // a multi-shard round needs its exchange transport before anything is launched
+  if (ctx->nranks > 1 && !ctx->comm)
+    return set_error(ctx, SGN_ESTATE, "multi-shard round without an RCCL communicator");
   hipStream_t st = ctx->stream;
   time_begin(ctx, K_EXECUTE);
   hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(64), exec_lds_bytes(S.CAP), st, (const DevSim*)ctx->d_S);
@@ -2058,7 +2070,7 @@ int launch_round(sgn_ctx* ctx) {
     int rc = comm_round_exchange(ctx);
     if (rc) return rc;
   } else {
-    // single shard: k_execute's last wave runs the round edge (finalize_round)
+    // single shard: k_execute's last wave runs the round edge (finalize_fused)
   }
   SGN_HIP(ctx, hipGetLastError());
   ctx->rounds_enqueued++;
@@ -2075,6 +2087,7 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow & OVF_EXCHANGE) what += " exchange slot (raise exchange_slot_events)";
   if (c.overflow & OVF_TRACE) what += " trace buffer";
   if (c.overflow & OVF_TIMEOUT) what += " persistent grid barrier timed out (grid not resident)";
+  if (c.overflow & OVF_HORIZON) what += " event calendar horizon (a delivery beyond the calendar's buckets)";
   if (c.overflow & OVF_DRAIN) what += " drain buffer (raise sgn_drain_enable's capacity or drain more often)";
   return set_error(ctx, SGN_EOVERFLOW,
                    "device capacity exceeded:" + what + " (info " +
@@ -2096,8 +2109,8 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
   ctx->graph_timed.clear();
   if (!all && !exec) return 0;
-  const void* fn[K_NUM] = {(const void*)k_execute, (const void*)k_finalize,
-                           (const void*)k_import, (const void*)k_advance};
+  const void* fn[K_NUM] = {(const void*)k_execute, (const void*)k_import,
+                           (const void*)k_advance};
   size_t n = 0;
   SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
   std::vector<hipGraphNode_t> nodes(n);
@@ -2199,6 +2212,7 @@ void free_sim(sgn_ctx* ctx) {
   ctx->graph_pending = false;
   for (void* p : ctx->allocs) hipFree(p);
   ctx->allocs.clear();
+  ctx->sim_bytes = 0;
   if (ctx->d_stage) hipFree(ctx->d_stage);
   ctx->d_stage = nullptr;
   ctx->stage_cap = 0;
@@ -2357,7 +2371,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least
   // one bucket, and in dynamic mode possibly many (executed bucket by bucket).
   uint64_t BW = std::max<uint64_t>(1, std::max(min_possible, cfg->runahead_ns));
-  uint64_t NB = max_lat / BW + 4;
+  // Every pending event lies in [ws, we + max_lat): sends happen before the window end and
+  // arrive at most max_lat later (worker.rs:386-390). A static window is BW long; a dynamic
+  // one is max(min used latency, configured runahead) (runahead.rs:44-57), i.e. up to
+  // max(max_lat, runahead). The calendar spans that plus one partial bucket at each end;
+  // send_batch checks the horizon on the device (OVF_HORIZON), so a violation is reported.
+  const uint64_t wmax = cfg->use_dynamic_runahead ? std::max<uint64_t>(BW, std::max(max_lat, cfg->runahead_ns)) : BW;
+  uint64_t NB = (wmax + max_lat) / BW + 4;
   if (NB > (1u << 20)) return set_error(ctx, SGN_EINVAL, "calendar would need > 2^20 buckets");
   while (NB & (NB - 1)) NB += NB & (~NB + 1);  // round up to a power of two
   // hosts per k_execute wave: fewer than 64 spreads the (divergent, per-lane serial) host
@@ -2377,10 +2397,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.BW = BW;
   S.bw_div.init(BW);
   S.pool = (decltype(S.pool))dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
-  S.w_next = (decltype(S.w_next))dalloc<uint64_t>(ctx, G);
-  S.w_keep = (decltype(S.w_keep))dalloc<uint64_t>(ctx, G);
   S.w_cnt = (decltype(S.w_cnt))dalloc<uint64_t>(ctx, W_N * G);
-  if (!S.w_next || !S.w_keep || !S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
+  if (!S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
   S.slab_n = (decltype(S.slab_n))dalloc<uint32_t>(ctx, (NB + 1) * G);
   if (!S.pool || !S.slab_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (event calendar)");
   std::vector<uint32_t> bslab(NB);
@@ -2440,7 +2458,6 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.keep_slab = (uint32_t)NB;
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
-  c.remote_min = INVALID;
   c.prev_we = SIM_START;
   S.ctrl = (decltype(S.ctrl))dalloc<Ctrl>(ctx, 1);
   if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
@@ -2467,6 +2484,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       // test hook: a smaller grid makes every workgroup serve several groups per round
       if (const char* e = getenv("SGN_PERSIST_GRID"))
         ctx->persist_grid = std::max<uint32_t>(1, std::min<uint32_t>(ctx->persist_grid, (uint32_t)atoi(e)));
+      // test hook: an oversized grid (not resident) exercises the residency census fallback
+      if (const char* e = getenv("SGN_PERSIST_GRID_FORCE")) ctx->persist_grid = (uint32_t)atoi(e);
     }
   }
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
@@ -2497,6 +2516,8 @@ int sgn_window(sgn_ctx* ctx, uint64_t* start, uint64_t* end, int32_t* active) {
 
 int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
   if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  if (ctx->comm_local)
+    return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_round");
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
   if (!ctx->h_ctrl->active) return set_error(ctx, SGN_ESTATE, "simulation already finished");
@@ -2508,6 +2529,8 @@ int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
 
 int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  if (ctx->comm_local)
+    return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_run");
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
   const uint64_t r_start = ctx->h_ctrl->rounds;
@@ -2519,15 +2542,29 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   const bool graph = ctx->nranks == 1 && ctx->use_graph;
   if (ctx->nranks == 1 && ctx->persist_grid) {
     // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside)
-    while (ctx->h_ctrl->active && enq < max_rounds) {
+    while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
+      SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
       time_begin(ctx, K_EXECUTE);
       hipLaunchKernelGGL(k_rounds, dim3(ctx->persist_grid), dim3(64), exec_lds_bytes(ctx->S.CAP),
                          ctx->stream, (const DevSim*)ctx->d_S, n);
       time_end(ctx);
       SGN_HIP(ctx, hipGetLastError());
-      enq += n;
       if ((rc = sync_ctrl(ctx))) return rc;
+      if (ctx->h_ctrl->res_verdict != 1) {
+        // the grid was not resident (the occupancy model was wrong, or another context holds
+        // part of the GPU): nothing ran; continue with one launch per round
+        ctx->persist_grid = 0;
+        ctx->persist_fallbacks++;
+        break;
+      }
+      enq += n;
+    }
+    if (!ctx->persist_grid) {
+      uint64_t more = 0;
+      rc = sgn_run(ctx, max_rounds - enq, &more);
+      if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
+      return rc;
     }
     if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
     return 0;
@@ -2643,35 +2680,42 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
   return rc;
 }
 
-int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
-  if (!ctx || !t) return SGN_EINVAL;
+namespace {
+// Host::next_event_time for owned HostIds [lo, hi): two small kernels, one copy.
+int next_event_times(sgn_ctx* ctx, uint32_t lo, uint32_t hi, uint64_t* out) {
+  if (!ctx || (!out && hi > lo)) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
-  if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
+  if (lo < ctx->lo || hi > ctx->hi || lo > hi) return set_error(ctx, SGN_EINVAL, "host range not owned by this shard");
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
-  const uint32_t h = host - ctx->lo;
-  std::vector<HostRec> rec;
-  if (int e = read_recs(ctx, h, 1, &rec)) return e;
-  uint64_t m = INVALID;
-  for (int s = 0; s < NSLOT; s++) m = std::min(m, rec[0].slot_t[s]);
-  // pending packet events for this host: its group's slab in every bucket
+  const uint32_t n = hi - lo;
+  if (n == 0) return 0;
   const DevSim& S = ctx->S;
-  const uint32_t g = h >> S.gsh;
-  std::vector<uint32_t> bs(S.NB);
-  SGN_HIP(ctx, hipMemcpy(bs.data(), (const void*)S.bucket_slab, bs.size() * 4, hipMemcpyDeviceToHost));
-  for (uint32_t b = 0; b < S.NB; b++) {
-    const size_t idx = (size_t)bs[b] * S.G + g;
-    uint32_t n = 0;
-    SGN_HIP(ctx, hipMemcpy(&n, (const void*)(S.slab_n + idx), 4, hipMemcpyDeviceToHost));
-    n = std::min(n, S.CAP);
-    if (!n) continue;
-    std::vector<EvRec> ev(n);
-    SGN_HIP(ctx, hipMemcpy(ev.data(), (const void*)(S.pool + idx * S.CAP), n * sizeof(EvRec), hipMemcpyDeviceToHost));
-    for (const EvRec& e : ev)
-      if (e.dst == host) m = std::min(m, e.time);
-  }
-  *t = m;
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  uint64_t* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, (size_t)n * 8));
+  const uint32_t l = lo - ctx->lo;
+  const uint32_t g0 = l >> S.gsh, g1 = (l + n - 1) >> S.gsh;
+  const uint32_t ng = g1 - g0 + 1;
+  hipLaunchKernelGGL(k_next_local, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (const DevSim*)ctx->d_S, l, n, d);
+  hipLaunchKernelGGL(k_next_packet, dim3(S.NB * ng), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, l, n, g0,
+                     ng, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "next event times");
   return 0;
+}
+}  // namespace
+
+int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t) {
+  if (!ctx || !t) return SGN_EINVAL;
+  return next_event_times(ctx, host, host + 1, t);
+}
+
+int sgn_hosts_next_event_time(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, uint64_t* out) {
+  return next_event_times(ctx, host_lo, host_hi, out);
 }
 
 int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_total) {
@@ -2683,6 +2727,21 @@ int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_t
   const uint64_t k = std::min(n, cap);
   if (k && out) SGN_HIP(ctx, hipMemcpy(out, ctx->S.trace, k * sizeof(sgn_trace_rec), hipMemcpyDeviceToHost));
   return rc;
+}
+
+int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  const DevSim& S = ctx->S;
+  out->calendar_buckets = S.NB;
+  out->bucket_width_ns = S.BW;
+  out->host_groups = S.G;
+  out->slab_capacity = S.CAP;
+  out->hosts_per_wave = 1u << S.gsh;
+  out->persistent_grid = ctx->persist_grid;
+  out->persistent_fallbacks = ctx->persist_fallbacks;
+  out->device_bytes = ctx->sim_bytes;
+  return 0;
 }
 
 int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
@@ -2796,6 +2855,74 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
   return 0;
 }
 
+// ---- per-thread staging: stages are plain host buffers; one flush submits all
+int sgn_stage_create(sgn_ctx* ctx, sgn_stage** out) {
+  if (!ctx || !out) return SGN_EINVAL;
+  sgn_stage* st = new sgn_stage();
+  st->ctx = ctx;
+  std::lock_guard<std::mutex> g(ctx->stage_mu);
+  ctx->stages.push_back(st);
+  *out = st;
+  return 0;
+}
+
+void sgn_stage_destroy(sgn_stage* st) {
+  if (!st) return;
+  if (st->ctx) {
+    std::lock_guard<std::mutex> g(st->ctx->stage_mu);
+    auto& v = st->ctx->stages;
+    v.erase(std::remove(v.begin(), v.end(), st), v.end());
+  }
+  delete st;
+}
+
+int sgn_stage_push(sgn_stage* st, const sgn_pkt_soa* b) {
+  if (!st || !b) return SGN_EINVAL;
+  if (b->n == 0) return 0;
+  if (!b->src_host || !b->dst_ip || !b->payload_len || !b->send_time) return SGN_EINVAL;
+  for (uint64_t i = 0; i < b->n; i++) {
+    if (b->payload_len[i] > 0xFFFFu) return SGN_EINVAL;
+    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != b->payload_len[i] + SGN_UDP_HEADER_BYTES)
+      return SGN_EINVAL;
+  }
+  st->src.insert(st->src.end(), b->src_host, b->src_host + b->n);
+  st->dst.insert(st->dst.end(), b->dst_ip, b->dst_ip + b->n);
+  st->pay.insert(st->pay.end(), b->payload_len, b->payload_len + b->n);
+  st->time.insert(st->time.end(), b->send_time, b->send_time + b->n);
+  for (uint64_t i = 0; i < b->n; i++) st->handle.push_back(b->handle ? b->handle[i] : 0);
+  return 0;
+}
+
+uint64_t sgn_stage_pending(const sgn_stage* st) { return st ? st->src.size() : 0; }
+
+int sgn_stage_flush(sgn_ctx* ctx) {
+  if (!ctx) return SGN_EINVAL;
+  std::vector<uint32_t> src, dst, pay;
+  std::vector<uint64_t> time, handle;
+  {
+    std::lock_guard<std::mutex> g(ctx->stage_mu);
+    for (sgn_stage* st : ctx->stages) {
+      src.insert(src.end(), st->src.begin(), st->src.end());
+      dst.insert(dst.end(), st->dst.begin(), st->dst.end());
+      pay.insert(pay.end(), st->pay.begin(), st->pay.end());
+      time.insert(time.end(), st->time.begin(), st->time.end());
+      handle.insert(handle.end(), st->handle.begin(), st->handle.end());
+    }
+  }
+  if (src.empty()) return 0;
+  sgn_pkt_soa b{src.size(), src.data(), dst.data(), pay.data(), nullptr, time.data(), handle.data()};
+  if (int rc = sgn_submit(ctx, &b)) return rc;
+  std::lock_guard<std::mutex> g(ctx->stage_mu);
+  for (sgn_stage* st : ctx->stages) {
+    st->src.clear();
+    st->dst.clear();
+    st->pay.clear();
+    st->time.clear();
+    st->handle.clear();
+  }
+  return 0;
+}
+
 int sgn_drain(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap, uint64_t* n_out) {
   if (!ctx || (!out && cap)) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
@@ -2855,27 +2982,57 @@ int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end) {
 }
 
 namespace {
-int rng_draw(sgn_ctx* ctx, uint32_t host, uint32_t n, uint64_t* out) {
-  if (!ctx || (!out && n)) return SGN_EINVAL;
+// counts[i] draws from each of n distinct owned hosts, concatenated in order into out
+int rng_draws(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint32_t n, uint64_t* out) {
+  if (!ctx || (n && (!hosts || !counts))) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
-  if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
-  SGN_HIP(ctx, hipSetDevice(ctx->device));
-  constexpr uint32_t CH = 1u << 16;
-  uint64_t* d = nullptr;
-  SGN_HIP(ctx, hipMalloc(&d, (size_t)std::min(n, CH) * 8 + 8));
-  hipError_t e = hipSuccess;
-  for (uint32_t o = 0; o < n && e == hipSuccess; o += CH) {
-    const uint32_t k = std::min(CH, n - o);
-    hipLaunchKernelGGL(k_rng, dim3(1), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, host - ctx->lo, k, d);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(out + o, d, (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  std::vector<uint32_t> loc(n);
+  std::vector<uint64_t> off(n);
+  uint64_t total = 0;
+  std::vector<uint32_t> seen;
+  for (uint32_t i = 0; i < n; i++) {
+    if (hosts[i] < ctx->lo || hosts[i] >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
+    loc[i] = hosts[i] - ctx->lo;
+    off[i] = total;
+    total += counts[i];
+    seen.push_back(hosts[i]);
   }
+  std::sort(seen.begin(), seen.end());
+  if (std::adjacent_find(seen.begin(), seen.end()) != seen.end())
+    return set_error(ctx, SGN_EINVAL, "sgn_rng_next_u64_batch: hosts must be distinct");
+  if (total && !out) return SGN_EINVAL;
+  if (n == 0) return 0;
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  char* d = nullptr;
+  const size_t bytes = (size_t)n * (4 + 4 + 8) + total * 8 + 16;
+  SGN_HIP(ctx, hipMalloc(&d, bytes));
+  uint32_t* dh = (uint32_t*)d;
+  uint32_t* dc = dh + n;
+  uint64_t* doff = (uint64_t*)(d + ((size_t)n * 8 + 7) / 8 * 8);
+  uint64_t* dout = doff + n;
+  hipError_t e = hipMemcpyAsync(dh, loc.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, counts, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(doff, off.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_rng, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, dh, dc,
+                       doff, n, dout);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && total) e = hipMemcpyAsync(out, dout, total * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   hipFree(d);
-  if (e != hipSuccess) return hip_fail(ctx, e, "host rng draw");
+  if (e != hipSuccess) return hip_fail(ctx, e, "host rng draws");
   return 0;
 }
+int rng_draw(sgn_ctx* ctx, uint32_t host, uint32_t n, uint64_t* out) {
+  return rng_draws(ctx, &host, &n, 1, out);
+}
 }  // namespace
+
+int sgn_rng_next_u64_batch(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint32_t n,
+                           uint64_t* out) {
+  return rng_draws(ctx, hosts, counts, n, out);
+}
 
 int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out) { return rng_draw(ctx, host, 1, out); }
 

@@ -14,6 +14,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -93,10 +94,14 @@ struct Ctrl {
   uint64_t rounds;
   uint64_t max_bucket;    // high-water mark of any (bucket, host group) slab fill
   uint64_t trace_n;       // trace records produced
-  uint64_t remote_min;    // multi-GPU: min over events exported this round
+  uint64_t pad1;
   uint64_t epoch;         // persistent rounds: round edges published (grid barrier)
   uint64_t prev_we;       // end of the last executed window (sgn_set_window's lower bound)
   uint64_t drain_n;       // drain records produced since the last sgn_drain
+  // persistent launch residency census (zeroed by the host before every k_rounds launch):
+  // workgroups that started, and the verdict (1 = whole grid resident, 2 = not: every
+  // workgroup left before touching simulation state; the host falls back to k_execute)
+  uint32_t res_arrive, res_verdict;
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -111,6 +116,7 @@ enum : uint32_t {
   OVF_TRACE = 32u,
   OVF_TIMEOUT = 64u,  // a persistent grid barrier gave up (grid not resident)
   OVF_DRAIN = 128u,   // drain buffer full (raise sgn_drain_enable's capacity)
+  OVF_HORIZON = 256u, // a delivery beyond the event calendar's horizon
 };
 
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
@@ -248,11 +254,8 @@ struct DevSim {
   uint32_t NB, G;         // NB: a power of two (bucket index = (t / BW) & (NB - 1))
   uint32_t CAP;
   uint32_t gsh;           // log2(hosts per group); a group is served by one 64-lane wave
-  // per-wave results of k_execute (plain stores, reduced by k_finalize: no same-address
-  // atomics across thousands of waves): next local event, min time kept in the spare slab,
-  // and cumulative {host executions, due runs, sorted segments}
-  SGN_GLB uint64_t* w_next;       // [G]
-  SGN_GLB uint64_t* w_keep;       // [G]
+  // per-wave cumulative counters (one row slot per wave, no-return adds: no same-address
+  // atomics across thousands of waves): {host executions, due runs, sorted segments, ...}
   SGN_GLB uint64_t* w_cnt;        // [W_N * G]
   SGN_GLB uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
   SGN_GLB uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
@@ -294,6 +297,14 @@ constexpr uint32_t LDS_BSLAB = 256;  // calendars with up to this many buckets k
 
 }  // namespace sgn
 
+struct sgn_ctx;
+// A CPU worker thread's staging buffer for sgn_submit (sgn_stage_*).
+struct sgn_stage {
+  sgn_ctx* ctx = nullptr;
+  std::vector<uint32_t> src, dst, pay;
+  std::vector<uint64_t> time, handle;
+};
+
 // Host-side context.
 struct sgn_ctx {
   int device = 0;
@@ -328,6 +339,7 @@ struct sgn_ctx {
   sgn::DevSim S{};
   void* d_S = nullptr;  // device copy of S (the execute kernel reads it through a pointer)
   std::vector<void*> allocs;
+  uint64_t sim_bytes = 0;  // device bytes in allocs
   sgn::Ctrl* h_ctrl = nullptr;  // pinned mirror for reads
   uint64_t trace_cap = 0;
   uint64_t drain_cap = 0;                 // sgn_drain_enable (EXTERNAL traffic)
@@ -335,6 +347,8 @@ struct sgn_ctx {
   std::vector<uint32_t> submit_seq;       // per owned host: submissions so far
   std::vector<sgn_drain_rec> drain_held;  // drained from the device, not yet returned
   void* d_stage = nullptr;                // sgn_submit staging (device)
+  std::vector<sgn_stage*> stages;         // sgn_stage_create order
+  std::mutex stage_mu;
   uint64_t stage_cap = 0;
   uint64_t rounds_enqueued = 0;
 
@@ -363,6 +377,7 @@ struct sgn_ctx {
   bool graph_pending = false;
   bool use_graph = true;
   uint32_t persist_grid = 0;  // persistent-rounds grid size (0: per-round launches)
+  uint32_t persist_fallbacks = 0;  // persistent launches refused by the residency census
   bool capturing = false;
 
   ~sgn_ctx();

@@ -163,6 +163,12 @@ class RoutesTiming(C.Structure):
                 ("loss_iters", C.c_uint32), ("tile", C.c_uint32), ("n_tight_edges", C.c_uint64)]
 
 
+class EngineInfo(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity", "hosts_per_wave",
+        "persistent_grid", "persistent_fallbacks", "device_bytes")]
+
+
 class KernelTimes(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 16), ("ms", C.c_double * 16),
                 ("name", C.c_char_p * 16), ("n_kernels", C.c_uint32)]
@@ -203,6 +209,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_trace_enable": (C.c_int, [vp, C.c_uint64]),
         "sgn_trace_read": (C.c_int, [vp, C.POINTER(TraceRec), C.c_uint64, u64p]),
         "sgn_kernel_times_get": (C.c_int, [vp, C.POINTER(KernelTimes)]),
+        "sgn_engine_info_get": (C.c_int, [vp, C.POINTER(EngineInfo)]),
         "sgn_comm_get_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "sgn_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_uint64]),
         "sgn_shard_range": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p]),
@@ -229,6 +236,13 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_rng_next_u64": (C.c_int, [vp, C.c_uint32, u64p]),
         "sgn_rng_double": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_double)]),
         "sgn_rng_fill_bytes": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t]),
+        "sgn_rng_next_u64_batch": (C.c_int, [vp, u32p, u32p, C.c_uint32, u64p]),
+        "sgn_hosts_next_event_time": (C.c_int, [vp, C.c_uint32, C.c_uint32, u64p]),
+        "sgn_stage_create": (C.c_int, [vp, C.POINTER(vp)]),
+        "sgn_stage_destroy": (None, [vp]),
+        "sgn_stage_push": (C.c_int, [vp, C.POINTER(PktSoa)]),
+        "sgn_stage_pending": (C.c_uint64, [vp]),
+        "sgn_stage_flush": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -445,6 +459,44 @@ class Context:
         buf = (C.c_uint8 * max(1, n))()
         self.check(self.L.sgn_rng_fill_bytes(self.h, host, buf, n))
         return bytes(buf[:n])
+
+    def engine_info(self):
+        e = EngineInfo()
+        self.check(self.L.sgn_engine_info_get(self.h, C.byref(e)))
+        return {n: int(getattr(e, n)) for n, _ in e._fields_}
+
+    def rng_next_u64_batch(self, hosts, counts):
+        h = np.ascontiguousarray(hosts, dtype=np.uint32)
+        k = np.ascontiguousarray(counts, dtype=np.uint32)
+        out = np.zeros(max(1, int(k.sum())), dtype=np.uint64)
+        self.check(self.L.sgn_rng_next_u64_batch(self.h, ptr(h, C.c_uint32), ptr(k, C.c_uint32), len(h),
+                                                 ptr(out, C.c_uint64)))
+        return out[: int(k.sum())]
+
+    def next_event_time(self, host):
+        t = C.c_uint64()
+        self.check(self.L.sgn_host_next_event_time(self.h, host, C.byref(t)))
+        return t.value
+
+    def next_event_times(self, lo, hi):
+        out = np.zeros(max(1, hi - lo), dtype=np.uint64)
+        self.check(self.L.sgn_hosts_next_event_time(self.h, lo, hi, ptr(out, C.c_uint64)))
+        return out[: hi - lo]
+
+    # ---- per-thread staging (sgn_stage_*) ----
+    def stage_create(self):
+        st = C.c_void_p()
+        self.check(self.L.sgn_stage_create(self.h, C.byref(st)))
+        return st
+
+    def stage_push(self, st, src_host, dst_ip, payload_len, send_time, handle=None, wire_len=None):
+        b, keep = pkt_soa(src_host, dst_ip, payload_len, send_time, handle, wire_len)
+        rc = self.L.sgn_stage_push(st, C.byref(b))
+        if rc != 0:
+            raise SgnError(rc, "sgn_stage_push: invalid batch")
+
+    def stage_flush(self):
+        self.check(self.L.sgn_stage_flush(self.h))
 
     def kernel_times(self):
         k = KernelTimes()

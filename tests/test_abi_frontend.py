@@ -48,7 +48,8 @@ def test_struct_layouts_match_header(tmp_path):
                "sgn_traffic": sgn.Traffic, "sgn_stats": sgn.Stats, "sgn_host_digest": sgn.HostDigest,
                "sgn_trace_rec": sgn.TraceRec, "sgn_create_opts": sgn.CreateOpts,
                "sgn_routes_timing": sgn.RoutesTiming, "sgn_kernel_times": sgn.KernelTimes,
-               "sgn_pkt_soa": sgn.PktSoa, "sgn_drain_rec": sgn.DrainRec}
+               "sgn_pkt_soa": sgn.PktSoa, "sgn_drain_rec": sgn.DrainRec,
+               "sgn_engine_info": sgn.EngineInfo}
     src = tmp_path / "sz.c"
     body = "".join(f'  printf("{k} %zu\\n", sizeof({k}));\n' for k in structs)
     src.write_text(f'#include <stdio.h>\n#include "sgn.h"\nint main(void) {{\n{body}  return 0;\n}}\n')

@@ -1,6 +1,8 @@
-"""The oracle's threaded round loop (worker threads over host chunks, per-host queue locks,
-as the reference's thread-per-core scheduler with Mutex<EventQueue>) gives exactly the
-single-threaded results: counters, per-host order-sensitive digests, traces and windows."""
+"""The oracle's threaded round loop (a persistent worker pool over host chunks, per-host queue
+locks, as the reference's thread-per-core scheduler with Mutex<EventQueue>) and its
+reference-faithful mode (hash-map lookups, the global packet-counter lock, heap packet copies)
+give exactly the single-threaded optimised results: counters, per-host order-sensitive
+digests, traces and windows. The same holds for the APSP restatement in both modes."""
 import numpy as np
 import pytest
 
@@ -15,8 +17,10 @@ def workload(kind):
     return g, used, n, bw
 
 
-@pytest.mark.parametrize("kind,dynamic", [("periodic", False), ("tgen", False), ("periodic", True)])
-def test_threaded_oracle_matches_sequential(oracle, kind, dynamic):
+@pytest.mark.parametrize("kind,dynamic,mode", [("periodic", False, "threads"), ("tgen", False, "threads"),
+                                               ("periodic", True, "threads"), ("tgen", False, "faithful"),
+                                               ("periodic", True, "faithful1")])
+def test_threaded_oracle_matches_sequential(oracle, kind, dynamic, mode):
     g, used, n, bw = workload(kind)
     lat, loss = oracle.routes(g, used)
     hosts = sgn.HostArrays(sgn.assign_ips(n), (np.arange(n) * 7) % len(used), bw, bw,
@@ -30,8 +34,14 @@ def test_threaded_oracle_matches_sequential(oracle, kind, dynamic):
     else:
         tr = sgn.make_traffic(period_ns=1_000_000, start_jitter_ns=2_000_000, unknown_dst_permille=10)
     a = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=True)
-    b = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=True, threads=4)
+    b = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=True, threads=1 if mode == "faithful1" else 4,
+                   faithful=mode.startswith("faithful"))
     a.run()
+    # switching modes and thread counts mid-run changes nothing either
+    b.run(100)
+    b.set_threads(3)
+    b.run(50)
+    b.set_faithful(mode == "threads")
     b.run()
     sa, sb = a.stats(), b.stats()
     assert sa["packets_sent"] > 1000
@@ -44,3 +54,24 @@ def test_threaded_oracle_matches_sequential(oracle, kind, dynamic):
     ta = ta[np.lexsort((ta["seq"], ta["host"]))]
     tb = tb[np.lexsort((tb["seq"], tb["host"]))]
     assert np.array_equal(ta, tb)
+
+
+@pytest.mark.parametrize("V,directed,seed", [(60, False, 1), (120, True, 2), (300, False, 3)])
+def test_routes_modes_agree(oracle, V, directed, seed):
+    g = sgn.random_graph(V, seed=seed, loss_frac=0.6)
+    if directed:
+        rs = np.concatenate([g.src, g.dst[: len(g.src) - V]])
+        rd = np.concatenate([g.dst, g.src[: len(g.src) - V]])
+        rl = np.concatenate([g.lat, g.lat[: len(g.src) - V][::-1]])
+        rp = np.concatenate([g.loss, g.loss[: len(g.src) - V]])
+        g = sgn.GraphArrays(g.node_id, rs, rd, rl, rp, True)
+    used = np.sort(np.random.default_rng(seed).choice(V, size=V * 2 // 3, replace=False))
+    l0, p0 = oracle.routes(g, used)
+    for faithful in (False, True):
+        for threads in (1, 4):
+            l1, p1 = oracle.routes(g, used, faithful=faithful, threads=threads)
+            assert np.array_equal(l0, l1) and np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
+    disc = sgn.GraphArrays([0, 1, 2], [0, 1, 2], [0, 1, 2], [1, 1, 1], [0, 0, 0], False)
+    for faithful in (False, True):
+        with pytest.raises(sgn.SgnError, match="0 -> 2 are not connected"):
+            oracle.routes(disc, [0, 2], faithful=faithful, threads=2)
