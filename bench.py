@@ -42,6 +42,11 @@ def build_workload(n_hosts, V, seed=1):
     hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), node, bw, bw, seeds)
     rng = np.random.default_rng(11)
     servers = np.sort(rng.choice(n_hosts, size=max(1, n_hosts // 10), replace=False)).astype(np.uint32)
+    if os.environ.get("SGN_BENCH_SORTED"):  # experiment: hosts of one kind in consecutive HostIds
+        ns = len(servers)
+        servers = np.arange(ns, dtype=np.uint32)
+        bw = np.concatenate([np.sort(bw[:ns]), np.sort(bw[ns:])])
+        hosts = sgn.HostArrays(hosts.ip, hosts.node_id, bw, bw, hosts.seed)
     # first fetch uniform over one mean think time: the fetch process is stationary from t=0
     tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, flow_seed=7, start_ns=0, start_jitter_ns=3_000_000_000,
                           period_ns=2_000_000_000, period_jitter_ns=2_000_000_000,
@@ -49,6 +54,22 @@ def build_workload(n_hosts, V, seed=1):
                           file_bytes=(50 * 1024, 1024 * 1024, 5 * 1024 * 1024))
     cfg = sgn.make_config(3600 * 1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64,
                           codel_cap=4096, event_capacity=1 << 24)
+    return g, used, hosts, cfg, tr
+
+
+def build_workload_d(n_hosts, V, seed=1):
+    """Config D (BASELINE.json configs[3]): the config-B graph (1000-node random GML, mean
+    degree 6, 20 % lossy edges, 100 Mbit), every host sends a 64 B datagram to a uniform
+    random peer every 1 ms (dense all-to-all)."""
+    g = sgn.random_graph(V, seed=42)
+    used = np.arange(V, dtype=np.uint32)
+    seeds = sgn.derive_seeds(seed, sgn.host_names(n_hosts))
+    bw = np.full(n_hosts, 100_000_000, dtype=np.uint64)
+    hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), (np.arange(n_hosts) % V).astype(np.uint32), bw, bw, seeds)
+    tr = sgn.make_traffic(sgn.TRAFFIC_PERIODIC, flow_seed=7, start_ns=0, start_jitter_ns=1_000_000,
+                          period_ns=1_000_000, payload_len=64, unknown_dst_permille=0)
+    cfg = sgn.make_config(1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=16, codel_cap=64,
+                          event_capacity=0)
     return g, used, hosts, cfg, tr
 
 
@@ -196,7 +217,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--hosts", type=int, default=100_000, help="hosts per GPU")
+    ap.add_argument("--workload", choices=("C", "D"), default="C",
+                    help="C: the headline 100k-host Tor-like tgen workload; D: 1M hosts, dense all-to-all")
+    ap.add_argument("--hosts", type=int, default=None, help="hosts per GPU (C: 100k, D: 1M)")
     ap.add_argument("--nodes", type=int, default=1000)
     ap.add_argument("--rounds-per-step", type=int, default=100)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
@@ -211,8 +234,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
+    if args.hosts is None:
+        args.hosts = 100_000 if args.workload == "C" else 1_000_000
     n_total = args.hosts * world
-    g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
+    if args.workload == "C":
+        g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
+    else:
+        g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes)
+        # calendar slabs for ~64 due runs per host group and bucket (+ fluctuation)
+        groups = -(-args.hosts // 64)
+        cfg.event_capacity = 257 * groups * 192
 
     ctx = sgn.Context(device=local, shard_rank=rank, shard_count=world,
                       flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around the round kernel
@@ -317,7 +348,8 @@ def main():
         "dtype": "u64",
         "data": "synthetic",
         "config": {
-            "workload": "C: Tor-like 1000-node complete graph, tgen-style UDP trains",
+            "workload": ("C: Tor-like 1000-node complete graph, tgen-style UDP trains" if args.workload == "C" else
+                         "D: 1000-node random graph, every host sends 64 B to a uniform random peer every 1 ms"),
             "hosts_per_gpu": args.hosts, "hosts_total": n_total, "graph_nodes": args.nodes,
             "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
             "parallelism": f"host-shard x{world}",

@@ -34,6 +34,16 @@
 #include "sgn_internal.h"
 #include "sgn_workload.h"
 
+// Cost experiments only (tools/build_exp.sh builds them as separate libraries; results are
+// not parity-valid): digests off, loss draws off.
+#ifdef SGN_EXP_NODIGEST
+#define sgn_drun_add_seq(...) ((void)0)
+#define sgn_drun_add_same(...) ((void)0)
+#define sgn_drun_flush_seq(...) ((void)0)
+#define sgn_drun_flush_same(...) ((void)0)
+#define sgn_digest3(h, ...) (h)
+#endif
+
 // Diagnostic build (libsgn_diag.so, -DSGN_DIAG): per-lane counts of the work kinds that
 // carry dependent global-memory round trips, reported through sgn_debug_stamps.
 #ifdef SGN_DIAG
@@ -54,7 +64,13 @@
 #endif
 enum { DG_RO = 0, DG_RI, DG_APP, DG_BATCH, DG_HDLOAD, DG_FQLOAD, DG_RMISS, DG_POPRUN, DG_N };
 // diagnostic timers: cycles while this lane was inside ...
-enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD, DGT_N };
+enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD,
+       DGT_HDLD, DGT_FHLD, DGT_RTLD, DGT_SVLD, DGT_SLAB, DGT_N };
+#ifdef SGN_DIAG
+#define DGT_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else
+#define DGT_WAIT() ((void)0)
+#endif
 
 namespace sgn {
 
@@ -211,6 +227,7 @@ struct Outbox {
   uint32_t n;          // records appended (may exceed OBOX: those were placed directly)
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
   uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
+  SGN_GLB uint64_t* keepmin;  // minimum of this round's new runs for the window's last bucket
 };
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
@@ -620,7 +637,10 @@ struct HostExec {
       tl_open = false;
     } else {
       DG(DG_HDLOAD);
+      DGT_BEGIN(th);
       L->hd = *cq_slot(0);
+      DGT_WAIT();
+      DGT_END(DGT_HDLD, th);
     }
     hd_valid = true;
   }
@@ -728,7 +748,10 @@ struct HostExec {
   // the head entry (from the LDS copy when it is current)
   __device__ __forceinline__ FifoEnt fifo_head() {
     if (L->fh_idx == fq_head) return L->fh;
+    DGT_BEGIN(tf);
     const FifoEnt e = *fq_slot(0);
+    DGT_WAIT();
+    DGT_END(DGT_FHLD, tf);
     L->fh = e;
     L->fh_idx = fq_head;
     return e;
@@ -934,9 +957,12 @@ struct HostExec {
       T = L->rc_T;
     } else {
       DG(DG_RMISS);
+      DGT_BEGIN(trt);
       const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
       const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
       delay = S.rlat[ri];
+      DGT_WAIT();
+      DGT_END(DGT_RTLD, trt);
       // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53:
       // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an
       // exact integer T and the test is (x >> 11) >= T, bit for bit the same decision
@@ -951,6 +977,12 @@ struct HostExec {
     const bool can_drop = !boot && payload > 0;
     uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
     DGT_BEGIN(tr0);
+#ifdef SGN_EXP_NORNG
+    if (true) {
+      run = n;
+      eid += n;
+    } else
+#endif
     if (S.trace_on || external()) {  // per-packet records
       for (uint32_t j = 0; j < n; j++) {
         const uint64_t x = rng_next() >> 11;
@@ -1015,7 +1047,7 @@ struct HostExec {
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
-      min_nr(b == b1 ? &C->keep_min : &S.bucket_min[b], deliver);
+      min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
       if (nrec == 1) {
         const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
         if (k < OBOX) {
@@ -1030,7 +1062,10 @@ struct HostExec {
           return;
         }
       }
+      DGT_BEGIN(tsl);
       pos = atomicAdd(&S.slab_n[idx], nrec);
+      DGT_WAIT();
+      DGT_END(DGT_SLAB, tsl);
       dstp = S.pool + idx * S.CAP;
       cap = S.CAP;
     } else {
@@ -1178,7 +1213,10 @@ struct HostExec {
     } else {
       uint32_t si = 0, cls = 0;
       sgn_tgen_fetch(S.flow_seed, gid, k, S.n_servers, &si, &cls);
+      DGT_BEGIN(tsv);
       dst = S.servers[si];
+      DGT_WAIT();
+      DGT_END(DGT_SVLD, tsv);
       payload = S.req_payload;
       tag = SGN_TAG_REQ | cls;
       next_delay = sgn_tgen_think(S.flow_seed, gid, k, S.period, S.period_jitter);
@@ -1663,7 +1701,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     for (int i = 0; i < DGT_N; i++) {
       const uint32_t v = loaded ? ex.dgt[i] : 0u;
       const uint32_t vs = wave_sum_u32(v);  // the wave's time in section i
-      if (lane == 0) st[24 + i] = vs;
+      if (lane == 0) st[80 + i] = vs;
     }
     if (lane == 0) {
       st[32] = w_load;
@@ -1754,6 +1792,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const uint32_t ks = C->keep_slab;
   if (S.NB <= LDS_BSLAB)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = S.bucket_slab[i];
+  if (threadIdx.x == 0) X.ob->keepmin = &C->keep_min;
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
@@ -1767,13 +1806,98 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
                  S.NB <= LDS_BSLAB ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]), S.fuse_finalize ? 0 : 1);
 }
 
+// ---- persistent rounds: a decentralized round edge ----
+// Per round r every workgroup folds its minima (runs kept in the spare slab, next local
+// events) into its chunk's slots of buffer p = r % 3, counts itself in (64 workgroups per
+// chunk, then chunks), waits for the whole grid, and then computes the next window ITSELF
+// from the same values (Controller::manager_finished_current_round, controller.rs:88-112):
+// no workgroup publishes the edge, so the barrier costs one arrival and one observation
+// instead of arrival + finalize + publish + wake-up. Shared bookkeeping is done by workgroup
+// 0 during the FOLLOWING round (bucket minima of consumed buckets, the swapped bucket's new
+// minimum, the global bucket -> slab table) and before the launch ends; buffer (r + 1) % 3 is
+// reset by workgroup 0 during round r (its last readers passed barrier r - 1). sim_init sizes
+// the calendar so no send of round r + 1 can reach a bucket consumed in round r.
+constexpr uint32_t RB_CH = 64;  // chunk slots per buffer (persistent grids up to 4096 workgroups)
+
+__device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
+                                          uint64_t m) {
+  if (threadIdx.x != 0) return;
+  const uint32_t ch = w >> 6;
+  const uint32_t csz = min(64u, nw - (ch << 6));
+  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * 2;
+  if (kmin != INVALID) min_nr(mn, kmin);
+  if (m != INVALID) min_nr(mn + 1, m);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
+  SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * (RB_CH + 1);
+  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The next window from buffer p after the barrier (every workgroup, identical results).
+struct RbEdge {
+  uint64_t ws, we, min_next, nb1;
+  uint32_t active;
+};
+__device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t nch, uint64_t ws, uint64_t we) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
+  uint64_t kk = INVALID, wn = INVALID, m = INVALID, km = INVALID, mu = INVALID;
+  if (lane < nch) {
+    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + lane) * 2;
+    kk = ld_dev(mn);
+    wn = ld_dev(mn + 1);
+  }
+  for (uint32_t b = lane; b < S.NB; b += 64) {
+    const bool consumed = ((b - b0) & (S.NB - 1)) < ((b1 - b0) & (S.NB - 1)) || b == b1;
+    if (!consumed) {
+      const uint64_t bm = ld_dev(&S.bucket_min[b]);
+      m = bm < m ? bm : m;
+    }
+  }
+  if (lane == 0) {
+    km = ld_dev(&S.rb_keep[p]);
+    mu = ld_dev(&S.ctrl->min_used);
+  }
+  kk = wave_min_u64(kk);
+  wn = wave_min_u64(wn);
+  m = wave_min_u64(m);
+  km = shfl64(km, 0);
+  mu = shfl64(mu, 0);
+  RbEdge e;
+  e.nb1 = km < kk ? km : kk;  // the spare slab set becomes bucket b1
+  m = e.nb1 < m ? e.nb1 : m;
+  m = wn < m ? wn : m;
+  e.min_next = m == INVALID ? EMU_MAX : m;  // unwrap_or(MAX)
+  // Runahead::get (runahead.rs:44-57)
+  uint64_t ra = (S.dynamic && mu != INVALID) ? mu : S.min_possible;
+  ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+  uint64_t ne = e.min_next + ra;
+  if (ne < e.min_next || ne > EMU_MAX) ne = EMU_MAX;
+  ne = ne < S.end_time ? ne : S.end_time;
+  e.active = e.min_next < ne ? 1u : 0u;
+  e.ws = e.min_next;
+  e.we = ne;
+  return e;
+}
+
+// Workgroup 0's bookkeeping of a finished round [ws, we) (lane-parallel plain stores).
+__device__ __forceinline__ void rb_bookkeep(const DevSim& S, uint64_t ws, uint64_t we, uint64_t nb1,
+                                            uint32_t new_keep) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
+  const uint32_t nc = (b1 - b0) & (S.NB - 1);
+  for (uint32_t i = lane; i < nc; i += 64) st_dev(&S.bucket_min[(b0 + i) & (S.NB - 1)], (uint64_t)INVALID);
+  if (lane == 0) {
+    st_dev(&S.bucket_min[b1], nb1);
+    st_dev(&S.bucket_slab[b1], new_keep);
+  }
+}
+
 // Persistent rounds (single shard): the grid stays resident and runs up to max_rounds
 // rounds, workgroup w serving groups w, w + P, ... every round (a group's host state stays
-// with one CU). A grid barrier per round replaces the kernel boundary: the last arrival
-// runs the round edge and publishes the round number in Ctrl::epoch (atomic store); the
-// others poll it (bounded: a spin past the limit flags OVF_TIMEOUT and exits) and then
-// acquire, so the next round's plain loads see every other workgroup's write-through
-// stores. Shared control words are read with atomic loads (never through the scalar cache).
+// with one CU). Data another workgroup wrote in this launch is read with device-scope loads
+// (event records, slab fills, bucket minima, the round buffers); the rest (host records,
+// queues) belongs to this workgroup's groups.
 __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds) {
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
@@ -1809,25 +1933,55 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     __syncthreads();
     if (verdict != 1) return;
   }
-  const uint64_t e0 = ld_dev(&C->epoch);
-  // the spare slab and the bucket -> slab table change by one swap per round, the same on
-  // every workgroup: each keeps its own copy (LDS) and applies the swap itself
-  uint32_t ks = ld_dev(&C->keep_slab);
+  const uint32_t nch = (P + 63) >> 6;
+  // The round state every workgroup keeps for itself, in LDS (registers are the scarce
+  // resource of the round kernel): the window, the spare slab, and the previous round's
+  // bookkeeping that workgroup 0 does during the next round. The bucket -> slab table
+  // changes by one swap per round, applied by every workgroup to its own LDS copy.
+  struct RoundLDS {
+    uint64_t ws, we, pend_ws, pend_we, pend_nb1;
+    uint32_t active, ks, pend_new, pend;
+  };
+  __shared__ RoundLDS rs;
+  if (threadIdx.x == 0) {
+    rs.ws = ld_dev(&C->ws);
+    rs.we = ld_dev(&C->we);
+    rs.active = ld_dev(&C->active);
+    rs.ks = ld_dev(&C->keep_slab);
+    rs.pend = 0;
+  }
+  const uint64_t rounds0 = ld_dev(&C->rounds);
   const bool lds_tab = S.NB <= LDS_BSLAB;
   if (lds_tab)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = ld_dev(&S.bucket_slab[i]);
   __syncthreads();
-  for (uint32_t r = 0; r < max_rounds; r++) {
-    if (!ld_dev(&C->active)) break;
-    const uint64_t ws = ld_dev(&C->ws), we = ld_dev(&C->we);
+  auto uni64 = [](uint64_t v) -> uint64_t {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  };
+  uint32_t r = 0;
+  for (; r < max_rounds; r++) {
+    if (!__builtin_amdgcn_readfirstlane((int)rs.active)) break;
+    const uint64_t ws = uni64(rs.ws), we = uni64(rs.we);
+    const uint32_t ks = (uint32_t)__builtin_amdgcn_readfirstlane((int)rs.ks);
+    const uint32_t p = r % 3;
+    if (w == 0) {
+      if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
+      // reset buffer (r + 1) % 3 for the next round
+      const uint32_t q = (r + 1) % 3;
+      for (uint32_t i = threadIdx.x; i < RB_CH * 2; i += 64) st_dev(&S.rb_min[(size_t)q * RB_CH * 2 + i], (uint64_t)INVALID);
+      for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64) st_dev(&S.rb_cnt[(size_t)q * (RB_CH + 1) + i], 0u);
+      if (threadIdx.x == 0) st_dev(&S.rb_keep[q], (uint64_t)INVALID);
+    }
     // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
-    // round edge done} on the 100 MHz clock
+    // round edge known} on the 100 MHz clock
     SGN_GLB uint64_t* rd = S.stamps ? S.rdbg + 3 * (size_t)(r & 127) : nullptr;
     if (rd && threadIdx.x == 0)
       __hip_atomic_fetch_min(rd, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) X.ob->keepmin = &S.rb_keep[p];
     uint64_t kall = INVALID, mall = INVALID;
-    bool last = false;
+    bool arrived = false;
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
       const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
@@ -1838,28 +1992,17 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
           if (rd && threadIdx.x == 0)
             __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          last = arrive(S, w, P, kall, mall);
+          rb_arrive(S, p, w, P, kall, mall);
+          arrived = true;
         }
       });
       __syncthreads();
     }
-    const uint32_t b1 = bucket_of(S, we - 1);
-    const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
-    if (last) {
-      finalize_fused(S, threadIdx.x, (P + 63) >> 6, ws, we, ks, slab_b1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) {
-        if (rd) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
-        st_dev(&C->epoch, e0 + r + 1);
-      }
-    }
-    __syncthreads();
-    if (lds_tab && threadIdx.x == 0) X.lbs[b1] = ks;
-    ks = slab_b1;
-    // grid barrier: wait for the round edge, bounded
+    if (!arrived) rb_arrive(S, p, w, P, INVALID, INVALID);  // a workgroup without groups
+    // grid barrier: every chunk complete, bounded
     uint32_t spins = 0;
     bool ok = true;
-    while (ld_dev(&C->epoch) < e0 + r + 1) {
+    while (ld_dev(&S.rb_cnt[(size_t)p * (RB_CH + 1) + RB_CH]) < nch) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {
         ok = false;
@@ -1870,11 +2013,41 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
       return;
     }
-    // no acquire fence: every load of data another workgroup wrote in this launch is a
-    // device-scope atomic load (control words, slab fills, event records, bucket minima);
-    // the rest (host records, queues) belongs to this workgroup's groups
     asm volatile("" ::: "memory");
+    const RbEdge e = rb_edge(S, p, nch, ws, we);
+    if (rd && w == 0 && threadIdx.x == 0) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
+    if (threadIdx.x == 0) {
+      // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
+      const uint32_t b1 = bucket_of(S, we - 1);
+      const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
+      if (lds_tab) X.lbs[b1] = ks;
+      rs.pend = 1;
+      rs.pend_ws = ws;
+      rs.pend_we = we;
+      rs.pend_nb1 = e.nb1;
+      rs.pend_new = ks;
+      rs.ks = slab_b1;
+      rs.ws = e.ws;
+      rs.we = e.we;
+      rs.active = e.active;
+      if (w == 0) {
+        st_dev(&C->last_min_next, e.min_next);
+        st_dev(&C->prev_we, we);
+      }
+    }
+    __syncthreads();
+  }
+  // the last round's bookkeeping and the host-visible control block
+  if (w == 0) {
+    if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
+    if (threadIdx.x == 0) {
+      st_dev(&C->keep_slab, rs.ks);
+      st_dev(&C->ws, rs.ws);
+      st_dev(&C->we, rs.we);
+      st_dev(&C->active, rs.active);
+      st_dev(&C->rounds, rounds0 + r);
+    }
   }
 }
 
@@ -2376,8 +2549,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // one is max(min used latency, configured runahead) (runahead.rs:44-57), i.e. up to
   // max(max_lat, runahead). The calendar spans that plus one partial bucket at each end;
   // send_batch checks the horizon on the device (OVF_HORIZON), so a violation is reported.
+  // The persistent kernel resets a round's consumed buckets during the next round, so one more
+  // window of slack keeps the next round's sends off them (see k_rounds).
   const uint64_t wmax = cfg->use_dynamic_runahead ? std::max<uint64_t>(BW, std::max(max_lat, cfg->runahead_ns)) : BW;
-  uint64_t NB = (wmax + max_lat) / BW + 4;
+  uint64_t NB = (3 * wmax + max_lat) / BW + 8;
   if (NB > (1u << 20)) return set_error(ctx, SGN_EINVAL, "calendar would need > 2^20 buckets");
   while (NB & (NB - 1)) NB += NB & (~NB + 1);  // round up to a power of two
   // hosts per k_execute wave: fewer than 64 spreads the (divergent, per-lane serial) host
@@ -2468,7 +2643,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // persistent rounds (single shard): a grid that is entirely resident — the occupancy
   // query, capped by LDS per CU — with workgroups looping over groups when G exceeds it
   ctx->persist_grid = 0;
-  if (ctx->nranks == 1 && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+  // persistent rounds keep the bucket -> slab table in LDS (each workgroup applies the round's
+  // swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per round
+  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
     int occ = 0, ncu = 0;
     const size_t dyn = exec_lds_bytes((uint32_t)CAP);
     hipFuncAttributes fa{};
@@ -2488,6 +2665,12 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       if (const char* e = getenv("SGN_PERSIST_GRID_FORCE")) ctx->persist_grid = (uint32_t)atoi(e);
     }
   }
+  // persistent-round buffers (three, by round % 3): chunk minima + keep minima, counters
+  S.rb_min = (decltype(S.rb_min))dalloc<uint64_t>(ctx, 3 * RB_CH * 2 + 4);
+  S.rb_keep = S.rb_min + 3 * RB_CH * 2;
+  S.rb_cnt = (decltype(S.rb_cnt))dalloc<uint32_t>(ctx, 3 * (RB_CH + 1));
+  if (!S.rb_min || !S.rb_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+  if (ctx->persist_grid > 64 * RB_CH) ctx->persist_grid = 64 * RB_CH;
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
   {
     std::vector<uint64_t> inv((G + 63) / 64, INVALID);
@@ -2545,6 +2728,8 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
       SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * 2 + 4) * 8, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, 3 * (RB_CH + 1) * 4, ctx->stream));
       time_begin(ctx, K_EXECUTE);
       hipLaunchKernelGGL(k_rounds, dim3(ctx->persist_grid), dim3(64), exec_lds_bytes(ctx->S.CAP),
                          ctx->stream, (const DevSim*)ctx->d_S, n);

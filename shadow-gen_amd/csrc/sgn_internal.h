@@ -260,6 +260,11 @@ struct DevSim {
   SGN_GLB uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
   SGN_GLB uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
   SGN_GLB uint64_t* fin_next;
+  // persistent rounds (k_rounds): per round % 3, chunk minima {kept, next} and the minimum of
+  // new runs for the window's last bucket, and the arrival counters (chunks, then chunks done)
+  SGN_GLB uint64_t* rb_min;       // [3][64][2]
+  SGN_GLB uint64_t* rb_keep;      // [3]
+  SGN_GLB uint32_t* rb_cnt;       // [3][65]
   uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
   uint32_t pad3;
   uint64_t BW;

@@ -12,12 +12,16 @@ import numpy as np
 import bench
 import sgn
 
-g, used, hosts, cfg, tr = bench.build_workload(int(sys.argv[1]) if len(sys.argv) > 1 else 100_000, 1000)
+if len(sys.argv) > 1 and sys.argv[1] == "D":
+    g, used, hosts, cfg, tr = bench.build_workload_d(1_000_000, 1000)
+    cfg.event_capacity = 257 * 15_626 * 192
+else:
+    g, used, hosts, cfg, tr = bench.build_workload(int(sys.argv[1]) if len(sys.argv) > 1 else 100_000, 1000)
 ctx = sgn.Context(flags=2)
 ctx.routes_build(g, used)
 ctx.hosts_set(hosts)
 ctx.sim_init(cfg, tr)
-ctx.run(1000)
+ctx.run(1000 if len(sys.argv) < 2 or sys.argv[1] != 'D' else 250)
 n = sgn.C.c_uint64()
 ctx.check(ctx.L.sgn_debug_stamps(ctx.h, None, 0, sgn.C.byref(n)))
 W = n.value
@@ -37,13 +41,19 @@ for r in range(3):
     for i in order[:12]:
         print(f"   wave {i:5d} cycles={cyc[i]:8d} events={ev[i]:5d} runs={runs[i]:4d} max_lane={mx[i]:4d}"
               f" busy_lanes={busy[i]:2d}  cyc/event={cyc[i] / max(ev[i], 1):7.1f} gather={tg[i]} exec={tx[i]}")
-        if s[i, 24:30].any():
-            tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app"]
-            print("      wave cycles in: " + " ".join(f"{n}={s[i, 24 + k]}" for k, n in enumerate(tn)))
-            sec = s[i, 25] + s[i, 26] + s[i, 27] + s[i, 29]
+        if s[i, 80:91].any():
+            tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app", "ld_codelhead", "ld_fifohead",
+                  "ld_route", "ld_server", "slab_atomic"]
+            print("      wave cycles in: " + " ".join(f"{n}={s[i, 80 + k]}" for k, n in enumerate(tn)))
+            sec = s[i, 81] + s[i, 82] + s[i, 83] + s[i, 85]
             print(f"      load={s[i, 32]} run={s[i, 33]} store={s[i, 34]} run-outside-handlers={s[i, 33] - sec}"
                   f" iterations={s[i, 35]}")
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
+    if s[:, 80:91].any():
+        tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app", "ld_codelhead", "ld_fifohead",
+              "ld_route", "ld_server", "slab_atomic"]
+        print("   section cycles median/p99/sum-share: " + " ".join(
+            f"{n}={np.median(s[:, 80 + k]):.0f}/{np.percentile(s[:, 80 + k], 99):.0f}" for k, n in enumerate(tn)))
     if s[:, 32:35].any():
         wl, wr, ws_ = s[:, 32], s[:, 33], s[:, 34]
         print(f"   wave phases (diag build) median: load={np.median(wl):.0f} run={np.median(wr):.0f} store={np.median(ws_):.0f}"

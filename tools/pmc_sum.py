@@ -1,10 +1,19 @@
-"""Per-dispatch averages of the counters a PMC pass directory holds (tools/pmc_exec.sh)."""
-import collections, csv, glob, sys
+"""Sums PMC counters per dispatch over rocprofv3 --pmc output directories (argv[1:])."""
+import collections
+import csv
+import glob
+import sys
 
-d = sys.argv[1]
-agg = collections.defaultdict(list)
-for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
-for (k, c), v in sorted(agg.items()):
-    print(f"{k:20s} {c:24s} n={len(v):5d} mean={sum(v) / len(v):14.1f}")
+for d in sys.argv[1:]:
+    f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
+    if not f:
+        print(d, "no data")
+        continue
+    acc = collections.defaultdict(float)
+    disp = set()
+    for r in csv.DictReader(open(f[0])):
+        acc[r["Counter_Name"]] += float(r["Counter_Value"])
+        disp.add(r["Dispatch_Id"])
+    print(d, "dispatches", len(disp))
+    for k, v in sorted(acc.items()):
+        print(f"  {k}: {v / len(disp):.5g} per dispatch")
