@@ -249,6 +249,8 @@ struct LaneLDS {
   uint64_t rc_T;
   uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
   uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
+  uint32_t rc_sid;   // ... whose slot id is this
+  uint32_t pad;
 };
 
 struct HostExec {
@@ -279,7 +281,7 @@ struct HostExec {
   // scarce resource: they set how many waves are resident)
   LaneLDS* L;
   SGN_GLB HostRec* R;     // this host's record (set by load())
-  const uint32_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
+  const uint16_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
   Outbox* ob;             // the wave's outbox (LDS)
 #ifdef SGN_DIAG
   uint32_t dgt[DGT_N];
@@ -287,14 +289,14 @@ struct HostExec {
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS* l, const uint32_t* bs, Outbox* o)
+                      LaneLDS* l, const uint16_t* bs, Outbox* o)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
   __device__ __forceinline__ void load() {
     R = S.hrec + h;
     const HostRec& r = *R;
-    gid = S.lo + h;
+    gid = r.gid;
     my_ip = r.ip;
     my_unode = r.unode;
     r0 = r.rng[0];
@@ -330,6 +332,7 @@ struct HostExec {
     // cache, token-bucket constants, digests; then the CoDel queue's head run and the send
     // queue's head entry
     L->rc_dst = r.rc_dst;
+    L->rc_sid = r.rc_sid;
     L->rc_lat = r.rc_lat;
     L->rc_T = r.rc_T;
     L->tbc[0] = r.tb_inc[0];
@@ -398,6 +401,7 @@ struct HostExec {
     r.fq_head = fq_head;
     r.fq_len = fq_len;
     r.rc_dst = L->rc_dst;
+    r.rc_sid = L->rc_sid;
     r.max_codel = c_maxcodel;
     r.n_sent += c_sent;
     r.n_popped += c_popped;
@@ -952,12 +956,15 @@ struct HostExec {
     // the route (WorkerShared::latency / reliability, worker.rs:523-537): a train goes to
     // one peer for many rounds, so the host keeps its last (peer, latency, threshold)
     uint64_t delay, T;
+    uint32_t dsid;  // the destination's slot id (where its events are filed)
     if (L->rc_dst == dst) {
       delay = L->rc_lat;
       T = L->rc_T;
+      dsid = L->rc_sid;
     } else {
       DG(DG_RMISS);
       DGT_BEGIN(trt);
+      dsid = S.sid_of[dst];
       const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
       const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
       delay = S.rlat[ri];
@@ -968,6 +975,7 @@ struct HostExec {
       // exact integer T and the test is (x >> 11) >= T, bit for bit the same decision
       T = (uint64_t)((double)rel32 * 9007199254740992.0);
       L->rc_dst = dst;
+      L->rc_sid = dsid;
       L->rc_lat = delay;
       L->rc_T = T;
     }
@@ -1046,7 +1054,7 @@ struct HostExec {
       }
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
-      const size_t idx = (size_t)slab * S.G + ((dst - S.lo) >> S.gsh);
+      const size_t idx = (size_t)slab * S.G + ((dsid - S.lo) >> S.gsh);
       min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
       if (nrec == 1) {
         const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
@@ -1055,7 +1063,7 @@ struct HostExec {
           r.time = deliver;
           r.eid = eid0;
           r.src = gid;
-          r.dst = dst;
+          r.dst = dsid;
           r.pc = payload | (nsent << 16);
           r.tag = tag;
           ob->idx[k] = (uint32_t)idx;
@@ -1089,7 +1097,7 @@ struct HostExec {
       r.time = deliver;
       r.eid = eid0 + (uint64_t)m * RUN_MAX;
       r.src = gid;
-      r.dst = dst;
+      r.dst = dsid;
       r.pc = payload | (k << 16);
       r.tag = tag;
       st_dev_rec(dstp + pos + m, r);
@@ -1454,7 +1462,7 @@ struct ExecLDS {
   uint32_t* lstart;
   uint32_t* lcur;
   LaneLDS* lslot;     // the lanes' LDS slots
-  uint32_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB)
+  uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   Outbox* ob;         // the wave's outbox
 };
 
@@ -1482,7 +1490,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint32_t* lstart = X.lstart;
   uint32_t* lcur = X.lcur;
   LaneLDS* lslot = X.lslot;
-  uint32_t* lbs = X.lbs;
+  uint16_t* lbs = X.lbs;
   const uint32_t lane = threadIdx.x;
   const uint32_t gsz = 1u << S.gsh;
   const uint32_t h = (g << S.gsh) + lane;  // local host index
@@ -1737,7 +1745,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];                     \
   __shared__ uint32_t lcnt_[64], lstart_[64], lcur_[64];                             \
   __shared__ LaneLDS lslot_[64];                                                     \
-  __shared__ uint32_t lbs_[LDS_BSLAB];                                               \
+  __shared__ uint16_t lbs_[LDS_BSLAB];                                               \
   __shared__ Outbox ob_;                                                             \
   ExecLDS X;                                                                         \
   X.lev = (EvRec*)lds_dyn;                                                           \
@@ -1791,7 +1799,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const uint64_t ws = C->ws, we = C->we;
   const uint32_t ks = C->keep_slab;
   if (S.NB <= LDS_BSLAB)
-    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = S.bucket_slab[i];
+    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)S.bucket_slab[i];
   if (threadIdx.x == 0) X.ob->keepmin = &C->keep_min;
   __syncthreads();
   uint64_t kmin, m;
@@ -1953,7 +1961,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   const uint64_t rounds0 = ld_dev(&C->rounds);
   const bool lds_tab = S.NB <= LDS_BSLAB;
   if (lds_tab)
-    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = ld_dev(&S.bucket_slab[i]);
+    for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
   __syncthreads();
   auto uni64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -2021,7 +2029,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
       const uint32_t b1 = bucket_of(S, we - 1);
       const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
-      if (lds_tab) X.lbs[b1] = ks;
+      if (lds_tab) X.lbs[b1] = (uint16_t)ks;
       rs.pend = 1;
       rs.pend_ws = ws;
       rs.pend_we = we;
@@ -2165,20 +2173,20 @@ __global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* c
   R->rng[3] = s3;
 }
 
-// Host::next_event_time (host.rs:832-834) for the owned hosts [lo, lo + n) (local indices),
-// between rounds: the earliest local event (the host record's slots) ...
+// Host::next_event_time (host.rs:832-834) for the owned HostIds [lo, lo + n), between rounds:
+// the earliest local event (the host record's slots) ...
 __global__ void k_next_local(const DevSim* Sp, uint32_t lo, uint32_t n, uint64_t* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const HostRec& r = Sp->hrec[lo + i];
+  const HostRec& r = Sp->hrec[Sp->sid_of[lo + i] - Sp->lo];
   uint64_t m = r.slot_t[0];
   m = r.slot_t[1] < m ? r.slot_t[1] : m;
   m = r.slot_t[2] < m ? r.slot_t[2] : m;
   out[i] = m;
 }
-// ... and the earliest pending packet event: one wave per (bucket, host group) slab that
-// overlaps the range, atomicMin into the destination's slot. Between rounds every pending
-// event is in a bucket's slab (the spare slab set is empty).
+// ... and the earliest pending packet event: one wave per (bucket, host group) slab,
+// atomicMin into the destination's slot of out when it is in the range. Between rounds every
+// pending event is in a bucket's slab (the spare slab set is empty).
 __global__ void k_next_packet(const DevSim* Sp, uint32_t lo, uint32_t n, uint32_t g0, uint32_t ng,
                               uint64_t* out) {
   const DevSim& S = *Sp;
@@ -2188,7 +2196,7 @@ __global__ void k_next_packet(const DevSim* Sp, uint32_t lo, uint32_t n, uint32_
   const uint32_t fill = min(S.slab_n[idx], S.CAP);
   for (uint32_t j = threadIdx.x; j < fill; j += blockDim.x) {
     const EvRec& e = S.pool[idx * S.CAP + j];
-    const uint32_t d = e.dst - S.lo;
+    const uint32_t d = S.host_of[e.dst - S.lo];
     if (d >= lo && d < lo + n) atomicMin((unsigned long long*)&out[d - lo], (unsigned long long)e.time);
   }
 }
@@ -2482,13 +2490,39 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     S.servers = (decltype(S.servers))d_sv;
   }
 
-  // ---- per-host state records, initialised on the host ----
+  // ---- host slots: every shard's HostId range, permuted so that hosts of one kind share
+  // waves (TGEN: servers by uplink, then clients by downlink; otherwise by bandwidth). The
+  // permutation only places hosts on lanes; semantics follow HostIds. SGN_HOST_ORDER=id keeps
+  // HostId order (test hook). Every shard computes every shard's permutation (same inputs).
+  {
+    const bool by_id = getenv("SGN_HOST_ORDER") && std::string(getenv("SGN_HOST_ORDER")) == "id";
+    ctx->sid_of.assign(N, 0);
+    std::vector<uint32_t> order;
+    for (uint32_t rk = 0; rk < ctx->nranks; rk++) {
+      uint32_t lo = 0, hi = 0;
+      sgn_shard_range(N, rk, ctx->nranks, &lo, &hi);
+      order.resize(hi - lo);
+      for (uint32_t i = lo; i < hi; i++) order[i - lo] = i;
+      if (!by_id) {
+        auto key = [&](uint32_t i) {
+          if (tr->kind == SGN_TRAFFIC_TGEN)
+            return std::make_tuple(is_server[i] ? 0u : 1u, is_server[i] ? ctx->bw_up[i] : ctx->bw_down[i], i);
+          return std::make_tuple(0u, ctx->bw_up[i] ^ (ctx->bw_down[i] << 1), i);
+        };
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+      }
+      for (uint32_t k = 0; k < hi - lo; k++) ctx->sid_of[order[k]] = lo + k;
+      if (rk == ctx->rank) ctx->host_of = order;
+    }
+  }
+  // ---- per-host state records (one per slot), initialised on the host ----
   std::vector<HostRec> recs(nH);
   std::vector<uint64_t> nextloc(nH, INVALID);
   std::memset(recs.data(), 0, recs.size() * sizeof(HostRec));
   for (uint32_t h = 0; h < nH; h++) {
-    const uint32_t g = ctx->lo + h;
+    const uint32_t g = ctx->host_of[h];
     HostRec& r = recs[h];
+    r.gid = g;
     // Xoshiro256PlusPlus::seed_from_u64 (SplitMix64 fill), host.rs:234
     uint64_t sm = ctx->seed[g];
     for (int i = 0; i < 4; i++) r.rng[i] = host_splitmix(sm);
@@ -2532,6 +2566,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     return 0;
   };
   int rc = 0;
+  if ((rc = up32(ctx->sid_of, &S.sid_of)) || (rc = up32(ctx->host_of, &S.host_of))) return rc;
   S.hrec = (decltype(S.hrec))dalloc<HostRec>(ctx, nH);
   S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
   S.fifo = (decltype(S.fifo))dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
@@ -2846,11 +2881,18 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   if (lo < ctx->lo || hi > ctx->hi || lo > hi) return set_error(ctx, SGN_EINVAL, "range outside the owned shard");
   int rc = sync_ctrl(ctx);
-  const uint32_t n = hi - lo, off = lo - ctx->lo;
+  const uint32_t n = hi - lo;
+  // the range's hosts sit in permuted slots: read the slots they span
+  uint32_t smin = ctx->hi, smax = ctx->lo;
+  for (uint32_t i = lo; i < hi; i++) {
+    smin = std::min(smin, ctx->sid_of[i]);
+    smax = std::max(smax, ctx->sid_of[i]);
+  }
   std::vector<HostRec> recs;
-  if (int e = read_recs(ctx, off, n, &recs)) return e;
+  if (n)
+    if (int e = read_recs(ctx, smin - ctx->lo, smax - smin + 1, &recs)) return e;
   for (uint32_t i = 0; i < n; i++) {
-    const HostRec& r = recs[i];
+    const HostRec& r = recs[ctx->sid_of[lo + i] - smin];
     sgn_host_digest& o = out[i];
     o.tx = r.dig[0];
     o.rx = r.dig[1];
@@ -2879,11 +2921,14 @@ int next_event_times(sgn_ctx* ctx, uint32_t lo, uint32_t hi, uint64_t* out) {
   SGN_HIP(ctx, hipSetDevice(ctx->device));
   uint64_t* d = nullptr;
   SGN_HIP(ctx, hipMalloc(&d, (size_t)n * 8));
-  const uint32_t l = lo - ctx->lo;
-  const uint32_t g0 = l >> S.gsh, g1 = (l + n - 1) >> S.gsh;
-  const uint32_t ng = g1 - g0 + 1;
-  hipLaunchKernelGGL(k_next_local, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (const DevSim*)ctx->d_S, l, n, d);
-  hipLaunchKernelGGL(k_next_packet, dim3(S.NB * ng), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, l, n, g0,
+  // the groups holding the range's slots: one host's group, or all of them
+  uint32_t g0 = 0, ng = S.G;
+  if (n == 1) {
+    g0 = (ctx->sid_of[lo] - ctx->lo) >> S.gsh;
+    ng = 1;
+  }
+  hipLaunchKernelGGL(k_next_local, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (const DevSim*)ctx->d_S, lo, n, d);
+  hipLaunchKernelGGL(k_next_packet, dim3(S.NB * ng), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S, lo, n, g0,
                      ng, d);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(out, d, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream);
@@ -3018,7 +3063,7 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
     r.time = t;
     r.eid = ((uint64_t)q++ << 32) | b->dst_ip[i];  // submission order, then the address
     r.src = src;
-    r.dst = src;
+    r.dst = ctx->sid_of[src];  // filed in the source's own slot
     r.pc = pay | (1u << 16);
     r.tag = SGN_TAG_EXT | (uint32_t)(ctx->handles.size() + i);
   }
@@ -3177,7 +3222,7 @@ int rng_draws(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint3
   std::vector<uint32_t> seen;
   for (uint32_t i = 0; i < n; i++) {
     if (hosts[i] < ctx->lo || hosts[i] >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
-    loc[i] = hosts[i] - ctx->lo;
+    loc[i] = ctx->sid_of[hosts[i]] - ctx->lo;  // the host's slot
     off[i] = total;
     total += counts[i];
     seen.push_back(hosts[i]);

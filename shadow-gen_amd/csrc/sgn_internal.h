@@ -140,13 +140,14 @@ struct __attribute__((aligned(128))) HostRec {
   uint32_t ri_src, ri_pay, ri_tag, cq_head;  // relay_inet_in cached packet; CoDel ring head
   uint32_t cq_nr, cq_len, fq_head, fq_len;   // CoDel runs / packets; send queue
   uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
+  uint32_t gid, rc_sid;                      // this host's HostId; route cache peer's slot id
   uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
   uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
   uint64_t app_k;                            // synthetic app counter
   // cold: rare paths only
   uint64_t tseq;                            // trace sequence
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
-  uint64_t pad[17];
+  uint64_t pad[16];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
@@ -233,6 +234,11 @@ struct DevSim {
   SGN_GLB const float* rloss;
   SGN_GLB const uint32_t* unode;  // [n_all] used-node index of every host
   SGN_GLB const uint32_t* ip;     // [n_all]
+  // Hosts live in SLOTS: a shard's HostId range [lo, hi) is permuted so that hosts of the
+  // same kind (server / client, bandwidth class) share waves (their event loops converge).
+  // A slot id (sid) is lo + slot; event records carry the destination's sid.
+  SGN_GLB const uint32_t* sid_of;   // [n_all] HostId -> sid (every shard's permutation)
+  SGN_GLB const uint32_t* host_of;  // [nH] slot -> HostId of this shard
   SGN_GLB const uint32_t* dns_key;
   SGN_GLB const uint32_t* dns_val;
   uint32_t dns_mask;
@@ -338,6 +344,8 @@ struct sgn_ctx {
   std::vector<uint32_t> dns_key, dns_val;
   uint32_t dns_mask = 0;
   uint32_t lo = 0, hi = 0;
+  std::vector<uint32_t> sid_of;   // HostId -> slot id (sim_init; every shard's permutation)
+  std::vector<uint32_t> host_of;  // this shard's slot -> HostId
 
   // simulation
   bool sim_ready = false;
