@@ -199,7 +199,12 @@ def apsp_roofline(apsp, V, U):
     per k-block (B_fw = 16 V^3 / T); the loss phase reads, per sweep and source, the tight arcs
     (20 B each) and the V-entry distance row (12 B each): B_loss = U H (20 E_tight + 12 V)."""
     T = apsp["tile"] or 64
-    b_fw = 16.0 * V ** 3 / T
+    if apsp.get("latency_u64", 1):
+        b_fw = 16.0 * V ** 3 / T  # u64 blocked Floyd-Warshall: the matrix read+written per k-block
+    else:
+        # u32 min-plus squaring: per pass every T x T output tile reads its row and column
+        # panels (2 T V entries of 4 B): 8 V^3 / T bytes per pass
+        b_fw = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
     b_loss = float(U) * max(1, apsp["loss_iters"]) * (20.0 * apsp["n_tight_edges"] / max(1, U) + 12.0 * V)
     out = {}
     for name, b, ms in (("latency_phase", b_fw, apsp["latency_ms"]), ("loss_phase", b_loss, apsp["loss_ms"])):
@@ -207,8 +212,9 @@ def apsp_roofline(apsp, V, U):
         out[name] = {"bound": "hbm", "alg_bytes": int(b), "ms": round(ms, 3), "achieved": round(gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5)}
     out["relaxations_per_s"] = round(V ** 3 / (apsp["latency_ms"] * 1e-3), 1) if apsp["latency_ms"] > 0 else None
-    out["note"] = ("the latency phase is a chain of V dependent pivot steps (64 per k-block), "
-                   "bounded by that chain's latency, not by bytes")
+    out["note"] = ("latency phase: u32 min-plus squaring passes (every pass one independent tiled "
+                   "product, VALU-bound: add-with-clamp + min per relaxation) or, for paths of 2^32 ns "
+                   "and more, the u64 Floyd-Warshall (a chain of V dependent pivot steps)")
     return out
 
 

@@ -185,6 +185,100 @@ __global__ __launch_bounds__(256) void fw_phase3(uint64_t* D, uint32_t Vp, int k
       D[(uint64_t)(bi * FW_T + ty + 16 * a) * Vp + bj * FW_T + tx + 16 * b] = c[a][b];
 }
 
+// ---- latency phase, fast form: min-plus squaring on saturating u32 ----
+// D <- min(D, D (+) D) until nothing changes: after k squarings D holds the shortest paths of
+// up to 2^k hops, so at most ceil(log2 V) + 1 passes, each an independent tiled min-plus
+// product (no dependent pivot chain: the whole chip works on every pass). Entries are u32
+// with a saturating add (v_add_u32 clamp): every finite entry is the length of a real path
+// and a true shortest path never saturates (its sub-path sums are <= its length), so the
+// result is exact whenever every used pair ends below 2^32 - 1; otherwise (a path of 4.29 s
+// or more, or a disconnected pair) the build redoes the phase with the u64 Floyd-Warshall
+// above. In place: a tile may read entries another workgroup already lowered this pass,
+// which are still real path lengths, so the fixed point is the same.
+constexpr uint32_t SQ_INF = 0xFFFFFFFFu;
+constexpr int SQ_T = 64, SQ_K = 32;
+
+__global__ void sq_init(uint32_t* D, uint32_t Vp) {
+  const uint64_t n = (uint64_t)Vp * Vp;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    D[i] = (i / Vp == i % Vp) ? 0u : SQ_INF;
+}
+
+__global__ void sq_edges(uint32_t* D, uint32_t Vp, const uint32_t* eu, const uint32_t* ev, const uint64_t* el,
+                         uint32_t E, int directed) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < E; k += gridDim.x * blockDim.x) {
+    const uint32_t u = eu[k], v = ev[k];
+    if (u == v) continue;  // the zero-length path always beats a self-loop
+    const uint32_t l = (uint32_t)el[k];  // < 2^32 - 1 (checked on the host)
+    atomicMin(&D[(uint64_t)u * Vp + v], l);
+    if (!directed) atomicMin(&D[(uint64_t)v * Vp + u], l);
+  }
+}
+
+// One pass, 64 x 64 output tile per workgroup of 256 threads, 4 x 4 consecutive entries per
+// thread; K in steps of 32 through LDS (A transposed so both operands are 16-byte reads).
+// flag[it] = 1 if anything changed; the pass returns at once when pass it - 1 changed nothing.
+__global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_t* flag, int it) {
+  if (it > 0 && __hip_atomic_load(&flag[it - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  __shared__ __attribute__((aligned(16))) uint32_t As[SQ_K][SQ_T + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t Bs[SQ_K][SQ_T + 4];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const uint64_t r0 = (uint64_t)blockIdx.y * SQ_T, c0 = (uint64_t)blockIdx.x * SQ_T;
+  uint32_t acc[4][4], orig[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint4 v = *(const uint4*)&D[(r0 + ty * 4 + i) * Vp + c0 + tx * 4];
+    acc[i][0] = orig[i][0] = v.x;
+    acc[i][1] = orig[i][1] = v.y;
+    acc[i][2] = orig[i][2] = v.z;
+    acc[i][3] = orig[i][3] = v.w;
+  }
+  for (uint32_t k0 = 0; k0 < Vp; k0 += SQ_K) {
+    // A = D[r0 .. +64][k0 .. +32] transposed into As[k][m]; B = D[k0 .. +32][c0 .. +64]
+    for (int e = threadIdx.x; e < SQ_T * SQ_K / 4; e += 256) {
+      const int m = e >> 3, kq = (e & 7) * 4;
+      const uint4 a = *(const uint4*)&D[(r0 + m) * Vp + k0 + kq];
+      As[kq][m] = a.x;
+      As[kq + 1][m] = a.y;
+      As[kq + 2][m] = a.z;
+      As[kq + 3][m] = a.w;
+      const int kb = e >> 4, nq = (e & 15) * 4;
+      *(uint4*)&Bs[kb][nq] = *(const uint4*)&D[(k0 + kb) * Vp + c0 + nq];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < SQ_K; k++) {
+      const uint4 a = *(const uint4*)&As[k][ty * 4];
+      const uint4 b = *(const uint4*)&Bs[k][tx * 4];
+      const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t s2 = __builtin_elementwise_add_sat(av[i], bv[j]);
+          acc[i][j] = s2 < acc[i][j] ? s2 : acc[i][j];
+        }
+    }
+    __syncthreads();
+  }
+  bool ch = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) ch |= acc[i][j] != orig[i][j];
+    *(uint4*)&D[(r0 + ty * 4 + i) * Vp + c0 + tx * 4] = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+  }
+  if (__ballot(ch) && (threadIdx.x & 63) == 0) flag[it] = 1;
+}
+
+// D32 -> the u64 matrix the loss pass and the extraction read (2^32 - 1 -> "no path")
+__global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = D32[i];
+    D[i] = v == SQ_INF ? FW_INF : v;
+  }
+}
+
 // Tight-arc loss fold, one workgroup per used source. The arcs that are tight for the
 // source (d[s][u] + lat(u,v) == d[s][v]) are found in ONE sweep over the arc list and kept in
 // LDS (packed u | v << 16 and the arc's loss); the fixed point then iterates over that short
@@ -500,16 +594,45 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     SGN_HIP(ctx, hipMalloc(&ctx->d_loss, (size_t)U * U * 4));
     hipStream_t st = ctx->stream;
     uint64_t* D = (uint64_t*)dD.p;
+    uint64_t max_edge = 0;
+    for (uint32_t k = 0; k < E; k++)
+      if (es[k] != ed[k]) max_edge = std::max(max_edge, g->edge_latency_ns[k]);
+    // latency phase: u32 min-plus squaring when edges fit (exact unless a used pair ends at
+    // 2^32 - 1 or above: then the u64 Floyd-Warshall redoes it), else Floyd-Warshall
+    bool fast = max_edge < SQ_INF && !getenv("SGN_APSP_FW");
+    DevBuf dD32, dflag;
+    const uint32_t max_pass = 34;
+    if (fast) {
+      SGN_HIP(ctx, hipMalloc(&dD32.p, (size_t)Vp * Vp * 4));
+      SGN_HIP(ctx, hipMalloc(&dflag.p, max_pass * 4));
+    }
+  latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
-    hipLaunchKernelGGL(fw_init, dim3(2048), dim3(256), 0, st, D, Vp);
-    hipLaunchKernelGGL(fw_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0, st,
-                       D, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
-                       (int)g->directed);
-    for (uint32_t kb = 0; kb < nb; kb++) {
-      hipLaunchKernelGGL(fw_phase1, dim3(1), dim3(1024), 0, st, D, Vp, (int)kb);
-      if (nb > 1) {
-        hipLaunchKernelGGL(fw_phase2, dim3(2 * (nb - 1)), dim3(1024), 0, st, D, Vp, (int)kb, (int)nb);
-        hipLaunchKernelGGL(fw_phase3, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
+    if (fast) {
+      uint32_t* D32 = (uint32_t*)dD32.p;
+      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, max_pass * 4, st));
+      hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
+      hipLaunchKernelGGL(sq_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0,
+                         st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
+                         (int)g->directed);
+      // ceil(log2 Vp) passes cover every simple path; one more confirms the fixed point
+      uint32_t passes = 1;
+      while ((1u << (passes - 1)) < Vp) passes++;
+      passes = std::min(passes + 1, max_pass);
+      for (uint32_t it = 0; it < passes; it++)
+        hipLaunchKernelGGL(sq_pass, dim3(nb, nb), dim3(256), 0, st, D32, Vp, (uint32_t*)dflag.p, (int)it);
+      hipLaunchKernelGGL(sq_widen, dim3(2048), dim3(256), 0, st, D32, D, (uint64_t)Vp * Vp);
+    } else {
+      hipLaunchKernelGGL(fw_init, dim3(2048), dim3(256), 0, st, D, Vp);
+      hipLaunchKernelGGL(fw_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0, st,
+                         D, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
+                         (int)g->directed);
+      for (uint32_t kb = 0; kb < nb; kb++) {
+        hipLaunchKernelGGL(fw_phase1, dim3(1), dim3(1024), 0, st, D, Vp, (int)kb);
+        if (nb > 1) {
+          hipLaunchKernelGGL(fw_phase2, dim3(2 * (nb - 1)), dim3(1024), 0, st, D, Vp, (int)kb, (int)nb);
+          hipLaunchKernelGGL(fw_phase3, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, D, Vp, (int)kb, (int)nb);
+        }
       }
     }
     SGN_HIP(ctx, hipGetLastError());
@@ -546,6 +669,23 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     if (n_global)
       fprintf(stderr, "libsgn: %u sources had more tight arcs than the LDS list (%u): global sweeps\n",
               n_global, cap);
+    uint32_t sq_passes = 0;
+    if (fast) {
+      std::vector<uint32_t> fl(max_pass);
+      SGN_HIP(ctx, hipMemcpy(fl.data(), dflag.p, max_pass * 4, hipMemcpyDeviceToHost));
+      while (sq_passes < max_pass && fl[sq_passes]) sq_passes++;
+      sq_passes++;  // the pass that found the fixed point
+    }
+    if (res[0] != ~0ULL && fast) {
+      // a used pair without a finite u32 path: disconnected, or a path of 2^32 - 1 ns or more;
+      // the u64 Floyd-Warshall decides
+      fast = false;
+      SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
+      goto latency_phase;
+    }
+    tm.tile = fast ? (uint32_t)SQ_T : (uint32_t)FW_T;
+    tm.latency_passes = fast ? sq_passes : nb;
+    tm.latency_u64 = fast ? 0u : 1u;
     if (res[0] != ~0ULL) {
       const uint64_t i = res[0] / U, j = res[0] % U;
       return set_error(ctx, SGN_EINVAL, "used nodes " + std::to_string(used[i]) + " -> " +

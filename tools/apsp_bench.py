@@ -1,19 +1,48 @@
-"""APSP build time at the bench's graph (V=1000 Tor-like complete graph), several builds:
-the first includes code-object loading; later ones are the steady-state build time."""
+"""APSP build times on the bench graphs (Tor-like complete graph, config C; random sparse
+graph, config B/D) at V = 1000 and 2000, both latency forms (u32 squaring, u64
+Floyd-Warshall via SGN_APSP_FW=1 in a child process). The first build of a process includes
+code-object loading; later ones are the steady-state build time. Prints JSON lines."""
+import json
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "shadow-gen_amd"))
-import numpy as np
+import numpy as np  # noqa: E402
 
-import bench
-import sgn
+import sgn  # noqa: E402
 
-V = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-g, used, hosts, cfg, tr = bench.build_workload(10_000, V)
-ctx = sgn.Context()
-for i in range(4):
-    ctx.routes_build(g, used)
-    print(i, ctx.routes_timing(), flush=True)
+
+def run(kind, V):
+    g = sgn.tor_graph(V, seed=42) if kind == "tor" else sgn.random_graph(V, seed=42)
+    used = np.arange(V, dtype=np.uint32)
+    ctx = sgn.Context()
+    ts = []
+    for i in range(4):
+        ctx.routes_build(g, used)
+        ts.append(ctx.routes_timing())
+    t = ts[-1]
+    return {"graph": kind, "V": V, "arcs": int(t["n_tight_edges"]), "first_build_ms": round(ts[0]["total_ms"], 3),
+            **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()},
+            "form": "u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring"}
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2:
+        print(json.dumps(run(sys.argv[1], int(sys.argv[2]))), flush=True)
+        sys.exit(0)
+    for fw in (False, True):
+        for kind in ("tor", "random"):
+            for V in (1000, 2000):
+                env = dict(os.environ)
+                if fw:
+                    env["SGN_APSP_FW"] = "1"
+                else:
+                    env.pop("SGN_APSP_FW", None)
+                r = subprocess.run([sys.executable, __file__, kind, str(V)], env=env, capture_output=True, text=True)
+                sys.stdout.write(r.stdout)
+                if r.returncode:
+                    sys.stderr.write(r.stderr)
+                    sys.exit(r.returncode)
