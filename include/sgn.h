@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 2
+#define SGN_ABI_VERSION 3
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -35,6 +35,9 @@ extern "C" {
 #define SGN_CONFIG_MTU 1500u
 /* IPv4 header (network/packet.rs:477-484) + UDP header (network/packet.rs:737-740) */
 #define SGN_UDP_HEADER_BYTES 28u
+/* IPv4 + TCP header: 20 B, plus the 3-B window-scale option padded to 4 (packet.rs:617-635) */
+#define SGN_TCP_HEADER_BYTES 40u
+#define SGN_TCP_WS_HEADER_BYTES 44u
 
 /* status codes */
 #define SGN_OK 0
@@ -157,7 +160,18 @@ typedef struct sgn_sim_config {
   uint32_t hosts_per_wave;      /* hosts served by one 64-lane execute wave: a power of two
                                    in [1, 64]; 0 = default (64). Performance only. */
   uint64_t event_capacity;      /* in-flight packet-event slots per shard (0 = auto) */
+  uint32_t interface_qdisc;     /* experimental.interface_qdisc (configuration.rs:448,568,972):
+                                   SGN_QDISC_FIFO (default) or SGN_QDISC_ROUND_ROBIN */
+  uint32_t reserved;
 } sgn_sim_config;
+
+/* The interface's send queue of sockets (host/network/interface.rs:94-106,216-256,
+ * queuing.rs:57-180). Every synthetic send-queue entry (a datagram, or a train written to its
+ * own socket) is one socket. FIFO: sockets by the priority of their next packet = packets in
+ * the order the applications wrote them. ROUND_ROBIN: the interface takes one packet from the
+ * socket at the front and re-queues that socket at the back while it has more. */
+#define SGN_QDISC_FIFO 0u
+#define SGN_QDISC_ROUND_ROBIN 1u
 
 /* Synthetic traffic (stands in for the managed processes, which stay on the CPU in
  * Shadow). Hosts talk UDP through the reference's own relay/router path. Workload
@@ -280,7 +294,10 @@ int sgn_trace_read(sgn_ctx* ctx, sgn_trace_rec* out, uint64_t cap, uint64_t* n_t
  * Rules: traffic kind SGN_TRAFFIC_EXTERNAL; src_host owned by this shard; send_time in
  * [current window start, stop time) and within the event calendar's horizon (the
  * longest route latency ahead of the window); payload_len <= 65535; wire_len 0 or
- * payload_len + 28 (UDP over IPv4, packet.rs:388-396,477-484,737-740). handle is opaque
+ * payload_len + 28 (UDP over IPv4, packet.rs:388-396,477-484,737-740), or payload_len + 40 /
+ * + 44 (a TCP segment from the CPU TCP stack without / with the window-scale option,
+ * packet.rs:617-635; the wire length feeds the token buckets and CoDel's byte count, and a
+ * zero-payload segment is never loss-dropped, worker.rs:371). handle is opaque
  * (the payload stays on the CPU) and comes back in the packet's drain record. Call between
  * rounds; a failed call queues nothing. Replaces Worker::send_packet's CPU callers. */
 typedef struct sgn_pkt_soa {
@@ -329,7 +346,7 @@ typedef struct sgn_drain_rec {
   uint32_t dst_host;    /* destination HostId (0xFFFFFFFF unknown / not resolved) */
   uint32_t status;      /* SGN_DRAIN_* */
   uint32_t payload_len;
-  uint32_t tag;         /* SGN_TAG_EXT | submission slot */
+  uint32_t tag;         /* SGN_TAG_EXT | header kind << 29 | submission slot (sgn_workload.h) */
 } sgn_drain_rec;
 /* Device buffer for drain records between two sgn_drain calls (before sgn_sim_init;
  * default 1<<20 for EXTERNAL traffic). Running out is SGN_EOVERFLOW at the round. */

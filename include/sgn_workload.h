@@ -84,7 +84,17 @@ SGN_HD uint64_t sgn_tgen_think(uint64_t flow_seed, uint32_t host, uint64_t k, ui
 #define SGN_TAG_DATA 0u        /* PERIODIC datagram */
 #define SGN_TAG_REQ 0x10000u   /* TGEN request | size class */
 #define SGN_TAG_RESP 0x20000u  /* TGEN response datagram */
-#define SGN_TAG_EXT 0x80000000u /* EXTERNAL datagram: low 31 bits = sgn_submit slot */
+#define SGN_TAG_EXT 0x80000000u /* EXTERNAL datagram: low 29 bits = sgn_submit slot */
+#define SGN_TAG_SLOT_MASK 0x1FFFFFFFu
+/* Header kind of a packet (tag bits 29-30): its wire length is payload + this many bytes
+ * (network/packet.rs:388-396: IPv4 20 + UDP 8, or + TCP 20 / 24 with window scale). */
+#define SGN_TAG_HDR_SHIFT 29
+#define SGN_TAG_HDR_TCP (1u << SGN_TAG_HDR_SHIFT)
+#define SGN_TAG_HDR_TCPWS (2u << SGN_TAG_HDR_SHIFT)
+SGN_HD uint32_t sgn_header_bytes(uint32_t tag) {
+  const uint32_t k = (tag >> SGN_TAG_HDR_SHIFT) & 3u;
+  return k == 0 ? 28u : (k == 1 ? 40u : 44u);
+}
 
 /* Order-sensitive per-host digest step: each word is xored in and followed by a
  * bijective multiply / xorshift, so any change of value or order changes the result

@@ -834,7 +834,9 @@ struct Pkt {
   uint32_t payload;
   uint32_t tag;
   uint64_t src_eid;
-  uint32_t wire() const { return payload + SGN_UDP_HEADER_BYTES; }  // packet.rs:388
+  // Packet::len (packet.rs:388-390): IPv4 20 + UDP 8, or + TCP 20 / 24 (window scale,
+  // :617-635); the header kind rides in the tag (sgn_workload.h)
+  uint32_t wire() const { return payload + sgn_header_bytes(tag); }
 };
 
 struct CoDelElem {
@@ -1345,7 +1347,17 @@ struct ora_sim {
       p.tag = f.tag;
       p.src_eid = 0;
       f.count--;
-      if (f.count == 0) h.fifo.pop_front();
+      if (f.count == 0) {
+        h.fifo.pop_front();
+      } else if (cfg.interface_qdisc == SGN_QDISC_ROUND_ROBIN) {
+        // round-robin qdisc: the socket is popped, gives one packet and, having more, is
+        // added back at the end of the queue (interface.rs:216-241, queuing.rs FirstInFirstOut)
+        FifoEnt keep = f;
+        h.fifo.pop_front();
+        h.fifo.push_back(keep);
+      }
+      // (FIFO qdisc, queuing.rs MinPriority: the socket whose next packet was written first,
+      // i.e. the front entry, keeps going)
       *out = p;
       return true;
     }
@@ -1828,7 +1840,14 @@ int ora_sim_submit(ora_sim* s, const sgn_pkt_soa* b) {
     const uint64_t t = b->send_time[i];
     const uint32_t pay = b->payload_len[i];
     if (src < s->lo || src >= s->hi || t < s->ws || t >= s->end_time || pay > 0xFFFFu) return SGN_EINVAL;
-    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != pay + SGN_UDP_HEADER_BYTES) return SGN_EINVAL;
+    uint32_t hdr = 0;
+    if (b->wire_len && b->wire_len[i] != 0) {
+      const uint32_t w = b->wire_len[i];
+      if (w == pay + SGN_UDP_HEADER_BYTES) hdr = 0;
+      else if (w == pay + SGN_TCP_HEADER_BYTES) hdr = SGN_TAG_HDR_TCP;
+      else if (w == pay + SGN_TCP_WS_HEADER_BYTES) hdr = SGN_TAG_HDR_TCPWS;
+      else return SGN_EINVAL;
+    }
     Event ev;
     ev.time = t;
     ev.kind = EV_PACKET;  // ordered with the host's packet events: (time, src = itself, order)
@@ -1838,7 +1857,7 @@ int ora_sim_submit(ora_sim* s, const sgn_pkt_soa* b) {
     ev.pkt.src_host = src;
     ev.pkt.dst_ip = b->dst_ip[i];
     ev.pkt.payload = pay;
-    ev.pkt.tag = SGN_TAG_EXT | (uint32_t)(s->handles.size() + i);
+    ev.pkt.tag = SGN_TAG_EXT | hdr | (uint32_t)(s->handles.size() + i);
     ev.pkt.src_eid = 0;
     evs.push_back(ev);
   }
@@ -1851,7 +1870,7 @@ int ora_sim_submit(ora_sim* s, const sgn_pkt_soa* b) {
 int ora_sim_drain(ora_sim* s, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap, uint64_t* n_out) {
   if (!s->external()) return SGN_ESTATE;
   for (sgn_drain_rec& r : s->drain_held) {
-    const uint32_t slot = r.tag & ~SGN_TAG_EXT;
+    const uint32_t slot = r.tag & SGN_TAG_SLOT_MASK;
     r.handle = ((r.tag & SGN_TAG_EXT) && slot < s->handles.size()) ? s->handles[slot] : 0;
   }
   std::vector<sgn_drain_rec> sel, keep;

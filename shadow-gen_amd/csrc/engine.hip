@@ -619,7 +619,7 @@ struct HostExec {
       cq_nr++;
     }
     cq_len += n;
-    cq_bytes += (uint64_t)n * ((uint64_t)payload + SGN_UDP_HEADER_BYTES);
+    cq_bytes += (uint64_t)n * ((uint64_t)payload + sgn_header_bytes(tag));
     if (cq_len > c_maxcodel) c_maxcodel = cq_len;
   }
   // process_standing_delay (:231-262)
@@ -663,7 +663,7 @@ struct HostExec {
       cq_nr--;
     }
     cq_len--;
-    cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + SGN_UDP_HEADER_BYTES);
+    cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + sgn_header_bytes(e.tag));
     *ok_to_drop = codel_standing(sat_sub(now, e.enqueue_ts));
     p->src = e.src;
     p->dst_ip = my_ip;
@@ -841,7 +841,7 @@ struct HostExec {
           const bool drop_quiet = (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now < L->cq[1];
           if (!standing || !ie_due || drop_quiet) {
             const uint32_t n = L->hd.count;
-            const uint64_t wire = (uint64_t)L->hd.payload + SGN_UDP_HEADER_BYTES;
+            const uint64_t wire = (uint64_t)L->hd.payload + sgn_header_bytes(L->hd.tag);
             uint32_t m = n;
             bool blocked = false;
             if (!boot) {
@@ -901,7 +901,7 @@ struct HostExec {
         DG(DG_FQLOAD);
       }
       // the source address is the router's (0.0.0.0), never this host's: no local bypass
-      if (!boot && !tb_remove<1>((uint64_t)p.payload + SGN_UDP_HEADER_BYTES, dur)) {
+      if (!boot && !tb_remove<1>((uint64_t)p.payload + sgn_header_bytes(p.tag), dur)) {
         fl |= F_RI_NEXT;
         ri_src = p.src;
         ri_pay = p.payload;
@@ -1123,7 +1123,7 @@ struct HostExec {
     if (fl & F_RO_NEXT) {
       fl &= ~F_RO_NEXT;
       const bool is_local = ro_dst == gid;
-      if (!boot && !is_local && !tb_remove<0>((uint64_t)ro_pay + SGN_UDP_HEADER_BYTES, &dur)) {
+      if (!boot && !is_local && !tb_remove<0>((uint64_t)ro_pay + sgn_header_bytes(ro_tag), &dur)) {
         fl |= F_RO_NEXT;
         blocked = true;
       } else {
@@ -1140,9 +1140,13 @@ struct HostExec {
       }
     } else if (fq_len > 0) {
       const FifoEnt e = fifo_head();
-      const uint32_t run = e.count == 1 ? 1u : e.count - 1;
+      // round-robin qdisc with other sockets waiting: one packet, then this socket goes to
+      // the back (NetworkInterface::pop, interface.rs:216-256); otherwise the leading
+      // datagrams of the train that share a payload size
+      const bool rr = S.qdisc_rr && fq_len > 1;
+      const uint32_t run = (e.count == 1 || rr) ? 1u : e.count - 1;
       const uint32_t payload = e.count == 1 ? (e.pay >> 16) : (e.pay & 0xFFFFu);
-      const uint64_t wire = (uint64_t)payload + SGN_UDP_HEADER_BYTES;
+      const uint64_t wire = (uint64_t)payload + sgn_header_bytes(e.tag);
       const bool is_local = e.dst == gid;
       uint32_t n_ok = run;
       if (!boot && !is_local) {
@@ -1176,6 +1180,13 @@ struct HostExec {
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         fq_len--;
+      } else if (rr) {
+        // the socket still has data: re-queued behind the others (same length)
+        FifoEnt m = e;
+        m.count = e.count - consumed;
+        fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
+        *fq_slot(fq_len - 1) = m;
+        L->fh_idx = NO_HOST;  // the cached head is stale
       } else {
         fq_slot(0)->count = e.count - consumed;
         L->fh.count = e.count - consumed;
@@ -2445,6 +2456,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.runahead_cfg = cfg->runahead_ns;
   S.dynamic = cfg->use_dynamic_runahead ? 1 : 0;
   S.fifo_cap = cfg->out_fifo_cap;
+  if (cfg->interface_qdisc > SGN_QDISC_ROUND_ROBIN) return set_error(ctx, SGN_EINVAL, "unknown interface_qdisc");
+  S.qdisc_rr = cfg->interface_qdisc == SGN_QDISC_ROUND_ROBIN ? 1u : 0u;
   S.codel_cap = cfg->codel_cap;
   S.trace_on = ctx->trace_cap > 0;
   S.tkind = tr->kind;
@@ -3039,8 +3052,8 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
   const uint64_t ws = ctx->h_ctrl->ws;
   // the calendar holds NB buckets of BW ns; the gather walks forward from the window
   const uint64_t horizon = ws + (uint64_t)(S.NB - 2) * S.BW;
-  if (ctx->handles.size() + b->n > 0x7FFFFFFFULL)
-    return set_error(ctx, SGN_ERANGE, "more than 2^31 submissions on one shard");
+  if (ctx->handles.size() + b->n > SGN_TAG_SLOT_MASK)
+    return set_error(ctx, SGN_ERANGE, "more than 2^29 submissions on one shard");
   std::vector<EvRec> recs(b->n);
   std::vector<uint32_t> seq_add;
   std::vector<uint32_t> seq = ctx->submit_seq;  // committed only on success
@@ -3055,8 +3068,16 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
     if (t >= horizon)
       return set_error(ctx, SGN_EINVAL, "sgn_submit: send_time beyond the event calendar's horizon; submit it closer to its window");
     if (pay > 0xFFFFu) return set_error(ctx, SGN_EINVAL, "sgn_submit: payload_len > 65535");
-    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != pay + SGN_UDP_HEADER_BYTES)
-      return set_error(ctx, SGN_EINVAL, "sgn_submit: wire_len must be payload_len + 28 (UDP/IPv4)");
+    uint32_t hdr = 0;
+    if (b->wire_len && b->wire_len[i] != 0) {
+      const uint32_t w = b->wire_len[i];
+      if (w == pay + SGN_UDP_HEADER_BYTES) hdr = 0;
+      else if (w == pay + SGN_TCP_HEADER_BYTES) hdr = SGN_TAG_HDR_TCP;
+      else if (w == pay + SGN_TCP_WS_HEADER_BYTES) hdr = SGN_TAG_HDR_TCPWS;
+      else
+        return set_error(ctx, SGN_EINVAL,
+                         "sgn_submit: wire_len must be payload_len + 28 (UDP/IPv4), + 40 or + 44 (TCP/IPv4)");
+    }
     uint32_t& q = seq[src - ctx->lo];
     if (q == 0xFFFFFFFFu) return set_error(ctx, SGN_ERANGE, "sgn_submit: 2^32 submissions from one host");
     EvRec& r = recs[i];
@@ -3065,7 +3086,7 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
     r.src = src;
     r.dst = ctx->sid_of[src];  // filed in the source's own slot
     r.pc = pay | (1u << 16);
-    r.tag = SGN_TAG_EXT | (uint32_t)(ctx->handles.size() + i);
+    r.tag = SGN_TAG_EXT | hdr | (uint32_t)(ctx->handles.size() + i);
   }
   SGN_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->stage_cap < b->n) {
@@ -3112,14 +3133,18 @@ int sgn_stage_push(sgn_stage* st, const sgn_pkt_soa* b) {
   if (!b->src_host || !b->dst_ip || !b->payload_len || !b->send_time) return SGN_EINVAL;
   for (uint64_t i = 0; i < b->n; i++) {
     if (b->payload_len[i] > 0xFFFFu) return SGN_EINVAL;
-    if (b->wire_len && b->wire_len[i] != 0 && b->wire_len[i] != b->payload_len[i] + SGN_UDP_HEADER_BYTES)
-      return SGN_EINVAL;
+    if (b->wire_len && b->wire_len[i] != 0) {
+      const uint32_t w = b->wire_len[i], p = b->payload_len[i];
+      if (w != p + SGN_UDP_HEADER_BYTES && w != p + SGN_TCP_HEADER_BYTES && w != p + SGN_TCP_WS_HEADER_BYTES)
+        return SGN_EINVAL;
+    }
   }
   st->src.insert(st->src.end(), b->src_host, b->src_host + b->n);
   st->dst.insert(st->dst.end(), b->dst_ip, b->dst_ip + b->n);
   st->pay.insert(st->pay.end(), b->payload_len, b->payload_len + b->n);
   st->time.insert(st->time.end(), b->send_time, b->send_time + b->n);
   for (uint64_t i = 0; i < b->n; i++) st->handle.push_back(b->handle ? b->handle[i] : 0);
+  for (uint64_t i = 0; i < b->n; i++) st->wire.push_back(b->wire_len ? b->wire_len[i] : 0);
   return 0;
 }
 
@@ -3127,11 +3152,12 @@ uint64_t sgn_stage_pending(const sgn_stage* st) { return st ? st->src.size() : 0
 
 int sgn_stage_flush(sgn_ctx* ctx) {
   if (!ctx) return SGN_EINVAL;
-  std::vector<uint32_t> src, dst, pay;
+  std::vector<uint32_t> src, dst, pay, wire;
   std::vector<uint64_t> time, handle;
   {
     std::lock_guard<std::mutex> g(ctx->stage_mu);
     for (sgn_stage* st : ctx->stages) {
+      wire.insert(wire.end(), st->wire.begin(), st->wire.end());
       src.insert(src.end(), st->src.begin(), st->src.end());
       dst.insert(dst.end(), st->dst.begin(), st->dst.end());
       pay.insert(pay.end(), st->pay.begin(), st->pay.end());
@@ -3140,7 +3166,7 @@ int sgn_stage_flush(sgn_ctx* ctx) {
     }
   }
   if (src.empty()) return 0;
-  sgn_pkt_soa b{src.size(), src.data(), dst.data(), pay.data(), nullptr, time.data(), handle.data()};
+  sgn_pkt_soa b{src.size(), src.data(), dst.data(), pay.data(), wire.data(), time.data(), handle.data()};
   if (int rc = sgn_submit(ctx, &b)) return rc;
   std::lock_guard<std::mutex> g(ctx->stage_mu);
   for (sgn_stage* st : ctx->stages) {
@@ -3149,6 +3175,7 @@ int sgn_stage_flush(sgn_ctx* ctx) {
     st->pay.clear();
     st->time.clear();
     st->handle.clear();
+    st->wire.clear();
   }
   return 0;
 }
@@ -3171,7 +3198,7 @@ int sgn_drain(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64
     ctx->h_ctrl->drain_n = 0;
     for (size_t i = old; i < ctx->drain_held.size(); i++) {
       sgn_drain_rec& r = ctx->drain_held[i];
-      const uint32_t slot = r.tag & ~SGN_TAG_EXT;
+      const uint32_t slot = r.tag & SGN_TAG_SLOT_MASK;
       // a slot is this shard's when the datagram's source is one of its hosts
       r.handle = ((r.tag & SGN_TAG_EXT) && r.src_host >= ctx->lo && r.src_host < ctx->hi &&
                   slot < ctx->handles.size()) ? ctx->handles[slot] : 0;

@@ -221,6 +221,8 @@ struct DevSim {
   uint64_t min_possible;
   int32_t dynamic;
   uint32_t fifo_cap, codel_cap;
+  uint32_t qdisc_rr;  // interface_qdisc == SGN_QDISC_ROUND_ROBIN
+  uint32_t pad_q;
   uint32_t trace_on;
   // traffic
   uint32_t tkind, payload_len, unknown_permille, req_payload;
@@ -312,7 +314,7 @@ struct sgn_ctx;
 // A CPU worker thread's staging buffer for sgn_submit (sgn_stage_*).
 struct sgn_stage {
   sgn_ctx* ctx = nullptr;
-  std::vector<uint32_t> src, dst, pay;
+  std::vector<uint32_t> src, dst, pay, wire;
   std::vector<uint64_t> time, handle;
 };
 

@@ -22,6 +22,7 @@ EMUTIME_MAX = 0xFFFFFFFFFFFFFFFE
 TRAFFIC_PERIODIC = 1
 TRAFFIC_TGEN = 2
 TRAFFIC_EXTERNAL = 3  # CPU-resident apps: sgn_submit / sgn_drain
+QDISC_FIFO, QDISC_ROUND_ROBIN = 0, 1
 TAG_EXT = 0x80000000
 DRAIN_DELIVERED, DRAIN_LOCAL, DRAIN_LOSS, DRAIN_UNKNOWN, DRAIN_CODEL, DRAIN_BLOCKED = range(6)
 STAMP_WORDS = 96  # include/sgn.h SGN_STAMP_WORDS
@@ -66,6 +67,8 @@ class SimConfig(C.Structure):
         ("codel_cap", C.c_uint32),
         ("hosts_per_wave", C.c_uint32),
         ("event_capacity", C.c_uint64),
+        ("interface_qdisc", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -325,7 +328,7 @@ def make_traffic(kind=TRAFFIC_PERIODIC, *, flow_seed=7, start_ns=0, start_jitter
 
 
 def make_config(stop_time_ns, *, bootstrap_end_ns=0, runahead_ns=1_000_000, dynamic=False,
-                out_fifo_cap=64, codel_cap=1024, event_capacity=0):
+                out_fifo_cap=64, codel_cap=1024, event_capacity=0, qdisc=0):
     c = SimConfig()
     c.stop_time_ns = stop_time_ns
     c.bootstrap_end_ns = bootstrap_end_ns
@@ -334,6 +337,7 @@ def make_config(stop_time_ns, *, bootstrap_end_ns=0, runahead_ns=1_000_000, dyna
     c.out_fifo_cap = out_fifo_cap
     c.codel_cap = codel_cap
     c.event_capacity = event_capacity
+    c.interface_qdisc = qdisc
     return c
 
 

@@ -42,13 +42,17 @@ def datagrams(hosts, k=600, seed=5, span_ns=150_000_000):
     t[: k // 4] = sgn.SIMULATION_START + np.sort(rng.integers(0, span_ns // 10, k // 4)).astype(np.uint64)
     order = np.argsort(t, kind="stable")
     handle = (np.arange(k, dtype=np.uint64) * 0x9E3779B97F4A7C15) & np.uint64(0xFFFFFFFFFFFFFFFF)
-    return src[order], dip[order], pay[order], t[order], handle[order]
+    # wire lengths: UDP (0 = implied, or payload + 28) and TCP segments from the CPU TCP stack
+    # (payload + 40, + 44 with the window-scale option: network/packet.rs:617-635)
+    kind = rng.integers(0, 4, k)
+    wire = np.where(kind == 0, 0, pay + np.array([0, 28, 40, 44])[kind]).astype(np.uint32)
+    return src[order], dip[order], pay[order], t[order], handle[order], wire[order]
 
 
 def drive(sims, dg, rng_hosts=(1, 2), max_rounds=100_000, on_round=None):
     """Runs every sim in lockstep as a CPU controller would; returns the drain records of
     each (list of arrays) and the number of rounds."""
-    src, dip, pay, t, handle = dg
+    src, dip, pay, t, handle, wire = dg
     nxt = 0
     drains = [[] for _ in sims]
     rounds = 0
@@ -68,7 +72,7 @@ def drive(sims, dg, rng_hosts=(1, 2), max_rounds=100_000, on_round=None):
             j += 1
         if j > nxt:
             for s in sims:
-                s.submit(src[nxt:j], dip[nxt:j], pay[nxt:j], t[nxt:j], handle[nxt:j])
+                s.submit(src[nxt:j], dip[nxt:j], pay[nxt:j], t[nxt:j], handle[nxt:j], wire_len=wire[nxt:j])
             nxt = j
         mins = [s.round() for s in sims]
         assert all(m == mins[0] for m in mins), mins

@@ -22,15 +22,19 @@ def test_every_datagram_fate_drained_once(oracle):
     dg = datagrams(hosts)
     recs, rounds = drive([o], dg)
     d = recs[0]
-    src, dip, pay, t, handle = dg
+    src, dip, pay, t, handle, wire = dg
     # one record per submitted datagram (the simulation ran dry: nothing in flight)
-    slots = d["tag"] & 0x7FFFFFFF
+    slots = d["tag"] & 0x1FFFFFFF
+    kinds = (d["tag"] >> 29) & 3  # header kind: 0 UDP, 1 TCP, 2 TCP + window scale
     assert np.all(d["tag"] & sgn.TAG_EXT)
     assert len(d) == len(t) and len(np.unique(slots)) == len(t)
     # the handle and the payload travel with the datagram
     order = np.argsort(slots)
     assert np.array_equal(d["handle"][order], handle)
     assert np.array_equal(d["payload_len"][order], pay)
+    hdr = np.array([28, 40, 44])[kinds[order]]
+    assert np.array_equal(np.where(wire == 0, pay + 28, wire), pay + hdr)
+    assert set(np.unique(kinds).tolist()) == {0, 1, 2}
     st = np.bincount(d["status"], minlength=6)
     for s in (sgn.DRAIN_DELIVERED, sgn.DRAIN_LOCAL, sgn.DRAIN_LOSS, sgn.DRAIN_UNKNOWN,
               sgn.DRAIN_BLOCKED):
@@ -116,3 +120,25 @@ def test_host_rng_fill_bytes_and_double(oracle, nbytes):
     x = nxt()
     assert o.rng_double(2) == (x >> 11) * 2.0 ** -53
     assert o.rng_next_u64(2) == nxt()
+
+
+def test_tcp_segments_take_their_wire_length_through_token_buckets(oracle):
+    """Packet::len (network/packet.rs:388-390, :617-635): a TCP segment is payload + 40 B on
+    the wire (+ 44 with window scale) and the relays' token buckets charge that length, so the
+    same payloads drain later from a slow link as TCP than as UDP."""
+    finish = {}
+    for hdr in (28, 44):
+        world = external_world(n=4, V=3, bw=400_000, fifo=1000, stop_ns=3_000_000_000)
+        o, _, _ = make_oracle(oracle, world)
+        ip = world[2].ip
+        k = 60
+        t = sgn.SIMULATION_START + 1_000_000 + np.arange(k, dtype=np.uint64)
+        o.submit(np.zeros(k), np.full(k, ip[1]), np.full(k, 500), t, wire_len=np.full(k, 500 + hdr))
+        while o.window()[2]:
+            o.round()
+        d = o.drain()
+        assert len(d) == k and np.all(d["status"] == sgn.DRAIN_DELIVERED)
+        finish[hdr] = int(d["time"].max())
+    assert finish[44] > finish[28]
+    with pytest.raises(sgn.SgnError):
+        o.submit([0], [ip[1]], [500], [o.window()[0]], wire_len=[530])

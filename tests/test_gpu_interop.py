@@ -103,13 +103,13 @@ class _Staged:
     def __getattr__(self, k):
         return getattr(self.c, k)
 
-    def submit(self, src, dip, pay, t, handle):
+    def submit(self, src, dip, pay, t, handle, wire_len=None):
         src = np.asarray(src)
         for k, st in enumerate(self.st):
             m = (src % len(self.st)) == k
             if m.any():
                 self.c.stage_push(st, src[m], np.asarray(dip)[m], np.asarray(pay)[m], np.asarray(t)[m],
-                                  np.asarray(handle)[m])
+                                  np.asarray(handle)[m], np.asarray(wire_len)[m])
         self.c.stage_flush()
         assert all(self.c.L.sgn_stage_pending(st) == 0 for st in self.st)
 
@@ -124,11 +124,11 @@ class _StageOrder:
     def __getattr__(self, k):
         return getattr(self.s, k)
 
-    def submit(self, src, dip, pay, t, handle):
+    def submit(self, src, dip, pay, t, handle, wire_len=None):
         src = np.asarray(src)
         order = np.argsort(src % self.k, kind="stable")
         self.s.submit(src[order], np.asarray(dip)[order], np.asarray(pay)[order], np.asarray(t)[order],
-                      np.asarray(handle)[order])
+                      np.asarray(handle)[order], wire_len=np.asarray(wire_len)[order])
 
 
 def test_stage_flush_equals_submit(oracle):

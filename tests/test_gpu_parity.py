@@ -130,7 +130,7 @@ def test_codel_control_law_on_device(ctxf, oracle):
 def scenario(n=200, V=50, *, kind=sgn.TRAFFIC_PERIODIC, stop_ns=500_000_000, bw=10_000_000,
              seed=1, graph_seed=1, dynamic=False, runahead_ns=1_000_000, bootstrap_ns=0,
              unknown=10, period_ns=1_000_000, fifo=64, codel=4096, tgen_think=50_000_000,
-             tor=False):
+             tor=False, qdisc=0):
     g = sgn.tor_graph(V, seed=graph_seed) if tor else sgn.random_graph(V, seed=graph_seed)
     used = np.arange(V)
     names = sgn.host_names(n)
@@ -139,7 +139,7 @@ def scenario(n=200, V=50, *, kind=sgn.TRAFFIC_PERIODIC, stop_ns=500_000_000, bw=
     hosts = sgn.HostArrays(sgn.assign_ips(n), (np.arange(n) * 7) % V, bwv, bwv, seeds)
     cfg = sgn.make_config(stop_ns, runahead_ns=runahead_ns, dynamic=dynamic,
                           bootstrap_end_ns=bootstrap_ns, out_fifo_cap=fifo, codel_cap=codel,
-                          event_capacity=1 << 20)
+                          event_capacity=1 << 20, qdisc=qdisc)
     if kind == sgn.TRAFFIC_PERIODIC:
         tr = sgn.make_traffic(period_ns=period_ns, start_jitter_ns=3_000_000,
                               unknown_dst_permille=unknown, payload_len=1024)
@@ -211,6 +211,17 @@ def test_engine_tgen_trace_codel(ctxf, oracle):
     o, c = run_both(ctxf, oracle, args)
     st = c.stats()
     assert st["codel_dropped"] > 0, st
+    assert_same_run(o, c, args[2].n)
+
+
+def test_engine_tgen_round_robin_qdisc(ctxf, oracle):
+    # experimental.interface_qdisc: round_robin; short think times keep several response
+    # trains (sockets) queued at a server, so the interface interleaves them packet by packet
+    bw = np.where(np.arange(300) % 10 == 0, 100_000_000, 8_000_000).astype(np.uint64)
+    args = scenario(n=300, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=600_000_000, bw=bw, tor=True,
+                    tgen_think=10_000_000, qdisc=sgn.QDISC_ROUND_ROBIN)
+    o, c = run_both(ctxf, oracle, args)
+    assert c.stats()["packets_sent"] > 10000
     assert_same_run(o, c, args[2].n)
 
 

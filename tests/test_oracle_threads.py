@@ -75,3 +75,31 @@ def test_routes_modes_agree(oracle, V, directed, seed):
     for faithful in (False, True):
         with pytest.raises(sgn.SgnError, match="0 -> 2 are not connected"):
             oracle.routes(disc, [0, 2], faithful=faithful, threads=2)
+
+
+def test_round_robin_qdisc_interleaves_sockets(oracle):
+    """experimental.interface_qdisc: with FIFO a server sends its response trains (one socket
+    each) one after another; with round-robin the interface takes one packet per socket in
+    turn (host/network/interface.rs:216-256, queuing.rs:57-180)."""
+    g, used, n, bw = workload("tgen")
+    lat, loss = oracle.routes(g, used)
+    hosts = sgn.HostArrays(sgn.assign_ips(n), (np.arange(n) * 7) % len(used), bw, bw,
+                           oracle.host_seeds(1, sgn.host_names(n)))
+    tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, period_ns=5_000_000, period_jitter_ns=5_000_000,
+                          start_jitter_ns=5_000_000, servers=np.arange(0, n, 10),
+                          file_bytes=(20_000, 80_000, 300_000))
+    alternations = {}
+    for qd in (sgn.QDISC_FIFO, sgn.QDISC_ROUND_ROBIN):
+        cfg = sgn.make_config(150_000_000, codel_cap=1 << 14, qdisc=qd)
+        o = oracle.Sim(used, lat, loss, hosts, cfg, tr, trace=True)
+        o.run()
+        t = o.trace()
+        t = t[np.lexsort((t["seq"], t["host"]))]
+        s = t[(t["kind"] == 1) & (t["flags"] == 0) & (t["host"] % 10 == 0)]  # servers' sends
+        # consecutive sends of one server at one time to different peers that come back
+        same = (s["host"][2:] == s["host"][:-2]) & (s["a"][2:] == s["a"][:-2])
+        alt = same & (s["peer"][2:] == s["peer"][:-2]) & (s["peer"][1:-1] != s["peer"][2:])
+        alternations[qd] = int(alt.sum())
+        assert o.stats()["packets_sent"] > 1000
+    assert alternations[sgn.QDISC_FIFO] == 0
+    assert alternations[sgn.QDISC_ROUND_ROBIN] > 100
