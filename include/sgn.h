@@ -457,6 +457,14 @@ int sgn_gml_graph(const sgn_gml* g, sgn_graph* out);
 int sgn_gml_node_bandwidth(const sgn_gml* g, uint32_t node_index, uint64_t* up_bits,
                            int32_t* has_up, uint64_t* down_bits, int32_t* has_down);
 
+/* assign_ips (core/sim_config.rs:386-407) over IpAssignment (network/graph/mod.rs:355-417),
+ * hosts in HostId (= hostname) order. Hosts with explicit_ip[i] != 0 keep ips[i] (host byte
+ * order) and are registered first; a repeated configured address is SGN_EINVAL with
+ * *bad_host = the later host. Every other host gets the next address after the last one
+ * handed out (from 11.0.0.0), skipping x.x.x.0, x.x.x.255 and configured addresses;
+ * SGN_ERANGE past 255.255.255.254. Host-side only. */
+int sgn_assign_ips(uint32_t n, const uint8_t* explicit_ip, uint32_t* ips, uint32_t* bad_host);
+
 /* units.rs:406-440 FromStr + convert(): parse "10 ms" / "81920 Kibit" / "1 GiB".
  * kind: 0 Time -> ns, 1 Bytes -> bytes, 2 BitsPerSec -> bits/s. */
 int sgn_units_parse(int32_t kind, const char* text, uint64_t* value_base);

@@ -166,6 +166,18 @@ def host_seeds(sim_seed, names):
     return out
 
 
+def assign_ips(n, explicit=None):
+    """ora_assign_ips: (rc, ips) with the reference's per-host vacancy loop (oracle.cpp)."""
+    L = load()
+    ips = np.zeros(n, dtype=np.uint32)
+    flags = np.zeros(n, dtype=np.uint8)
+    for i, ip in (explicit or {}).items():
+        ips[i] = ip
+        flags[i] = 1
+    rc = L.ora_assign_ips(n, flags.ctypes.data_as(C.POINTER(C.c_uint8)), sgn.ptr(ips, C.c_uint32))
+    return rc, ips
+
+
 class Sim:
     """The reference-structured round loop (core/manager.rs:541-656) on the CPU."""
 

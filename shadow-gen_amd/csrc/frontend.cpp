@@ -12,6 +12,7 @@
 //   edge latency (string, non-zero), jitter (string, ignored), packet_loss (Float in [0,1]).
 // Units: utility/units.rs FromStr (:406-440) and convert() with checked_mul (:378-389).
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -372,6 +373,46 @@ int sgn_gml_graph(const sgn_gml* g, sgn_graph* o) {
   o->edge_latency_ns = g->lat.data();
   o->edge_loss = g->loss.data();
   o->directed = g->directed;
+  return 0;
+}
+
+int sgn_assign_ips(uint32_t n, const uint8_t* explicit_ip, uint32_t* ips, uint32_t* bad_host) {
+  if (n && (!ips || !explicit_ip)) return SGN_EINVAL;
+  // Configured addresses first, in HostId order; a repeat is IpPreviouslyAssignedError.
+  std::vector<std::pair<uint32_t, uint32_t>> fixed;  // (address, host)
+  for (uint32_t i = 0; i < n; i++)
+    if (explicit_ip[i]) fixed.emplace_back(ips[i], i);
+  std::sort(fixed.begin(), fixed.end());
+  // Registration stops at the first host (in HostId order) whose address is taken: in each
+  // group of equal addresses that is the group's second-lowest host.
+  uint32_t first_bad = UINT32_MAX;
+  for (size_t k = 1; k < fixed.size(); k++)
+    if (fixed[k].first == fixed[k - 1].first && (k < 2 || fixed[k - 2].first != fixed[k].first))
+      first_bad = std::min(first_bad, fixed[k].second);
+  if (first_bad != UINT32_MAX) {
+    if (bad_host) *bad_host = first_bad;
+    return SGN_EINVAL;
+  }
+  // The dynamic cursor only moves up, so one pass over the sorted configured addresses
+  // finds the collisions that IpAssignment::assign's vacancy loop skips.
+  uint64_t last = 11ull << 24;  // 11.0.0.0
+  size_t f = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (explicit_ip[i]) continue;
+    for (;;) {
+      uint64_t next = last + 1;
+      while ((next & 0xFF) == 0 || (next & 0xFF) == 255) next++;
+      if (next > 0xFFFFFFFFull) {
+        if (bad_host) *bad_host = i;
+        return SGN_ERANGE;  // the reference's u32 addition would overflow here
+      }
+      last = next;
+      while (f < fixed.size() && fixed[f].first < next) f++;
+      if (f < fixed.size() && fixed[f].first == next) continue;
+      ips[i] = (uint32_t)next;
+      break;
+    }
+  }
   return 0;
 }
 

@@ -230,6 +230,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_gml_node_bandwidth": (C.c_int, [vp, C.c_uint32, u64p, C.POINTER(C.c_int32), u64p,
                                              C.POINTER(C.c_int32)]),
         "sgn_units_parse": (C.c_int, [C.c_int32, C.c_char_p, u64p]),
+        "sgn_assign_ips": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint8), u32p, u32p]),
         "sgn_selftest_codel_law": (C.c_int, [vp, C.c_uint64, u64p]),
         "sgn_debug_stamps": (C.c_int, [vp, u64p, C.c_uint64, u64p]),
         "sgn_debug_rounds": (C.c_int, [vp, u64p]),
@@ -518,18 +519,51 @@ def host_names(n, prefix="h"):
     return [f"{prefix}{i:0{width}d}" for i in range(n)]
 
 
-def assign_ips(n):
-    """IpAssignment::assign for hosts without an explicit address: 11.0.0.1, ... skipping
-    addresses ending in .0/.255 (network/graph/mod.rs:364-417)."""
-    ips = np.empty(n, dtype=np.uint32)
-    last = 11 << 24
-    for i in range(n):
-        nxt = last + 1
-        while (nxt & 0xFF) in (0, 255):
-            nxt += 1
-        ips[i] = nxt
-        last = nxt
+def assign_ips(n, explicit=None, lib=None):
+    """assign_ips (core/sim_config.rs:386-407) through libsgn's sgn_assign_ips: hosts in HostId
+    order; `explicit` maps host index -> configured IPv4 (int, host byte order); every other
+    host gets the next free address from 11.0.0.1 on, skipping .0/.255 and configured ones
+    (IpAssignment, network/graph/mod.rs:355-417)."""
+    L = lib or load()
+    ips = np.zeros(n, dtype=np.uint32)
+    flags = np.zeros(n, dtype=np.uint8)
+    for i, ip in (explicit or {}).items():
+        ips[i] = ip
+        flags[i] = 1
+    bad = C.c_uint32(0)
+    rc = L.sgn_assign_ips(n, ptr(flags, C.c_uint8), ptr(ips, C.c_uint32), C.byref(bad))
+    if rc != 0:
+        what = "IP address has already been assigned" if rc == -22 else "address space exhausted"
+        raise SgnError(rc, f"sgn_assign_ips: host {bad.value}: {what}")
     return ips
+
+
+def gml_parse(text, lib=None):
+    """GML text -> (GraphArrays, [(up_bits|None, down_bits|None) per node]) through libsgn's
+    sgn_gml_parse (gml_parser + NetworkGraph::parse, network/graph/mod.rs:28-179)."""
+    L = lib or load()
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    h = C.c_void_p()
+    err = C.create_string_buffer(512)
+    rc = L.sgn_gml_parse(b, len(b), C.byref(h), err, 512)
+    if rc != 0:
+        raise SgnError(rc, err.value.decode(errors="replace"))
+    try:
+        g = Graph()
+        L.sgn_gml_graph(h, C.byref(g))
+        n, e = g.n_nodes, g.n_edges
+        arr = lambda p, k: np.ctypeslib.as_array(p, (k,)).copy() if k else []
+        ga = GraphArrays(arr(g.node_id, n), arr(g.edge_src, e), arr(g.edge_dst, e),
+                         arr(g.edge_latency_ns, e), arr(g.edge_loss, e), g.directed)
+        bws = []
+        for i in range(n):
+            up, down = C.c_uint64(), C.c_uint64()
+            hu, hd = C.c_int32(), C.c_int32()
+            L.sgn_gml_node_bandwidth(h, i, C.byref(up), C.byref(hu), C.byref(down), C.byref(hd))
+            bws.append((up.value if hu.value else None, down.value if hd.value else None))
+    finally:
+        L.sgn_gml_free(h)
+    return ga, bws
 
 
 def derive_seeds(sim_seed, names, lib=None):

@@ -10,6 +10,9 @@ import sys
 
 d = sys.argv[1]
 timed = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+# the bench workload the passes ran (bench.py matches on it before quoting "traffic")
+workload = sys.argv[3] if len(sys.argv) > 3 else "C"
+hosts = {"C": 100_000, "D": 1_000_000}[workload]
 
 
 def per_dispatch(counter):
@@ -19,7 +22,7 @@ def per_dispatch(counter):
     for r in rows:
         if ("k_rounds" in r["Kernel_Name"] or "k_execute" in r["Kernel_Name"]) and \
                 r["Counter_Name"] == counter:
-            kern = r["Kernel_Name"].split("(")[0]
+            kern = r["Kernel_Name"].split("(")[0].split("::")[-1]
             k = int(r["Dispatch_Id"])
             vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
     v = [vals[k] for k in sorted(vals)]
@@ -36,5 +39,7 @@ print(json.dumps({
     "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
     "traffic_bytes_per_launch": round(fetch + write),
     "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB -> bytes x1024",
-    "bench_args": "default (steps 10, warmup 5, 100k hosts, 1000 nodes, 100 rounds/step)",
+    "workload": {"name": workload, "hosts_per_gpu": hosts, "graph_nodes": 1000,
+                 "rounds_per_launch": 100, "n_gpus": 1},
+    "bench_args": f"--workload {workload} (steps 10, warmup 5, {hosts} hosts, 1000 nodes, 100 rounds/step)",
 }, indent=1))
