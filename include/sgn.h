@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 3
+#define SGN_ABI_VERSION 4
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -263,18 +263,32 @@ int sgn_host_next_event_time(sgn_ctx* ctx, uint32_t host, uint64_t* t);
  * hosts' worker_maxEventRunaheadTime inputs with one call per round, not one per host. */
 int sgn_hosts_next_event_time(sgn_ctx* ctx, uint32_t host_lo, uint32_t host_hi, uint64_t* out);
 
-/* Per-packet trace (for bit-exact comparison at small sizes). Enable before sim_init. */
+/* Per-packet trace (for bit-exact comparison at small sizes). Enable before sim_init.
+ * The record kinds follow a packet through the path:
+ *   IF_POP   the interface hands a packet to relay_inet_out (NetworkInterface::pop,
+ *            interface.rs:216-256 - the pcap capture point of a sent packet, interface.rs:192-215)
+ *   SEND     Worker::send_packet's outcome (worker.rs:330-403)
+ *   POP      the packet event runs at its destination (host.rs:762-830)
+ *   DELIVER  the interface receives it (NetworkInterface::push - the receive capture point)
+ *   LOCAL    a packet to the host's own address, pushed back into the interface (relay/mod.rs:84-87)
+ *   CODEL_DROP the router's CoDel queue drops it (codel_queue.rs:319-321)
+ * b of IF_POP / DELIVER / LOCAL = payload | tag << 32 (the header kind rides in the tag). */
 #define SGN_TRACE_SEND 1u   /* a = now, b = deliver time (0 if dropped/unknown), c = event id */
 #define SGN_TRACE_POP 2u    /* a = event time, b = 0, c = src event id */
-#define SGN_TRACE_DELIVER 3u/* a = now, b = 0, c = src event id */
+#define SGN_TRACE_DELIVER 3u/* a = now, b = payload|tag<<32, c = src event id */
 #define SGN_TRACE_CODEL_DROP 4u
+#define SGN_TRACE_IF_POP 5u /* a = now, b = payload|tag<<32, c = dst address when peer is unknown */
+#define SGN_TRACE_LOCAL 6u  /* a = now, b = payload|tag<<32 */
 typedef struct sgn_trace_rec {
   uint32_t kind;     /* SGN_TRACE_* */
   uint32_t host;     /* host where it happened */
-  uint32_t peer;     /* SEND: dst HostId (0xFFFFFFFF unknown); others: src HostId */
+  uint32_t peer;     /* SEND / IF_POP: dst HostId (0xFFFFFFFF unknown); LOCAL: itself; others: src HostId */
   uint32_t flags;    /* SEND: 0 sent, 1 loss-dropped, 2 unknown dst */
   uint64_t a, b, c;
   uint64_t seq;      /* per-host sequence number of this record */
+  uint64_t rng_pos;  /* the host RNG's stream position: draws made so far, this record's
+                        loss draw included (host.rs:234; worker.rs:366 draws one per
+                        send_packet past the DNS check; sgn_rng_* draws count too) */
 } sgn_trace_rec;
 int sgn_trace_enable(sgn_ctx* ctx, uint64_t capacity);
 /* Copies up to cap records (unordered; sort by (host, seq)). n_total = records produced. */
@@ -468,6 +482,35 @@ int sgn_assign_ips(uint32_t n, const uint8_t* explicit_ip, uint32_t* ips, uint32
 /* units.rs:406-440 FromStr + convert(): parse "10 ms" / "81920 Kibit" / "1 GiB".
  * kind: 0 Time -> ns, 1 Bytes -> bytes, 2 BitsPerSec -> bits/s. */
 int sgn_units_parse(int32_t kind, const char* text, uint64_t* value_base);
+
+/* ------------------------------------------------------------------------------------ */
+/* Packet capture (utility/pcap_writer.rs, network/packet.rs:800-934, interface.rs:192-215)  */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct sgn_pcap sgn_pcap;
+/* PcapWriter::new: a file with the libpcap global header (magic 0xA1B2C3D4, v2.4, zone 0,
+ * sigfigs 0, snaplen = capture_len, link type 101 raw IP), native byte order. */
+int sgn_pcap_open(const char* path, uint32_t capture_len, sgn_pcap** out);
+/* PcapWriter::write_packet: record header {ts_sec, ts_usec, min(len, capture_len), len}
+ * and the first min(len, capture_len) bytes. */
+int sgn_pcap_write_packet(sgn_pcap* p, uint32_t ts_sec, uint32_t ts_usec, const uint8_t* bytes,
+                          uint32_t len);
+int sgn_pcap_close(sgn_pcap* p);
+/* Packet::display_bytes for the path's packets: the IPv4 header (0x45, DSCP 0, total length,
+ * id 0, DF, TTL 64, protocol, checksum 0, addresses), then a UDP header (ports, length,
+ * checksum 0) or, by the tag's header kind, a TCP header (20 B, or 24 B with the window
+ * scale option 3,3,ws + padding), then the payload. The synthetic applications have no
+ * sockets: ports, TCP sequence/ack/flags/window and the payload bytes are 0. Returns the
+ * packet length (header + payload) and writes min(that, cap) bytes. */
+uint32_t sgn_packet_bytes(uint32_t src_ip, uint32_t dst_ip, uint32_t payload_len, uint32_t tag,
+                          uint8_t* out, uint32_t cap);
+/* One host's interface capture from trace records (any order; the host's records are taken
+ * in seq order): every IF_POP record (send side) and every DELIVER and LOCAL record
+ * (receive side) is one captured packet, stamped with the record's time as
+ * to_abs_simtime (seconds saturated to u32, microseconds). host_ip[HostId] gives addresses;
+ * an unknown peer's address is the record's c. Returns the number of packets written. */
+int64_t sgn_trace_pcap(const sgn_trace_rec* recs, uint64_t n, uint32_t host, const uint32_t* host_ip,
+                       uint32_t n_hosts, const char* path, uint32_t capture_len);
 
 /* ------------------------------------------------------------------------------------ */
 /* Test hooks (not part of the reference interface)                                      */

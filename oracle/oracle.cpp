@@ -62,6 +62,7 @@ uint64_t splitmix_next(uint64_t& state) {
 
 struct Xoshiro {
   uint64_t s[4];
+  uint64_t pos = 0;  // draws so far: the stream position the trace reports
   static Xoshiro seed_from_u64(uint64_t seed) {
     Xoshiro x;
     uint64_t st = seed;
@@ -69,6 +70,7 @@ struct Xoshiro {
     return x;
   }
   uint64_t next_u64() {
+    pos++;
     const uint64_t result = rotl(s[0] + s[3], 23) + s[0];
     const uint64_t t = s[1] << 17;
     s[2] ^= s[0];
@@ -1175,6 +1177,7 @@ struct ora_sim {
     r.b = b;
     r.c = c;
     r.seq = seq;
+    r.rng_pos = h.rng.pos;
     W().tr.push_back(r);
   }
 
@@ -1222,6 +1225,7 @@ struct ora_sim {
   void deliver_to_app(Host& h, const Pkt& p, bool local) {
     if (local) {
       W().st.local_delivered++;
+      trace_rec(h, SGN_TRACE_LOCAL, h.id, 0, W().now, (uint64_t)p.payload | ((uint64_t)p.tag << 32), 0);
       if (external()) drain_rec(h, SGN_DRAIN_LOCAL, h.id, h.id, 0, p.payload, p.tag);
       sgn_drun_flush_seq(&h.d_app, &h.r_app);  // a local delivery is a run of its own
       h.d_app = sgn_digest3(h.d_app, W().now, (uint64_t)p.src_host | (1ULL << 62) | (1ULL << 32),
@@ -1232,7 +1236,8 @@ struct ora_sim {
     W().st.bytes_delivered += p.payload;
     h.n_delivered++;
     sgn_drun_add_seq(&h.d_app, &h.r_app, W().now, p.src_host, p.src_eid, 1);
-    trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, W().now, 0, p.src_eid);
+    trace_rec(h, SGN_TRACE_DELIVER, p.src_host, 0, W().now, (uint64_t)p.payload | ((uint64_t)p.tag << 32),
+              p.src_eid);
     if (external()) drain_rec(h, SGN_DRAIN_DELIVERED, p.src_host, h.id, p.src_eid, p.payload, p.tag);
     if (traffic.kind == SGN_TRAFFIC_TGEN && h.is_server && (p.tag & SGN_TAG_REQ)) {
       uint64_t size = traffic.file_bytes[p.tag & 3u];
@@ -1346,6 +1351,13 @@ struct ora_sim {
       p.payload = f.count == 1 ? f.last_payload : f.payload;
       p.tag = f.tag;
       p.src_eid = 0;
+      // the capture point of a sent packet (interface.rs:252-253)
+      if (trace) {
+        auto d = dns.find(p.dst_ip);
+        const bool known = d != dns.end();
+        trace_rec(h, SGN_TRACE_IF_POP, known ? d->second : 0xFFFFFFFFu, 0, W().now,
+                  (uint64_t)p.payload | ((uint64_t)p.tag << 32), known ? 0 : p.dst_ip);
+      }
       f.count--;
       if (f.count == 0) {
         h.fifo.pop_front();

@@ -253,6 +253,9 @@ struct LaneLDS {
   uint32_t pad;
 };
 
+// kTrace: the per-packet trace can be on (k_execute). The persistent k_rounds is built
+// without it (its registers are fully used; a traced run executes round by round).
+template <bool kTrace>
 struct HostExec {
   const DevSim& S;
   SGN_GLB Ctrl* C;
@@ -451,9 +454,10 @@ struct HostExec {
     return (double)(rng_next() >> 11) * 0x1.0p-53;
   }
 
+  __device__ __forceinline__ bool tr() const { return kTrace && S.trace_on; }
   __device__ __forceinline__ void trace(uint32_t kind, uint32_t peer, uint32_t flags, uint64_t a, uint64_t b,
                         uint64_t c) {
-    if (!S.trace_on) return;
+    if (!tr()) return;
     const uint64_t seq = R->tseq++;
     uint64_t pos = atomicAdd((unsigned long long*)&C->trace_n, 1ULL);
     if (pos >= S.trace_cap) {
@@ -469,6 +473,7 @@ struct HostExec {
     r.b = b;
     r.c = c;
     r.seq = seq;
+    r.rng_pos = R->rng_pos;
     S.trace[pos] = r;
   }
 
@@ -733,9 +738,12 @@ struct HostExec {
     if (idx >= S.fifo_cap) idx -= S.fifo_cap;
     return S.fifo + (size_t)h * S.fifo_cap + idx;
   }
+  // dst NO_HOST: a datagram to `addr`, an address outside the simulation (the trace keeps
+  // it in a side array, S.fifo_addr, for the capture record)
   __device__ __forceinline__ bool fifo_push(uint32_t dst, uint32_t payload, uint32_t last, uint32_t count,
-                            uint32_t tag) {
+                            uint32_t tag, uint32_t addr = 0) {
     if (fq_len >= S.fifo_cap) return false;
+    if (tr() && dst == NO_HOST) S.fifo_addr[fq_slot(fq_len) - S.fifo] = addr;
     FifoEnt e;
     e.dst = dst;
     e.pay = (payload & 0xFFFFu) | (last << 16);
@@ -782,8 +790,9 @@ struct HostExec {
     c_deliv += m;
     c_bytes += (uint64_t)m * payload;
     sgn_drun_add_seq(&L->dig[2], &L->run[2], now, src, e0, m);
-    if (S.trace_on)
-      for (uint32_t k = 0; k < m; k++) trace(SGN_TRACE_DELIVER, src, 0, now, 0, e0 + k);
+    if (tr())
+      for (uint32_t k = 0; k < m; k++)
+        trace(SGN_TRACE_DELIVER, src, 0, now, (uint64_t)payload | ((uint64_t)tag << 32), e0 + k);
     if (external())
       for (uint32_t k = 0; k < m; k++) drain_rec(SGN_DRAIN_DELIVERED, src, gid, e0 + k, payload, tag);
     if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
@@ -802,6 +811,7 @@ struct HostExec {
   }
   __device__ __forceinline__ void deliver_local(const Pkt& p) {  // loopback: a digest run of its own
     cnt_add(&R->n_local_deliv, 1);
+    if (tr()) trace(SGN_TRACE_LOCAL, gid, 0, now, (uint64_t)p.payload | ((uint64_t)p.tag << 32), 0);
     if (external()) drain_rec(SGN_DRAIN_LOCAL, gid, gid, 0, p.payload, p.tag);
     sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
     L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
@@ -921,9 +931,12 @@ struct HostExec {
   // digest takes runs of equal outcomes. Sent packets take consecutive source event ids and
   // share one delivery time, so their events are reserved with one atomic and written as
   // one contiguous run.
-  __device__ __forceinline__ void send_batch(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
+  // pop: (trace) each packet was just popped from the interface (an IF_POP record precedes its
+  // SEND record, as NetworkInterface::pop precedes send_packet)
+  __device__ __forceinline__ void send_batch(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n,
+                                             bool pop = false) {
     DGT_BEGIN(t0);
-    send_batch_(dst, payload, tag, n);
+    send_batch_(dst, payload, tag, n, pop);
     DGT_END(DGT_SEND, t0);
   }
   // one loss-draw outcome of send_batch_'s record-free path (tx digest runs only)
@@ -940,15 +953,23 @@ struct HostExec {
     }
   }
   // dst: the HostId the address resolves to (FifoEnt), NO_HOST: not in the simulation
-  __device__ __forceinline__ void send_batch_(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n) {
+  // IF_POP of the send queue's head entry (an unknown address from the trace's side array)
+  __device__ __forceinline__ void trace_pop(uint32_t dst, uint32_t payload, uint32_t tag) {
+    trace(SGN_TRACE_IF_POP, dst, 0, now, (uint64_t)payload | ((uint64_t)tag << 32),
+          dst == NO_HOST ? S.fifo_addr[fq_slot(0) - S.fifo] : 0);
+  }
+  __device__ __forceinline__ void send_batch_(uint32_t dst, uint32_t payload, uint32_t tag, uint32_t n, bool pop) {
     if (n == 0 || now >= S.end_time) return;
     DG(DG_BATCH);
     const bool boot = now < S.boot_end;
     if (dst == NO_HOST) {  // resolve_ip_to_host_id failed: InetDropped (worker.rs:347-357)
       cnt_add(&R->n_unknown, n);
       sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
-      if (S.trace_on)
-        for (uint32_t j = 0; j < n; j++) trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+      if (tr())
+        for (uint32_t j = 0; j < n; j++) {
+          if (pop) trace_pop(NO_HOST, payload, tag);
+          trace(SGN_TRACE_SEND, 0xFFFFFFFFu, 2, now, 0, 0);
+        }
       if (external())
         for (uint32_t j = 0; j < n; j++) drain_rec(SGN_DRAIN_UNKNOWN, gid, NO_HOST, 0, payload, tag);
       return;
@@ -991,20 +1012,22 @@ struct HostExec {
       eid += n;
     } else
 #endif
-    if (S.trace_on || external()) {  // per-packet records
+    if (tr() || external()) {  // per-packet records
       for (uint32_t j = 0; j < n; j++) {
+        if (tr() && pop) trace_pop(dst, payload, tag);
         const uint64_t x = rng_next() >> 11;
+        if (tr()) R->rng_pos++;
         if (can_drop && x >= T) {
           c_loss++;
           if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
           run = 0;
           sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
-          if (S.trace_on) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
+          if (tr()) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
           if (external()) drain_rec(SGN_DRAIN_LOSS, gid, dst, 0, payload, tag);
         } else {
           const uint64_t e = eid++;
           run++;
-          if (S.trace_on) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
+          if (tr()) trace(SGN_TRACE_SEND, dst, 0, now, deliver, e);
         }
       }
     } else if (!can_drop || T >= (1ULL << 53)) {
@@ -1172,10 +1195,15 @@ struct HostExec {
         p.payload = payload;
         p.tag = e.tag;
         p.eid = 0;
-        for (uint32_t j = 0; j < n_ok; j++) deliver_local(p);
+        for (uint32_t j = 0; j < n_ok; j++) {
+          if (tr()) trace_pop(gid, payload, e.tag);
+          deliver_local(p);
+        }
       } else {
-        send_batch(e.dst, payload, e.tag, n_ok);
+        send_batch(e.dst, payload, e.tag, n_ok, true);
       }
+      // the packet the bucket refused was popped too: it waits in Relay::next_packet
+      if (tr() && blocked) trace_pop(e.dst, payload, e.tag);
       const uint32_t consumed = n_ok + (blocked ? 1u : 0u);
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
@@ -1219,10 +1247,10 @@ struct HostExec {
 
   __device__ __forceinline__ void app_task() {
     const uint64_t k = L->app_k++;
-    uint32_t dst, payload, tag;
+    uint32_t dst, payload, tag, uip = 0;
     uint64_t next_delay;
     if (S.tkind == SGN_TRAFFIC_PERIODIC) {
-      uint32_t peer = 0, uip = 0;
+      uint32_t peer = 0;
       // an address outside the simulation (10.255.0.0/16, never registered) is NO_HOST
       dst = sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip)
                 ? peer : NO_HOST;
@@ -1240,7 +1268,7 @@ struct HostExec {
       tag = SGN_TAG_REQ | cls;
       next_delay = sgn_tgen_think(S.flow_seed, gid, k, S.period, S.period_jitter);
     }
-    if (fifo_push(dst, payload, payload, 1, tag))
+    if (fifo_push(dst, payload, payload, 1, tag, uip))
       relay_notify<0>();  // Host::notify_socket_has_packets (host.rs:969-983)
     else
       cnt_add(&R->n_blocked, 1);
@@ -1255,7 +1283,7 @@ struct HostExec {
     uint32_t dst;
     if (!dns_lookup((uint32_t)e.eid, &dst)) dst = NO_HOST;
     const uint32_t payload = ev_payload(e);
-    if (fifo_push(dst, payload, payload, 1, e.tag)) {
+    if (fifo_push(dst, payload, payload, 1, e.tag, (uint32_t)e.eid)) {
       relay_notify<0>();
     } else {
       cnt_add(&R->n_blocked, 1);
@@ -1324,7 +1352,7 @@ struct HostExec {
           const uint64_t eid0 = e.eid;
           c_popped += n;
           sgn_drun_add_seq(&L->dig[1], &L->run[1], now, src, eid0, n);
-          if (S.trace_on)
+          if (tr())
             for (uint32_t k = 0; k < n; k++) trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
           // Router::route_incoming_packet (router/mod.rs:55-57)
           codel_push_run(src, eid0, ev_payload(e), e.tag, n);
@@ -1489,7 +1517,7 @@ struct ExecLDS {
 // at_end(kmin, next) runs once the group's cross-workgroup data (calendar records, slab
 // fills, minima) is issued and before the host records are written back: the round's
 // arrival goes there, so its wait covers only what other workgroups read.
-template <typename AtEnd>
+template <bool kTrace, typename AtEnd>
 __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
                            const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out,
                            AtEnd&& at_end) {
@@ -1527,7 +1555,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     ob->hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
   }
   __syncthreads();
-  HostExec ex(S, h, we, be, ks, lslot + lane, lbs, ob);
+  HostExec<kTrace> ex(S, h, we, be, ks, lslot + lane, lbs, ob);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -1815,7 +1843,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
-  exec_group(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+  exec_group<true>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
     last = arrive(S, blockIdx.x, gridDim.x, k, n);
   });
   if (!last) return;
@@ -2004,7 +2032,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
       const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
-      exec_group(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+      exec_group<false>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
         if (lastg) {
@@ -2182,6 +2210,7 @@ __global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* c
   R->rng[1] = s1;
   R->rng[2] = s2;
   R->rng[3] = s3;
+  R->rng_pos += count[i];
 }
 
 // Host::next_event_time (host.rs:832-834) for the owned HostIds [lo, lo + n), between rounds:
@@ -2583,6 +2612,11 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.hrec = (decltype(S.hrec))dalloc<HostRec>(ctx, nH);
   S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
   S.fifo = (decltype(S.fifo))dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
+  S.fifo_addr = nullptr;
+  if (ctx->trace_cap) {
+    S.fifo_addr = (decltype(S.fifo_addr))dalloc<uint32_t>(ctx, (size_t)nH * cfg->out_fifo_cap);
+    if (!S.fifo_addr) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
+  }
   if (!S.hrec || !S.codel || !S.fifo)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
@@ -2692,8 +2726,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // query, capped by LDS per CU — with workgroups looping over groups when G exceeds it
   ctx->persist_grid = 0;
   // persistent rounds keep the bucket -> slab table in LDS (each workgroup applies the round's
-  // swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per round
-  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+  // swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per round, and
+  // so does a traced run (k_rounds is built without the per-packet trace)
+  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
     int occ = 0, ncu = 0;
     const size_t dyn = exec_lds_bytes((uint32_t)CAP);
     hipFuncAttributes fa{};

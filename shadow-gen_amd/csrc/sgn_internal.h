@@ -146,8 +146,9 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t app_k;                            // synthetic app counter
   // cold: rare paths only
   uint64_t tseq;                            // trace sequence
+  uint64_t rng_pos;                         // RNG draws so far (kept while tracing, and by sgn_rng_*)
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
-  uint64_t pad[16];
+  uint64_t pad[15];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
@@ -251,6 +252,7 @@ struct DevSim {
   SGN_GLB uint64_t* nextloc;    // [nH]
   SGN_GLB CodelEnt* codel;      // [nH * codel_cap] run ring per host
   SGN_GLB FifoEnt* fifo;        // [nH * fifo_cap] send queue per host
+  SGN_GLB uint32_t* fifo_addr;  // [nH * fifo_cap] traced runs: an unknown entry's address
   // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host
   // group (2^gsh consecutive hosts = one wave of k_execute), of CAP event runs each. Slab
   // ids are indirect (bucket_slab) so the partially consumed last bucket of a window can

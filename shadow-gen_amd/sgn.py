@@ -115,11 +115,13 @@ class TraceRec(C.Structure):
     _fields_ = [
         ("kind", C.c_uint32), ("host", C.c_uint32), ("peer", C.c_uint32), ("flags", C.c_uint32),
         ("a", C.c_uint64), ("b", C.c_uint64), ("c", C.c_uint64), ("seq", C.c_uint64),
+        ("rng_pos", C.c_uint64),
     ]
 
 
 TRACE_DTYPE = np.dtype([("kind", "<u4"), ("host", "<u4"), ("peer", "<u4"), ("flags", "<u4"),
-                        ("a", "<u8"), ("b", "<u8"), ("c", "<u8"), ("seq", "<u8")])
+                        ("a", "<u8"), ("b", "<u8"), ("c", "<u8"), ("seq", "<u8"), ("rng_pos", "<u8")])
+TRACE_SEND, TRACE_POP, TRACE_DELIVER, TRACE_CODEL_DROP, TRACE_IF_POP, TRACE_LOCAL = 1, 2, 3, 4, 5, 6
 DIGEST_DTYPE = np.dtype([("tx", "<u8"), ("rx", "<u8"), ("app", "<u8"), ("rng", "<u8", (4,)),
                          ("next_event_id", "<u8"), ("n_sent", "<u8"), ("n_popped", "<u8"),
                          ("n_delivered", "<u8"), ("n_codel_dropped", "<u8")])
@@ -231,6 +233,13 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
                                              C.POINTER(C.c_int32)]),
         "sgn_units_parse": (C.c_int, [C.c_int32, C.c_char_p, u64p]),
         "sgn_assign_ips": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint8), u32p, u32p]),
+        "sgn_pcap_open": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(vp)]),
+        "sgn_pcap_write_packet": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), C.c_uint32]),
+        "sgn_pcap_close": (C.c_int, [vp]),
+        "sgn_packet_bytes": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.POINTER(C.c_uint8), C.c_uint32]),
+        "sgn_trace_pcap": (C.c_int64, [C.POINTER(TraceRec), C.c_uint64, C.c_uint32, u32p, C.c_uint32,
+                                       C.c_char_p, C.c_uint32]),
         "sgn_selftest_codel_law": (C.c_int, [vp, C.c_uint64, u64p]),
         "sgn_debug_stamps": (C.c_int, [vp, u64p, C.c_uint64, u64p]),
         "sgn_debug_rounds": (C.c_int, [vp, u64p]),
@@ -564,6 +573,39 @@ def gml_parse(text, lib=None):
     finally:
         L.sgn_gml_free(h)
     return ga, bws
+
+
+def packet_bytes(src_ip, dst_ip, payload_len, tag=0, lib=None):
+    """Packet::display_bytes of one path packet (sgn_packet_bytes)."""
+    L = lib or load()
+    n = L.sgn_packet_bytes(src_ip, dst_ip, payload_len, tag, None, 0)
+    out = np.zeros(n, dtype=np.uint8)
+    L.sgn_packet_bytes(src_ip, dst_ip, payload_len, tag, ptr(out, C.c_uint8), n)
+    return out.tobytes()
+
+
+def write_pcaps(trace, host_ips, out_dir, names=None, hosts=None, capture_len=65535, lib=None):
+    """Per-host interface captures from trace records (sgn_trace_pcap), one file per host in
+    `hosts` (default: every host with a captured packet), laid out like the reference's
+    <data_directory>/hosts/<hostname>/eth0.pcap (interface.rs:45-51, namespace.rs:42) when
+    names are given (else <out_dir>/h<id>/eth0.pcap). Returns {host: (path, packets)}."""
+    L = lib or load()
+    tr = np.ascontiguousarray(trace, dtype=TRACE_DTYPE)
+    ips = np.ascontiguousarray(host_ips, dtype=np.uint32)
+    if hosts is None:
+        cap = tr[np.isin(tr["kind"], [TRACE_IF_POP, TRACE_DELIVER, TRACE_LOCAL])]
+        hosts = np.unique(cap["host"]).tolist()
+    out = {}
+    for h in hosts:
+        d = os.path.join(out_dir, "hosts", names[h]) if names is not None else os.path.join(out_dir, f"h{h}")
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, "eth0.pcap")
+        n = L.sgn_trace_pcap(tr.ctypes.data_as(C.POINTER(TraceRec)), len(tr), int(h), ptr(ips, C.c_uint32),
+                             len(ips), path.encode(), capture_len)
+        if n < 0:
+            raise SgnError(int(n), f"sgn_trace_pcap host {h}")
+        out[int(h)] = (path, int(n))
+    return out
 
 
 def derive_seeds(sim_seed, names, lib=None):

@@ -190,7 +190,7 @@ def assert_same_run(o, c, n, trace=True):
     if trace:
         to, tg = sort_trace(o.trace()), sort_trace(c.trace())
         assert len(to) == len(tg)
-        for f in ("kind", "host", "peer", "flags", "a", "b", "c", "seq"):
+        for f in ("kind", "host", "peer", "flags", "a", "b", "c", "seq", "rng_pos"):
             bad = np.nonzero(to[f] != tg[f])[0]
             assert len(bad) == 0, (f, to[bad[:3]], tg[bad[:3]])
 
@@ -355,6 +355,28 @@ def test_external_apps_submit_drain_rng(ctxf, oracle):
     st = np.bincount(dc["status"], minlength=6)
     assert st[sgn.DRAIN_DELIVERED] > 0 and st[sgn.DRAIN_LOSS] > 0 and st[sgn.DRAIN_BLOCKED] > 0
     assert_same_run(o, c, world[2].n)
+
+
+def test_trace_captures_identical(ctxf, oracle, tmp_path):
+    """§8f row 1: the per-host interface captures (pcap, utility/pcap_writer.rs) built from
+    libsgn's trace and from the oracle's are byte-identical: external apps (unknown addresses,
+    loopback, TCP sizes, CPU-side RNG draws) and a PERIODIC run with unknown destinations."""
+    from external_common import datagrams, drive, external_world
+    world = external_world()
+    o, c = _external_pair(ctxf, oracle, world)
+    drive([o, c], datagrams(world[2]))
+    runs = [(o, c, world[2])]
+    args = scenario(n=120, V=30, unknown=50, stop_ns=200_000_000)
+    o2, c2 = run_both(ctxf, oracle, args)
+    runs.append((o2, c2, args[2]))
+    for k, (o, c, hosts) in enumerate(runs):
+        names = sgn.host_names(hosts.n)
+        po = sgn.write_pcaps(o.trace(), hosts.ip, tmp_path / f"o{k}", names=names)
+        pc = sgn.write_pcaps(c.trace(), hosts.ip, tmp_path / f"c{k}", names=names)
+        assert po.keys() == pc.keys() and len(po) > 10
+        for h in po:
+            assert po[h][1] == pc[h][1] > 0
+            assert open(po[h][0], "rb").read() == open(pc[h][0], "rb").read(), h
 
 
 def test_external_rules_on_device(ctxf, oracle):
