@@ -107,6 +107,66 @@ STAT_KEYS = ("rounds", "packets_sent", "packets_loss_dropped", "packets_unknown_
 DIGEST_KEYS = ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered", "n_codel_dropped")
 
 
+def shard_check(ctx, dist, rank, world, n_hosts, rounds_done, build_unsharded):
+    """N > 1: the sharded run (RCCL exchange) against ONE unsharded run of all N x hosts on
+    rank 0's GPU for the same rounds (build_unsharded() -> a context after sim_init) — bit for
+    bit: every host's digests, the summed counters, the window. (The unsharded path is the one
+    checked against the oracle at N = 1.) Collective over gloo; frees the shard's context
+    first. Returns rank 0's verdict dict (None on other ranks)."""
+    import torch
+    lo, hi = sgn.C.c_uint32(), sgn.C.c_uint32()
+    rc = sgn.load().sgn_shard_range(n_hosts, rank, world, sgn.C.byref(lo), sgn.C.byref(hi))
+    assert rc == 0
+    lo, hi = lo.value, hi.value
+    d = ctx.digests(lo, hi)
+    st = ctx.stats()
+    ws, we, act = ctx.window()
+    if hasattr(ctx, "close"):
+        ctx.close()
+    width = sgn.DIGEST_DTYPE.itemsize // 8
+    per = -(-n_hosts // world) + 1
+    buf = np.zeros((per, width), dtype=np.uint64)
+    buf[: hi - lo] = d.view(np.uint64).reshape(-1, width)
+    meta = np.array([lo, hi, ws, we, int(act)] + [st[k] for k in STAT_KEYS], dtype=np.uint64)
+    tb, tm = torch.from_numpy(buf.view(np.int64)), torch.from_numpy(meta.view(np.int64))
+    gb = [torch.zeros_like(tb) for _ in range(world)] if rank == 0 else None
+    gm = [torch.zeros_like(tm) for _ in range(world)] if rank == 0 else None
+    dist.gather(tb, gb, dst=0)
+    dist.gather(tm, gm, dst=0)
+    out = None
+    if rank == 0:
+        c1 = build_unsharded()
+        assert c1.run(rounds_done) == rounds_done
+        so = c1.stats()
+        d1 = c1.digests(0, n_hosts).view(np.uint64).reshape(-1, width)
+        w1 = c1.window()
+        if hasattr(c1, "close"):
+            c1.close()
+        mism = []
+        metas = [m.numpy().view(np.uint64) for m in gm]
+        for r in range(world):
+            a, b = int(metas[r][0]), int(metas[r][1])
+            got = gb[r].numpy().view(np.uint64)[: b - a]
+            bad = np.nonzero((got != d1[a:b]).any(axis=1))[0]
+            if len(bad):
+                mism.append(f"rank {r}: {len(bad)} host digests differ (first HostId {a + int(bad[0])})")
+            if tuple(int(x) for x in metas[r][2:5]) != (w1[0], w1[1], int(w1[2])):
+                mism.append(f"rank {r}: window {metas[r][2:5].tolist()} vs {list(w1)}")
+        add_keys = [k for k in STAT_KEYS if k not in ("rounds", "min_used_latency_ns", "max_codel_len")]
+        for i, k in enumerate(STAT_KEYS):
+            vals = [int(m[5 + i]) for m in metas]
+            want = so[k]
+            got = sum(vals) if k in add_keys else (min(vals) if k == "min_used_latency_ns" else max(vals))
+            if got != want:
+                mism.append(f"{k}: shards {got} vs unsharded {want}")
+        out = {"ok": not mism, "mismatches": mism[:10], "rounds_compared": int(rounds_done),
+               "hosts_compared": int(n_hosts),
+               "reference": "one unsharded libsgn run of all hosts on rank 0's GPU (the path checked "
+                            "against the oracle at N=1)"}
+    dist.barrier()
+    return out
+
+
 def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
     """The CPU restatement of the reference's hot path (oracle/, a C++ port: the Rust
     reference cannot be built here), timed on this box's host cores, and the parity check of
@@ -231,6 +291,8 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
                     help="wall budget of the CPU mode samples after the parity run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shard-check", action="store_true",
+                    help="N > 1: skip the unsharded re-run on rank 0 that checks the sharded results")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -386,6 +448,19 @@ def main():
         out["parity"] = par["ok"]
         out["parity_detail"] = par
         ok = par["ok"]
+    if world > 1 and args.workload == "C" and not args.no_shard_check:
+        def unsharded():
+            c1 = sgn.Context(device=local)
+            c1.routes_build(g, used)
+            c1.hosts_set(hosts)
+            c1.sim_init(cfg, tr)
+            return c1
+
+        par = shard_check(ctx, dist, rank, world, hosts.n, int(st1["rounds"]), unsharded)
+        if rank == 0:
+            out["parity"] = par["ok"]
+            out["parity_detail"] = par
+            ok = par["ok"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

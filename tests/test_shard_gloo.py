@@ -26,7 +26,7 @@ def workload(kind):
     import sgn
 
     n, V = 240, 24
-    g = sgn.tor_graph(V, seed=4) if kind == "tgen" else sgn.random_graph(V, seed=4)
+    g = sgn.tor_graph(V, seed=4) if kind in ("tgen", "bench_check", "bench_check_bad") else sgn.random_graph(V, seed=4)
     used = np.arange(V)
     lat, loss = oracle_py.routes(g, used)
     seeds = oracle_py.host_seeds(1, sgn.host_names(n))
@@ -35,7 +35,7 @@ def workload(kind):
     dyn = kind == "dynamic"
     cfg = sgn.make_config(400_000_000, runahead_ns=0 if dyn else 1_000_000, dynamic=dyn,
                           codel_cap=1 << 14)
-    if kind == "tgen":
+    if kind in ("tgen", "bench_check", "bench_check_bad"):
         tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, period_ns=60_000_000, period_jitter_ns=60_000_000,
                               start_jitter_ns=30_000_000, servers=np.arange(0, n, 8),
                               file_bytes=(20_000, 80_000, 200_000))
@@ -92,6 +92,22 @@ def worker(rank, world, port, kind, q):
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             sim.shard_advance(from_i64(t[0].item()), from_i64(t[1].item()))
             rounds += 1
+        if kind in ("bench_check", "bench_check_bad"):
+            # bench.py's N > 1 verification, over this sharded run: rank 0 re-runs unsharded
+            sys.path.insert(0, str(ROOT))
+            import bench
+
+            def unsharded():
+                if kind == "bench_check_bad":  # a different run: the verdict must say so
+                    seeds = hosts.seed.copy()
+                    seeds[7] ^= 1
+                    h2 = sgn.HostArrays(hosts.ip, hosts.node_id, hosts.bw_up, hosts.bw_down, seeds)
+                    return oracle_py.Sim(used, lat, loss, h2, cfg, tr)
+                return oracle_py.Sim(used, lat, loss, hosts, cfg, tr)
+
+            out = bench.shard_check(sim, dist, rank, world, hosts.n, rounds, unsharded)
+            q.put((rank, out))
+            return
         q.put((rank, lo, hi, sim.digests(lo, hi), sim.stats(), sim.window(), rounds))
     finally:
         dist.destroy_process_group()
@@ -130,3 +146,29 @@ def test_two_shards_match_single(kind):
     for k in ("packets_sent", "packets_loss_dropped", "packet_events_popped", "delivered",
               "codel_dropped", "local_events"):
         assert total[k] == ref_st[k], k
+
+
+@pytest.mark.parametrize("kind", ["bench_check", "bench_check_bad"])
+def test_bench_shard_check_over_gloo(kind):
+    """bench.py's multi-GPU parity verdict (shard_check: gather every shard's digests and
+    counters, re-run unsharded on rank 0, compare) on two oracle shards over gloo; a
+    reference run that differs in one host's seed must be reported."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=worker, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    v = res[0]
+    assert v["hosts_compared"] == 240 and v["rounds_compared"] > 100
+    if kind == "bench_check":
+        assert v["ok"], v["mismatches"]
+    else:
+        assert not v["ok"] and any("HostId 7" in m for m in v["mismatches"]), v
