@@ -57,6 +57,22 @@ def build_workload(n_hosts, V, seed=1):
     return g, used, hosts, cfg, tr
 
 
+def build_workload_b(n_hosts, V, seed=1):
+    """Config B (BASELINE.json configs[1]): 10k hosts on a 1000-node random graph (mean degree
+    6, 20 % lossy edges), every host sends 1024 B UDP every 10 ms to a seeded random peer
+    (1 permille to addresses outside the simulation), 100 Mbit, 10 simulated seconds."""
+    g = sgn.random_graph(V, seed=42)
+    used = np.arange(V, dtype=np.uint32)
+    seeds = sgn.derive_seeds(seed, sgn.host_names(n_hosts))
+    bw = np.full(n_hosts, 100_000_000, dtype=np.uint64)
+    hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), (np.arange(n_hosts) % V).astype(np.uint32), bw, bw, seeds)
+    tr = sgn.make_traffic(sgn.TRAFFIC_PERIODIC, flow_seed=7, period_ns=10_000_000,
+                          start_jitter_ns=10_000_000, payload_len=1024, unknown_dst_permille=1)
+    cfg = sgn.make_config(10_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64, codel_cap=4096,
+                          event_capacity=1 << 22)
+    return g, used, hosts, cfg, tr
+
+
 def build_workload_d(n_hosts, V, seed=1):
     """Config D (BASELINE.json configs[3]): the config-B graph (1000-node random GML, mean
     degree 6, 20 % lossy edges, 100 Mbit), every host sends a 64 B datagram to a uniform
@@ -283,9 +299,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=("C", "D"), default="C",
-                    help="C: the headline 100k-host Tor-like tgen workload; D: 1M hosts, dense all-to-all")
-    ap.add_argument("--hosts", type=int, default=None, help="hosts per GPU (C: 100k, D: 1M)")
+    ap.add_argument("--workload", choices=("B", "C", "D"), default="C",
+                    help="C: the headline 100k-host Tor-like tgen workload; B: 10k hosts, UDP every 10 ms "
+                         "on a random graph; D: 1M hosts, dense all-to-all")
+    ap.add_argument("--hosts", type=int, default=None, help="hosts per GPU (B: 10k, C: 100k, D: 1M)")
     ap.add_argument("--nodes", type=int, default=1000)
     ap.add_argument("--rounds-per-step", type=int, default=100)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
@@ -303,10 +320,12 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
     if args.hosts is None:
-        args.hosts = 100_000 if args.workload == "C" else 1_000_000
+        args.hosts = {"B": 10_000, "C": 100_000, "D": 1_000_000}[args.workload]
     n_total = args.hosts * world
     if args.workload == "C":
         g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
+    elif args.workload == "B":
+        g, used, hosts, cfg, tr = build_workload_b(n_total, args.nodes)
     else:
         g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes)
         # calendar slabs for ~64 due runs per host group and bucket (+ fluctuation)
@@ -396,8 +415,8 @@ def main():
         if tf.exists():
             t = json.loads(tf.read_text())
             wl = t.get("workload", {})
-            if (wl.get("hosts_per_gpu"), wl.get("graph_nodes"), wl.get("rounds_per_launch"), wl.get("n_gpus"),
-                    t.get("kernel")) == (args.hosts, args.nodes, round(rpl), world, rk):
+            if (wl.get("name"), wl.get("hosts_per_gpu"), wl.get("graph_nodes"), wl.get("rounds_per_launch"),
+                    wl.get("n_gpus"), t.get("kernel")) == (args.workload, args.hosts, args.nodes, round(rpl), world, rk):
                 roof["traffic"] = t["traffic_bytes_per_launch"]
                 roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
                 roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
@@ -416,8 +435,10 @@ def main():
         "dtype": "u64",
         "data": "synthetic",
         "config": {
-            "workload": ("C: Tor-like 1000-node complete graph, tgen-style UDP trains" if args.workload == "C" else
-                         "D: 1000-node random graph, every host sends 64 B to a uniform random peer every 1 ms"),
+            "workload": {"C": "C: Tor-like 1000-node complete graph, tgen-style UDP trains",
+                         "B": "B: 1000-node random graph (20 % lossy edges), 1024 B UDP every 10 ms to random peers",
+                         "D": "D: 1000-node random graph, every host sends 64 B to a uniform random peer every 1 ms",
+                         }[args.workload],
             "hosts_per_gpu": args.hosts, "hosts_total": n_total, "graph_nodes": args.nodes,
             "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
             "parallelism": f"host-shard x{world}",
