@@ -202,18 +202,36 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
     import oracle_py
 
     cores, visible, model = cpu_share()
+    last = [time.perf_counter()]
+
+    def progress(msg):  # long CPU phases keep writing (a silent GPU-box command is taken as hung)
+        if time.perf_counter() - last[0] > 15:
+            print(f"bench: cpu baseline: {msg}", file=sys.stderr, flush=True)
+            last[0] = time.perf_counter()
+
+    def run_rounds(sim, n, what):
+        done = 0
+        while done < n:
+            k = sim.run(min(25, n - done))
+            done += k
+            progress(f"{what} {done}/{n} rounds")
+            if k == 0:
+                break
+        return done
+
     apsp = {}
     for faithful in (True, False):
         for th in (cores, 1):
             t0 = time.perf_counter()
             lat, loss = oracle_py.routes(g, used, faithful=faithful, threads=th)
             apsp[f"{'faithful' if faithful else 'optimised'}_{th}c_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+            progress(f"APSP faithful={faithful} threads={th}")
     sim = oracle_py.Sim(used, lat, loss, hosts, cfg, tr, threads=cores)
     warm = args.warmup * args.rounds_per_step
-    assert sim.run(warm) == warm
+    assert run_rounds(sim, warm, "parity warm-up") == warm
     st0 = sim.stats()
     t0 = time.perf_counter()
-    timed_rounds = sim.run(gpu["rounds_timed"])
+    timed_rounds = run_rounds(sim, gpu["rounds_timed"], "parity replay of the timed rounds")
     el = time.perf_counter() - t0
     ev = events_of(sim.stats()) - events_of(st0)
     # parity with the GPU run: same rounds, same counters, same window, same digests
@@ -241,6 +259,7 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
         r = 0
         while time.perf_counter() - t1 < budget and sim.window()[2]:
             r += sim.run(20)
+            progress(f"{name} sample")
         e1 = time.perf_counter() - t1
         e = events_of(sim.stats()) - s0
         modes[name] = {"value": e / e1, "cores": th, "rounds": r, "events": e, "wall_s": round(e1, 2),

@@ -15,6 +15,8 @@ import sgn
 if len(sys.argv) > 1 and sys.argv[1] == "D":
     g, used, hosts, cfg, tr = bench.build_workload_d(1_000_000, 1000)
     cfg.event_capacity = 257 * 15_626 * 192
+elif len(sys.argv) > 1 and sys.argv[1] == "B":
+    g, used, hosts, cfg, tr = bench.build_workload_b(10_000, 1000)
 else:
     g, used, hosts, cfg, tr = bench.build_workload(int(sys.argv[1]) if len(sys.argv) > 1 else 100_000, 1000)
 ctx = sgn.Context(flags=2)

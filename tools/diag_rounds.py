@@ -12,7 +12,10 @@ import numpy as np
 import bench
 import sgn
 
-g, used, hosts, cfg, tr = bench.build_workload(100_000, 1000)
+if len(sys.argv) > 1 and sys.argv[1] == "B":
+    g, used, hosts, cfg, tr = bench.build_workload_b(10_000, 1000)
+else:
+    g, used, hosts, cfg, tr = bench.build_workload(100_000, 1000)
 ctx = sgn.Context(flags=2)
 ctx.routes_build(g, used)
 ctx.hosts_set(hosts)
