@@ -255,7 +255,9 @@ struct LaneLDS {
 
 // kTrace: the per-packet trace can be on (k_execute). The persistent k_rounds is built
 // without it (its registers are fully used; a traced run executes round by round).
-template <bool kTrace>
+// kApp: the traffic kind (SGN_TRAFFIC_*), fixed per instantiation so that each kernel
+// carries only its application's code (fewer registers, no dead branches).
+template <bool kTrace, uint32_t kApp>
 struct HostExec {
   const DevSim& S;
   SGN_GLB Ctrl* C;
@@ -391,7 +393,8 @@ struct HostExec {
     r.dig[0] = L->dig[0];
     r.dig[1] = L->dig[1];
     r.dig[2] = L->dig[2];
-    r.flags = fl;
+    if (fl & F_FH_DIRTY) *fq_slot(0) = L->fh;  // a queued head that lived in LDS
+    r.flags = fl & ~F_FH_DIRTY;
     r.ro_dst = ro_dst;
     r.ro_pay = ro_pay;
     r.ro_tag = ro_tag;
@@ -501,7 +504,7 @@ struct HostExec {
     r.tag = tag;
     S.drain[pos] = r;
   }
-  __device__ __forceinline__ bool external() const { return S.tkind == SGN_TRAFFIC_EXTERNAL; }
+  __device__ __forceinline__ bool external() const { return kApp == SGN_TRAFFIC_EXTERNAL; }
 
   // ---- local event slots: Host::schedule_task_* / push_local_event (host.rs:703-722);
   //      Event::new_local consumes an event id even if the event is then dropped ----
@@ -749,10 +752,15 @@ struct HostExec {
     e.pay = (payload & 0xFFFFu) | (last << 16);
     e.count = count;
     e.tag = tag;
-    *fq_slot(fq_len) = e;
-    if (fq_len == 0) {  // the new head: keep its copy
+    if (fq_len == 0) {
+      // the new head lives in LDS only: most are sent within the round, and a global store
+      // here would hold up the wave's next dependent load (stores and loads share vmcnt);
+      // store() writes it back if it is still queued
       L->fh = e;
       L->fh_idx = fq_head;
+      fl |= F_FH_DIRTY;
+    } else {
+      *fq_slot(fq_len) = e;
     }
     fq_len++;
     return true;
@@ -795,7 +803,7 @@ struct HostExec {
         trace(SGN_TRACE_DELIVER, src, 0, now, (uint64_t)payload | ((uint64_t)tag << 32), e0 + k);
     if (external())
       for (uint32_t k = 0; k < m; k++) drain_rec(SGN_DRAIN_DELIVERED, src, gid, e0 + k, payload, tag);
-    if (S.tkind == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
+    if (kApp == SGN_TRAFFIC_TGEN && (fl & F_SERVER) && (tag & SGN_TAG_REQ)) {
       const uint32_t c = tag & 3u;  // the class picks one of three (scalar) sizes
       const uint64_t size = c == 0 ? S.file_bytes[0] : (c == 1 ? S.file_bytes[1] : S.file_bytes[2]);
       const uint64_t n = (size + SGN_TGEN_MSS - 1) / SGN_TGEN_MSS;
@@ -1208,6 +1216,7 @@ struct HostExec {
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         fq_len--;
+        fl &= ~F_FH_DIRTY;
       } else if (rr) {
         // the socket still has data: re-queued behind the others (same length)
         FifoEnt m = e;
@@ -1215,8 +1224,9 @@ struct HostExec {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         *fq_slot(fq_len - 1) = m;
         L->fh_idx = NO_HOST;  // the cached head is stale
+        fl &= ~F_FH_DIRTY;
       } else {
-        fq_slot(0)->count = e.count - consumed;
+        if (!(fl & F_FH_DIRTY)) fq_slot(0)->count = e.count - consumed;
         L->fh.count = e.count - consumed;
       }
       if (blocked) {
@@ -1249,7 +1259,7 @@ struct HostExec {
     const uint64_t k = L->app_k++;
     uint32_t dst, payload, tag, uip = 0;
     uint64_t next_delay;
-    if (S.tkind == SGN_TRAFFIC_PERIODIC) {
+    if (kApp == SGN_TRAFFIC_PERIODIC) {
       uint32_t peer = 0;
       // an address outside the simulation (10.255.0.0/16, never registered) is NO_HOST
       dst = sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip)
@@ -1517,7 +1527,7 @@ struct ExecLDS {
 // at_end(kmin, next) runs once the group's cross-workgroup data (calendar records, slab
 // fills, minima) is issued and before the host records are written back: the round's
 // arrival goes there, so its wait covers only what other workgroups read.
-template <bool kTrace, typename AtEnd>
+template <bool kTrace, uint32_t kApp, typename AtEnd>
 __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
                            const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out,
                            AtEnd&& at_end) {
@@ -1555,7 +1565,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     ob->hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
   }
   __syncthreads();
-  HostExec<kTrace> ex(S, h, we, be, ks, lslot + lane, lbs, ob);
+  HostExec<kTrace, kApp> ex(S, h, we, be, ks, lslot + lane, lbs, ob);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -1828,6 +1838,7 @@ __device__ bool arrive(const DevSim& S, uint32_t w, uint32_t nw, uint64_t kmin, 
 
 // One round per launch: one workgroup (one wave) per group; single shard: the last arrival
 // runs the round edge (finalize_fused), multi-shard: comm.cpp's exchange follows.
+template <uint32_t kApp>
 __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg) {
   // the simulation constants are read from device memory where they are used (a by-value
   // kernel argument would pin ~90 scalar registers for the whole kernel)
@@ -1843,7 +1854,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
-  exec_group<true>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+  exec_group<true, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
     last = arrive(S, blockIdx.x, gridDim.x, k, n);
   });
   if (!last) return;
@@ -1945,6 +1956,7 @@ __device__ __forceinline__ void rb_bookkeep(const DevSim& S, uint64_t ws, uint64
 // with one CU). Data another workgroup wrote in this launch is read with device-scope loads
 // (event records, slab fills, bucket minima, the round buffers); the rest (host records,
 // queues) belongs to this workgroup's groups.
+template <uint32_t kApp>
 __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds) {
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
@@ -2032,7 +2044,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
       const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
-      exec_group<false>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+      exec_group<false, kApp>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
         if (lastg) {
@@ -2277,14 +2289,49 @@ constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then 
 
 namespace {
 
+// the round kernels of the simulation's traffic kind
+const void* execute_fn(uint32_t kind) {
+  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_execute<SGN_TRAFFIC_TGEN>;
+  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_execute<SGN_TRAFFIC_EXTERNAL>;
+  return (const void*)k_execute<SGN_TRAFFIC_PERIODIC>;
+}
+const void* rounds_fn(uint32_t kind) {
+  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_rounds<SGN_TRAFFIC_TGEN>;
+  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_rounds<SGN_TRAFFIC_EXTERNAL>;
+  return (const void*)k_rounds<SGN_TRAFFIC_PERIODIC>;
+}
+void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
+  const uint32_t k = ctx->S.tkind;
+  const dim3 grid(ctx->S.G), block(64);
+  const size_t lds = exec_lds_bytes(ctx->S.CAP);
+  const DevSim* d = (const DevSim*)ctx->d_S;
+  if (k == SGN_TRAFFIC_TGEN)
+    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_TGEN>, grid, block, lds, st, d);
+  else if (k == SGN_TRAFFIC_EXTERNAL)
+    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_EXTERNAL>, grid, block, lds, st, d);
+  else
+    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_PERIODIC>, grid, block, lds, st, d);
+}
+void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
+  const uint32_t k = ctx->S.tkind;
+  const dim3 grid(ctx->persist_grid), block(64);
+  const size_t lds = exec_lds_bytes(ctx->S.CAP);
+  const DevSim* d = (const DevSim*)ctx->d_S;
+  if (k == SGN_TRAFFIC_TGEN)
+    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_TGEN>, grid, block, lds, ctx->stream, d, n);
+  else if (k == SGN_TRAFFIC_EXTERNAL)
+    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_EXTERNAL>, grid, block, lds, ctx->stream, d, n);
+  else
+    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_PERIODIC>, grid, block, lds, ctx->stream, d, n);
+}
+
 int launch_round(sgn_ctx* ctx) {
-  DevSim& S = ctx->S;
   // a multi-shard round needs its exchange transport before anything is launched
   if (ctx->nranks > 1 && !ctx->comm)
     return set_error(ctx, SGN_ESTATE, "multi-shard round without an RCCL communicator");
   hipStream_t st = ctx->stream;
   time_begin(ctx, K_EXECUTE);
-  hipLaunchKernelGGL(k_execute, dim3(S.G), dim3(64), exec_lds_bytes(S.CAP), st, (const DevSim*)ctx->d_S);
+  launch_k_execute(ctx, st);
   time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
@@ -2330,7 +2377,7 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
   ctx->graph_timed.clear();
   if (!all && !exec) return 0;
-  const void* fn[K_NUM] = {(const void*)k_execute, (const void*)k_import,
+  const void* fn[K_NUM] = {execute_fn(ctx->S.tkind), (const void*)k_import,
                            (const void*)k_advance};
   size_t n = 0;
   SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
@@ -2732,9 +2779,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     int occ = 0, ncu = 0;
     const size_t dyn = exec_lds_bytes((uint32_t)CAP);
     hipFuncAttributes fa{};
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_rounds, 64, dyn) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rounds_fn(S.tkind), 64, dyn) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
-        hipFuncGetAttributes(&fa, (const void*)k_rounds) == hipSuccess && occ > 0 && ncu > 0) {
+        hipFuncGetAttributes(&fa, rounds_fn(S.tkind)) == hipSuccess && occ > 0 && ncu > 0) {
       // LDS is allocated per workgroup in 512-byte granules (a 23184-byte workgroup fits 6
       // per CU, not 7: a grid sized for 7 was not resident and its barrier timed out)
       const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
@@ -2814,8 +2861,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * 2 + 4) * 8, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, 3 * (RB_CH + 1) * 4, ctx->stream));
       time_begin(ctx, K_EXECUTE);
-      hipLaunchKernelGGL(k_rounds, dim3(ctx->persist_grid), dim3(64), exec_lds_bytes(ctx->S.CAP),
-                         ctx->stream, (const DevSim*)ctx->d_S, n);
+      launch_k_rounds(ctx, n);
       time_end(ctx);
       SGN_HIP(ctx, hipGetLastError());
       if ((rc = sync_ctrl(ctx))) return rc;
@@ -3371,10 +3417,7 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
 
 // hooks used by comm.cpp
 namespace sgn {
-void launch_execute(sgn_ctx* ctx) {
-  hipLaunchKernelGGL(k_execute, dim3(ctx->S.G), dim3(64), exec_lds_bytes(ctx->S.CAP), ctx->stream,
-                     (const DevSim*)ctx->d_S);
-}
+void launch_execute(sgn_ctx* ctx) { launch_k_execute(ctx, ctx->stream); }
 void launch_import(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_import, dim3(256), dim3(256), 0, ctx->stream, ctx->S);
 }

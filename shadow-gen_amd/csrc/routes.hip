@@ -279,6 +279,107 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
   }
 }
 
+// Tight arcs for S sources at once (u32 latency form): a workgroup holds the S sources'
+// distance rows interleaved in LDS (row[u * S + k] = d[source k][u], so one arc's S tests are
+// two 8-S-byte reads) and sweeps one P-th of the arc list; each arc load now serves S sources
+// instead of one (the single-source sweep re-read the whole arc list once per source, from
+// L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
+template <int S>
+__global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
+                                                  uint32_t U, const uint32_t* auv, const uint64_t* al,
+                                                  uint32_t E2, uint32_t capg, uint32_t* tcnt,
+                                                  uint32_t* tlist) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* row = (uint32_t*)smem;  // [Vp][S]
+  const uint32_t g0 = blockIdx.x * S;
+  for (uint32_t i = threadIdx.x; i < Vp * S; i += blockDim.x) {
+    const uint32_t u = i / S, k = i % S;
+    row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
+  }
+  __syncthreads();
+  const uint32_t per = (E2 + gridDim.y - 1) / gridDim.y;
+  const uint32_t e0 = blockIdx.y * per, e1 = min(E2, e0 + per);
+  for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const uint32_t uv = auv[e];
+    const uint64_t l = al[e];
+    if (l >= SQ_INF) continue;  // no u32 path is that long: never tight
+    const uint32_t* du = row + (uv & 0xFFFFu) * S;
+    const uint32_t* dv = row + (uv >> 16) * S;
+    uint32_t a[S], b[S];
+#pragma unroll
+    for (int k = 0; k < S; k += 2) {
+      const uint2 x = *(const uint2*)(du + k), y = *(const uint2*)(dv + k);
+      a[k] = x.x;
+      a[k + 1] = x.y;
+      b[k] = y.x;
+      b[k + 1] = y.y;
+    }
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      if (a[k] == SQ_INF || (uint64_t)a[k] + l != (uint64_t)b[k]) continue;
+      const uint32_t src = g0 + k;
+      const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+      if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+    }
+  }
+}
+
+// The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
+// then the fixed point as in loss_pass. (tcnt > capg: the caller reruns loss_pass instead.)
+__global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
+                                                 const float* ap, const uint32_t* tcnt, const uint32_t* tlist,
+                                                 uint32_t capg, uint32_t cap, float* Lout, uint32_t* iters) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* L = (float*)smem;
+  uint32_t* tuv = (uint32_t*)(L + Vp);
+  float* tp = (float*)(tuv + cap);
+  uint32_t* ctl = (uint32_t*)(tp + cap);
+  const uint32_t s = usrc[blockIdx.x];
+  const uint32_t nt = min(tcnt[blockIdx.x], capg);
+  const bool in_lds = nt <= cap;
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) L[v] = 2.0f;
+  if (in_lds)
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+      const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
+      tuv[i] = auv[e];
+      tp[i] = ap[e];
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) L[s] = 0.0f;
+  uint32_t it = 0;
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) ctl[0] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+      uint32_t uv;
+      float pe;
+      if (in_lds) {
+        uv = tuv[i];
+        pe = tp[i];
+      } else {
+        const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
+        uv = auv[e];
+        pe = ap[e];
+      }
+      const float lu = L[uv & 0xFFFFu];
+      if (lu > 1.0f) continue;
+      const float cand = __fsub_rn(1.0f, __fmul_rn(__fsub_rn(1.0f, lu), __fsub_rn(1.0f, pe)));
+      const uint32_t cb = __float_as_uint(cand);
+      float* lv = &L[uv >> 16];
+      if (cb < __float_as_uint(*lv)) {
+        const uint32_t old = atomicMin((unsigned int*)lv, cb);
+        if (cb < old) ctl[0] = 1;
+      }
+    }
+    __syncthreads();
+    it++;
+    if (!ctl[0]) break;
+  }
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) Lout[(uint64_t)blockIdx.x * Vp + v] = L[v];
+  if (threadIdx.x == 0) iters[blockIdx.x] = it | (in_lds ? 0u : 0x80000000u);
+}
+
 // Tight-arc loss fold, one workgroup per used source. The arcs that are tight for the
 // source (d[s][u] + lat(u,v) == d[s][v]) are found in ONE sweep over the arc list and kept in
 // LDS (packed u | v << 16 and the arc's loss); the fixed point then iterates over that short
@@ -637,11 +738,55 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipEventRecord(e1, st));
-    hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
-                       (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
-                       (float*)dL.p, (uint32_t*)dit.p);
-    SGN_HIP(ctx, hipGetLastError());
-    SGN_HIP(ctx, hipEventRecord(e2, st));
+    // loss phase. u32 form: multi-source tight sweep + per-source fold (each arc load serves
+    // kS sources); u64 form, a tight-list overflow, or SGN_APSP_LOSS1: the one-source kernel
+    const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
+    const int kS = Vp <= 2048 ? 8 : (Vp <= 4096 ? 4 : 2);
+    const size_t lds_sw = (size_t)Vp * kS * 4;
+    const size_t lds_fold = (size_t)Vp * 4 + (size_t)cap * 8 + 16;
+    bool multi = fast && !getenv("SGN_APSP_LOSS1") && lds_sw <= 64 * 1024 && lds_fold <= 160 * 1024;
+    DevBuf dtc, dtl;
+    if (multi) {
+      SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
+      SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
+      SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+      const uint32_t groups = (U + kS - 1) / kS;
+      const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
+      const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
+      const uint32_t* d32 = (const uint32_t*)dD32.p;
+      if (kS == 8)
+        hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
+                           (uint32_t*)dtl.p);
+      else if (kS == 4)
+        hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
+                           (uint32_t*)dtl.p);
+      else
+        hipLaunchKernelGGL(loss_sweep<2>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
+                           (uint32_t*)dtl.p);
+      hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
+                         (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
+                         (const uint32_t*)dtl.p, capg, cap, (float*)dL.p, (uint32_t*)dit.p);
+      SGN_HIP(ctx, hipGetLastError());
+      SGN_HIP(ctx, hipEventRecord(e2, st));
+      // a source with more tight arcs than its global list: redo the phase the one-source way
+      std::vector<uint32_t> tc(U);
+      SGN_HIP(ctx, hipMemcpyAsync(tc.data(), dtc.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
+      SGN_HIP(ctx, hipStreamSynchronize(st));
+      for (uint32_t x : tc)
+        if (x > capg) multi = false;
+      tm.loss_multi = multi ? (uint32_t)kS : 0u;
+    }
+    if (!multi) {
+      hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
+                         (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
+                         (float*)dL.p, (uint32_t*)dit.p);
+      tm.loss_multi = 0;
+      SGN_HIP(ctx, hipGetLastError());
+      SGN_HIP(ctx, hipEventRecord(e2, st));
+    }
     hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
                        (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p, (const float*)dsp.p,
                        ctx->d_lat, ctx->d_loss, (unsigned long long*)dres.p);

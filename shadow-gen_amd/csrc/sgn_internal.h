@@ -168,6 +168,7 @@ enum : uint32_t {
   F_CODEL_DN = 0x200u,       // CoDel drop_next is Some
   F_HAS_APP = 0x400u,        // host runs a synthetic app timer
   F_RO_CONT = 0x800u,        // inside relay_inet_out's forwarding task (never stored)
+  F_FH_DIRTY = 0x1000u,      // the send queue's head exists only in LDS (never stored)
 };
 
 enum { SLOT_RO = 0, SLOT_RI = 1, SLOT_APP = 2, NSLOT = 3 };

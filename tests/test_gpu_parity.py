@@ -98,6 +98,38 @@ def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle):
     assert t["latency_u64"] == 0 and 1 <= t["latency_passes"] <= 8
 
 
+def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
+    """The loss phase's multi-source tight sweep (u32 form) against the oracle and against the
+    one-source kernel (SGN_APSP_LOSS1), incl. a graph whose sources have more tight arcs than
+    the per-source list holds (complete bipartite layers of equal latency: |A| x |B| ties),
+    which falls back to the one-source kernel."""
+    cases = [sgn.tor_graph(600, seed=3), sgn.random_graph(1500, seed=8, loss_frac=0.5)]
+    a, b = 90, 90  # s -> A (1 ms) -> B (1 ms): every A x B arc is tight for s
+    src = [0] * a + [1 + i for i in range(a) for _ in range(b)]
+    dst = list(range(1, a + 1)) + [1 + a + j for _ in range(a) for j in range(b)]
+    n = 1 + a + b
+    rng = np.random.default_rng(1)
+    lossy = np.round(rng.uniform(0, 0.01, len(src)), 6).astype(np.float32)
+    cases.append(sgn.GraphArrays(np.arange(n), src + list(range(n)), dst + list(range(n)),
+                                 [1_000_000] * len(src) + [1_000_000] * n,
+                                 np.concatenate([lossy, np.zeros(n, np.float32)]), False))
+    for k, g in enumerate(cases):
+        used = np.arange(len(g.node_id))
+        ol, op = oracle.routes(g, used)
+        c = ctxf()
+        c.routes_build(g, used)
+        t = c.routes_timing()
+        gl, gp = c.routes_copy()
+        assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), k
+        assert t["loss_multi"] == (0 if k == 2 else 8), (k, t)
+        monkeypatch.setenv("SGN_APSP_LOSS1", "1")
+        c.routes_build(g, used)
+        monkeypatch.delenv("SGN_APSP_LOSS1")
+        g1, p1 = c.routes_copy()
+        assert c.routes_timing()["loss_multi"] == 0
+        assert np.array_equal(gl, g1) and np.array_equal(gp.view(np.uint32), p1.view(np.uint32)), k
+
+
 def test_apsp_errors(ctxf):
     c = ctxf()
     g = sgn.GraphArrays([0, 1], [0, 0, 1], [1, 0, 1], [5, 3, 3], [0, 0, 0], False)

@@ -61,7 +61,9 @@ def test_round_kernels_have_no_scratch():
     # or a spill puts it in scratch memory and costs ~2x (seen when send_batch was outlined)
     meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
     for k in ("k_rounds", "k_execute"):
-        (name,) = [n for n in meta if k in n]
-        m = meta[name]
-        assert m["private_segment_fixed_size"] == 0, (k, m)
-        assert m["vgpr_spill_count"] == 0 and m["vgpr_count"] <= 256, (k, m)
+        names = [n for n in meta if k in n]
+        assert len(names) == 3, names  # one instantiation per traffic kind
+        for name in names:
+            m = meta[name]
+            assert m["private_segment_fixed_size"] == 0, (name, m)
+            assert m["vgpr_spill_count"] == 0 and m["vgpr_count"] <= 256, (name, m)

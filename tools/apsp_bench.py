@@ -26,21 +26,24 @@ def run(kind, V):
     t = ts[-1]
     return {"graph": kind, "V": V, "arcs": int(t["n_tight_edges"]), "first_build_ms": round(ts[0]["total_ms"], 3),
             **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()},
-            "form": "u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring"}
+            "form": "u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring",
+            "loss_form": f"{t['loss_multi']}-source sweep + fold" if t["loss_multi"] else "one-source pass"}
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 2:
         print(json.dumps(run(sys.argv[1], int(sys.argv[2]))), flush=True)
         sys.exit(0)
-    for fw in (False, True):
+    for mode in ("default", "loss1", "fw"):
         for kind in ("tor", "random"):
             for V in (1000, 2000):
                 env = dict(os.environ)
-                if fw:
+                env.pop("SGN_APSP_FW", None)
+                env.pop("SGN_APSP_LOSS1", None)
+                if mode == "fw":
                     env["SGN_APSP_FW"] = "1"
-                else:
-                    env.pop("SGN_APSP_FW", None)
+                elif mode == "loss1":
+                    env["SGN_APSP_LOSS1"] = "1"
                 r = subprocess.run([sys.executable, __file__, kind, str(V)], env=env, capture_output=True, text=True)
                 sys.stdout.write(r.stdout)
                 if r.returncode:
