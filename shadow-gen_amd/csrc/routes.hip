@@ -281,12 +281,12 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
 
 // Tight arcs for S sources at once (u32 latency form): a workgroup holds the S sources'
 // distance rows interleaved in LDS (row[u * S + k] = d[source k][u], so one arc's S tests are
-// two 8-S-byte reads) and sweeps one P-th of the arc list; each arc load now serves S sources
+// two 4S-byte reads; arcs are 8 bytes: u | v << 16 and the u32 latency) and sweeps one P-th of the arc list; each arc load now serves S sources
 // instead of one (the single-source sweep re-read the whole arc list once per source, from
 // L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
 template <int S>
 __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
-                                                  uint32_t U, const uint32_t* auv, const uint64_t* al,
+                                                  uint32_t U, const uint32_t* auv, const uint32_t* al32,
                                                   uint32_t E2, uint32_t capg, uint32_t* tcnt,
                                                   uint32_t* tlist) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -301,18 +301,32 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
   const uint32_t e0 = blockIdx.y * per, e1 = min(E2, e0 + per);
   for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
     const uint32_t uv = auv[e];
-    const uint64_t l = al[e];
-    if (l >= SQ_INF) continue;  // no u32 path is that long: never tight
+    const uint32_t l = al32[e];  // SQ_INF: 2^32 - 1 ns or more
+    if (l == SQ_INF) continue;   // no u32 path is that long: never tight
     const uint32_t* du = row + (uv & 0xFFFFu) * S;
     const uint32_t* dv = row + (uv >> 16) * S;
     uint32_t a[S], b[S];
 #pragma unroll
     for (int k = 0; k < S; k += 2) {
-      const uint2 x = *(const uint2*)(du + k), y = *(const uint2*)(dv + k);
-      a[k] = x.x;
-      a[k + 1] = x.y;
-      b[k] = y.x;
-      b[k + 1] = y.y;
+      if constexpr (S >= 4) {
+        if (k % 4 == 0) {
+          const uint4 x = *(const uint4*)(du + k), y = *(const uint4*)(dv + k);
+          a[k] = x.x;
+          a[k + 1] = x.y;
+          a[k + 2] = x.z;
+          a[k + 3] = x.w;
+          b[k] = y.x;
+          b[k + 1] = y.y;
+          b[k + 2] = y.z;
+          b[k + 3] = y.w;
+        }
+      } else {
+        const uint2 x = *(const uint2*)(du + k), y = *(const uint2*)(dv + k);
+        a[k] = x.x;
+        a[k + 1] = x.y;
+        b[k] = y.x;
+        b[k + 1] = y.y;
+      }
     }
 #pragma unroll
     for (int k = 0; k < S; k++) {
@@ -741,12 +755,29 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     // loss phase. u32 form: multi-source tight sweep + per-source fold (each arc load serves
     // kS sources); u64 form, a tight-list overflow, or SGN_APSP_LOSS1: the one-source kernel
     const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
-    const int kS = Vp <= 2048 ? 8 : (Vp <= 4096 ? 4 : 2);
-    const size_t lds_sw = (size_t)Vp * kS * 4;
     const size_t lds_fold = (size_t)Vp * 4 + (size_t)cap * 8 + 16;
-    bool multi = fast && !getenv("SGN_APSP_LOSS1") && lds_sw <= 64 * 1024 && lds_fold <= 160 * 1024;
-    DevBuf dtc, dtl;
+    // dense graphs only: a sparse arc list is re-read from L2 cheaply source by source
+    bool multi = fast && !getenv("SGN_APSP_LOSS1") && E2 >= 32ull * Vp && lds_fold <= 160 * 1024;
+    // sources per workgroup: the largest whose rows fit the LDS a workgroup may have
+    int kS = 0;
+    for (int k : {16, 8, 4, 2}) {
+      const size_t b = (size_t)Vp * k * 4;
+      if (!multi || b > 160 * 1024) continue;
+      const void* f = k == 16 ? (const void*)loss_sweep<16> : k == 8 ? (const void*)loss_sweep<8>
+                    : k == 4 ? (const void*)loss_sweep<4> : (const void*)loss_sweep<2>;
+      if (b <= 64 * 1024 || hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
+        kS = k;
+        break;
+      }
+      (void)hipGetLastError();
+    }
+    if (!kS) multi = false;
+    const size_t lds_sw = (size_t)Vp * kS * 4;
+    DevBuf dtc, dtl, dal32;
     if (multi) {
+      std::vector<uint32_t> al32(E2);
+      for (uint32_t e = 0; e < E2; e++) al32[e] = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
+      if ((rc = upload(ctx, dal32, al32.data(), E2))) return rc;
       SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
       SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
@@ -754,18 +785,19 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
       const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
       const uint32_t* d32 = (const uint32_t*)dD32.p;
-      if (kS == 8)
+      const uint32_t* a32 = (const uint32_t*)dal32.p;
+      if (kS == 16)
+        hipLaunchKernelGGL(loss_sweep<16>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+      else if (kS == 8)
         hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
-                           (uint32_t*)dtl.p);
+                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       else if (kS == 4)
         hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
-                           (uint32_t*)dtl.p);
+                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       else
         hipLaunchKernelGGL(loss_sweep<2>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, capg, (uint32_t*)dtc.p,
-                           (uint32_t*)dtl.p);
+                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
                          (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
                          (const uint32_t*)dtl.p, capg, cap, (float*)dL.p, (uint32_t*)dit.p);

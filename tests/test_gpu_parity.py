@@ -99,11 +99,12 @@ def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle):
 
 
 def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
-    """The loss phase's multi-source tight sweep (u32 form) against the oracle and against the
-    one-source kernel (SGN_APSP_LOSS1), incl. a graph whose sources have more tight arcs than
-    the per-source list holds (complete bipartite layers of equal latency: |A| x |B| ties),
-    which falls back to the one-source kernel."""
-    cases = [sgn.tor_graph(600, seed=3), sgn.random_graph(1500, seed=8, loss_frac=0.5)]
+    """The loss phase's multi-source tight sweep (u32 form, complete graphs; 96 KB of rows per
+    workgroup at V = 1500) against the oracle and against the one-source kernel
+    (SGN_APSP_LOSS1); a sparse graph takes the one-source kernel, and a graph whose sources
+    have more tight arcs than the per-source list holds (complete bipartite layers of equal
+    latency: |A| x |B| ties) falls back to it."""
+    cases = [sgn.tor_graph(600, seed=3), sgn.tor_graph(1500, seed=4), sgn.random_graph(1500, seed=8, loss_frac=0.5)]
     a, b = 90, 90  # s -> A (1 ms) -> B (1 ms): every A x B arc is tight for s
     src = [0] * a + [1 + i for i in range(a) for _ in range(b)]
     dst = list(range(1, a + 1)) + [1 + a + j for _ in range(a) for j in range(b)]
@@ -121,7 +122,7 @@ def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
         t = c.routes_timing()
         gl, gp = c.routes_copy()
         assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), k
-        assert t["loss_multi"] == (0 if k == 2 else 8), (k, t)
+        assert (t["loss_multi"] >= 8) == (k < 2), (k, t)  # dense: multi-source; sparse / overflow: one-source
         monkeypatch.setenv("SGN_APSP_LOSS1", "1")
         c.routes_build(g, used)
         monkeypatch.delenv("SGN_APSP_LOSS1")
