@@ -285,10 +285,31 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
 // instead of one (the single-source sweep re-read the whole arc list once per source, from
 // L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
 template <int S>
+__device__ __forceinline__ void sweep_arc(const uint32_t* row, uint32_t g0, uint32_t uv, uint32_t l, uint32_t e,
+                                          uint32_t capg, uint32_t* tcnt, uint32_t* tlist) {
+  if (l == SQ_INF) return;  // 2^32 - 1 ns or more: no u32 path is that long, never tight
+  const uint32_t* du = row + (uv & 0xFFFFu) * S;
+  const uint32_t* dv = row + (uv >> 16) * S;
+#pragma unroll
+  for (int k = 0; k < S; k += 4) {
+    const uint4 x = *(const uint4*)(du + k), y = *(const uint4*)(dv + k);
+    const uint32_t a[4] = {x.x, x.y, x.z, x.w}, b[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (a[j] == SQ_INF || (uint64_t)a[j] + l != (uint64_t)b[j]) continue;
+      const uint32_t src = g0 + k + j;
+      const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+      if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+    }
+  }
+}
+
+template <int S>
 __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
                                                   uint32_t U, const uint32_t* auv, const uint32_t* al32,
                                                   uint32_t E2, uint32_t capg, uint32_t* tcnt,
                                                   uint32_t* tlist) {
+  static_assert(S % 4 == 0, "rows are read 4 sources at a time");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* row = (uint32_t*)smem;  // [Vp][S]
   const uint32_t g0 = blockIdx.x * S;
@@ -297,45 +318,33 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
     row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
   }
   __syncthreads();
-  const uint32_t per = (E2 + gridDim.y - 1) / gridDim.y;
-  const uint32_t e0 = blockIdx.y * per, e1 = min(E2, e0 + per);
-  for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint32_t uv = auv[e];
-    const uint32_t l = al32[e];  // SQ_INF: 2^32 - 1 ns or more
-    if (l == SQ_INF) continue;   // no u32 path is that long: never tight
-    const uint32_t* du = row + (uv & 0xFFFFu) * S;
-    const uint32_t* dv = row + (uv >> 16) * S;
-    uint32_t a[S], b[S];
-#pragma unroll
-    for (int k = 0; k < S; k += 2) {
-      if constexpr (S >= 4) {
-        if (k % 4 == 0) {
-          const uint4 x = *(const uint4*)(du + k), y = *(const uint4*)(dv + k);
-          a[k] = x.x;
-          a[k + 1] = x.y;
-          a[k + 2] = x.z;
-          a[k + 3] = x.w;
-          b[k] = y.x;
-          b[k + 1] = y.y;
-          b[k + 2] = y.z;
-          b[k + 3] = y.w;
-        }
-      } else {
-        const uint2 x = *(const uint2*)(du + k), y = *(const uint2*)(dv + k);
-        a[k] = x.x;
-        a[k + 1] = x.y;
-        b[k] = y.x;
-        b[k + 1] = y.y;
-      }
+  // this workgroup's share of the arc list in 4-arc quads; two quads per thread in flight
+  const uint32_t E4 = E2 / 4;
+  const uint32_t per = (E4 + gridDim.y - 1) / gridDim.y;
+  const uint32_t q0 = blockIdx.y * per, q1 = min(E4, q0 + per);
+  const uint4* a4 = (const uint4*)auv;
+  const uint4* l4 = (const uint4*)al32;
+  for (uint32_t q = q0 + threadIdx.x; q < q1; q += 2 * blockDim.x) {
+    const uint32_t q2 = q + blockDim.x;
+    const bool two = q2 < q1;
+    const uint4 a = a4[q], l = l4[q];
+    uint4 b = make_uint4(0, 0, 0, 0), m = make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF);
+    if (two) {
+      b = a4[q2];
+      m = l4[q2];
     }
-#pragma unroll
-    for (int k = 0; k < S; k++) {
-      if (a[k] == SQ_INF || (uint64_t)a[k] + l != (uint64_t)b[k]) continue;
-      const uint32_t src = g0 + k;
-      const uint32_t pos = atomicAdd(&tcnt[src], 1u);
-      if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
-    }
+    sweep_arc<S>(row, g0, a.x, l.x, 4 * q, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.y, l.y, 4 * q + 1, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.z, l.z, 4 * q + 2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.w, l.w, 4 * q + 3, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.x, m.x, 4 * q2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.y, m.y, 4 * q2 + 1, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.z, m.z, 4 * q2 + 2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.w, m.w, 4 * q2 + 3, capg, tcnt, tlist);
   }
+  if (blockIdx.y == gridDim.y - 1)
+    for (uint32_t e = 4 * E4 + threadIdx.x; e < E2; e += blockDim.x)
+      sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist);
 }
 
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
@@ -760,11 +769,10 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     bool multi = fast && !getenv("SGN_APSP_LOSS1") && E2 >= 32ull * Vp && lds_fold <= 160 * 1024;
     // sources per workgroup: the largest whose rows fit the LDS a workgroup may have
     int kS = 0;
-    for (int k : {16, 8, 4, 2}) {
+    for (int k : {8, 4}) {
       const size_t b = (size_t)Vp * k * 4;
       if (!multi || b > 160 * 1024) continue;
-      const void* f = k == 16 ? (const void*)loss_sweep<16> : k == 8 ? (const void*)loss_sweep<8>
-                    : k == 4 ? (const void*)loss_sweep<4> : (const void*)loss_sweep<2>;
+      const void* f = k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>;
       if (b <= 64 * 1024 || hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
         kS = k;
         break;
@@ -786,17 +794,11 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
       const uint32_t* d32 = (const uint32_t*)dD32.p;
       const uint32_t* a32 = (const uint32_t*)dal32.p;
-      if (kS == 16)
-        hipLaunchKernelGGL(loss_sweep<16>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
-      else if (kS == 8)
+      if (kS == 8)
         hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
                            (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
-      else if (kS == 4)
-        hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       else
-        hipLaunchKernelGGL(loss_sweep<2>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+        hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
                            (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
                          (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
