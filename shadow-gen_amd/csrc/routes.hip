@@ -347,11 +347,94 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
       sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist);
 }
 
+// Dense form of the arc list (complete-ish graphs): A[u][v] = the least latency of an arc
+// u -> v (u32, SQ_INF: none or >= 2^32 - 1 ns), then P[u][v] = the least loss among the arcs
+// of that latency (only those can be tight; the fold is isotone in the arc's loss, so the
+// least one gives every tight label its minimum).
+__global__ void arc_lat(uint32_t* A, uint32_t Vp, const uint32_t* auv, const uint64_t* al, uint32_t E2) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
+    const uint32_t uv = auv[e];
+    const uint32_t l = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
+    atomicMin(&A[(uint64_t)(uv & 0xFFFFu) * Vp + (uv >> 16)], l);
+  }
+}
+__global__ void arc_loss(const uint32_t* A, uint32_t* P, uint32_t Vp, const uint32_t* auv, const uint64_t* al,
+                         const float* ap, uint32_t E2) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
+    const uint32_t uv = auv[e];
+    const uint64_t x = (uint64_t)(uv & 0xFFFFu) * Vp + (uv >> 16);
+    const uint32_t l = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
+    if (l == A[x]) atomicMin(&P[x], __float_as_uint(ap[e]));  // losses >= 0: bit order = order
+  }
+}
+
+// Tight pairs, dense form: every (u, v) with d[s][u] + A[u][v] == d[s][v] for the used
+// sources s — the equality test of one min-plus product, tiled like sq_pass (64 sources x 64
+// nodes per workgroup, 4 x 4 per thread, K through LDS), so each LDS value serves 4 tests
+// instead of the arc sweep's 2 reads per test. Pairs go to the source's list as u | v << 16.
+__global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
+                                                  const uint32_t* usrc, uint32_t U, uint32_t capg,
+                                                  uint32_t* tcnt, uint32_t* tlist) {
+  __shared__ __attribute__((aligned(16))) uint32_t As[SQ_K][SQ_T + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t Bs[SQ_K][SQ_T + 4];
+  __shared__ uint32_t srow[SQ_T];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const uint32_t si0 = blockIdx.y * SQ_T, c0 = blockIdx.x * SQ_T;
+  if (threadIdx.x < SQ_T) srow[threadIdx.x] = si0 + threadIdx.x < U ? usrc[si0 + threadIdx.x] : 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t dsv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t r = srow[ty * 4 + i];
+    const uint4 v = r == 0xFFFFFFFFu ? make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF)
+                                     : *(const uint4*)&D[(uint64_t)r * Vp + c0 + tx * 4];
+    dsv[i][0] = v.x;
+    dsv[i][1] = v.y;
+    dsv[i][2] = v.z;
+    dsv[i][3] = v.w;
+  }
+  for (uint32_t k0 = 0; k0 < Vp; k0 += SQ_K) {
+    for (int e = threadIdx.x; e < SQ_T * SQ_K / 4; e += 256) {
+      const int m = e >> 3, kq = (e & 7) * 4;
+      const uint32_t r = srow[m];
+      const uint4 a = r == 0xFFFFFFFFu ? make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF)
+                                       : *(const uint4*)&D[(uint64_t)r * Vp + k0 + kq];
+      As[kq][m] = a.x;
+      As[kq + 1][m] = a.y;
+      As[kq + 2][m] = a.z;
+      As[kq + 3][m] = a.w;
+      const int kb = e >> 4, nq = (e & 15) * 4;
+      *(uint4*)&Bs[kb][nq] = *(const uint4*)&A[(uint64_t)(k0 + kb) * Vp + c0 + nq];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < SQ_K; k++) {
+      const uint4 a = *(const uint4*)&As[k][ty * 4];
+      const uint4 b = *(const uint4*)&Bs[k][tx * 4];
+      const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          // saturating: INF operands and overflows give SQ_INF, which no reachable d equals
+          if (__builtin_elementwise_add_sat(av[i], bv[j]) == dsv[i][j] && dsv[i][j] != SQ_INF) {
+            const uint32_t si = si0 + ty * 4 + i;
+            const uint32_t pos = atomicAdd(&tcnt[si], 1u);
+            if (pos < capg) tlist[(uint64_t)si * capg + pos] = (k0 + k) | ((c0 + tx * 4 + j) << 16);
+          }
+        }
+    }
+    __syncthreads();
+  }
+}
+
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
 // then the fixed point as in loss_pass. (tcnt > capg: the caller reruns loss_pass instead.)
+// (P != null: the lists hold packed pairs u | v << 16 and the loss is P[u][v]; else arc indices)
 __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
-                                                 const float* ap, const uint32_t* tcnt, const uint32_t* tlist,
-                                                 uint32_t capg, uint32_t cap, float* Lout, uint32_t* iters) {
+                                                 const float* ap, const float* P, const uint32_t* tcnt,
+                                                 const uint32_t* tlist, uint32_t capg, uint32_t cap, float* Lout,
+                                                 uint32_t* iters) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* L = (float*)smem;
   uint32_t* tuv = (uint32_t*)(L + Vp);
@@ -364,8 +447,8 @@ __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* us
   if (in_lds)
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
       const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
-      tuv[i] = auv[e];
-      tp[i] = ap[e];
+      tuv[i] = P ? e : auv[e];
+      tp[i] = P ? P[(uint64_t)(e & 0xFFFFu) * Vp + (e >> 16)] : ap[e];
     }
   __syncthreads();
   if (threadIdx.x == 0) L[s] = 0.0f;
@@ -382,8 +465,8 @@ __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* us
         pe = tp[i];
       } else {
         const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
-        uv = auv[e];
-        pe = ap[e];
+        uv = P ? e : auv[e];
+        pe = P ? P[(uint64_t)(e & 0xFFFFu) * Vp + (e >> 16)] : ap[e];
       }
       const float lu = L[uv & 0xFFFFu];
       if (lu > 1.0f) continue;
@@ -730,6 +813,45 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipMalloc(&dD32.p, (size_t)Vp * Vp * 4));
       SGN_HIP(ctx, hipMalloc(&dflag.p, max_pass * 4));
     }
+    // the loss phase's form and buffers (allocated here, outside the timed build)
+    const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
+    const size_t lds_fold = (size_t)Vp * 4 + (size_t)cap * 8 + 16;
+    int lform = 0;  // 0 one-source kernel, 1 multi-source arc sweep, 2 dense tiled pass
+    if (fast && !getenv("SGN_APSP_LOSS1") && lds_fold <= 160 * 1024) {
+      if (E2 >= (uint64_t)Vp * Vp / 8 && !getenv("SGN_APSP_SWEEP"))
+        lform = 2;
+      else if (E2 >= 32ull * Vp)
+        lform = 1;
+    }
+    int kS = 0;  // sources per sweep workgroup: the largest whose rows fit its LDS
+    if (lform == 1) {
+      for (int k : {8, 4}) {
+        const size_t b = (size_t)Vp * k * 4;
+        if (b > 160 * 1024) continue;
+        const void* f = k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>;
+        if (b <= 64 * 1024 ||
+            hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
+          kS = k;
+          break;
+        }
+        (void)hipGetLastError();
+      }
+      if (!kS) lform = 0;
+    }
+    const size_t lds_sw = (size_t)Vp * kS * 4;
+    DevBuf dtc, dtl, dal32, dA, dP;
+    if (lform) {
+      SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
+      SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
+    }
+    if (lform == 1) {
+      std::vector<uint32_t> al32(E2);
+      for (uint32_t e = 0; e < E2; e++) al32[e] = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
+      if ((rc = upload(ctx, dal32, al32.data(), E2))) return rc;
+    } else if (lform == 2) {
+      SGN_HIP(ctx, hipMalloc(&dA.p, (size_t)Vp * Vp * 4));
+      SGN_HIP(ctx, hipMalloc(&dP.p, (size_t)Vp * Vp * 4));
+    }
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
     if (fast) {
@@ -761,63 +883,57 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipEventRecord(e1, st));
-    // loss phase. u32 form: multi-source tight sweep + per-source fold (each arc load serves
-    // kS sources); u64 form, a tight-list overflow, or SGN_APSP_LOSS1: the one-source kernel
-    const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
-    const size_t lds_fold = (size_t)Vp * 4 + (size_t)cap * 8 + 16;
-    // dense graphs only: a sparse arc list is re-read from L2 cheaply source by source
-    bool multi = fast && !getenv("SGN_APSP_LOSS1") && E2 >= 32ull * Vp && lds_fold <= 160 * 1024;
-    // sources per workgroup: the largest whose rows fit the LDS a workgroup may have
-    int kS = 0;
-    for (int k : {8, 4}) {
-      const size_t b = (size_t)Vp * k * 4;
-      if (!multi || b > 160 * 1024) continue;
-      const void* f = k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>;
-      if (b <= 64 * 1024 || hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
-        kS = k;
-        break;
-      }
-      (void)hipGetLastError();
-    }
-    if (!kS) multi = false;
-    const size_t lds_sw = (size_t)Vp * kS * 4;
-    DevBuf dtc, dtl, dal32;
-    if (multi) {
-      std::vector<uint32_t> al32(E2);
-      for (uint32_t e = 0; e < E2; e++) al32[e] = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
-      if ((rc = upload(ctx, dal32, al32.data(), E2))) return rc;
-      SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
-      SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
+    // loss phase (u32 form): tight pairs per used source — dense graphs by the tiled equality
+    // pass over the arc matrix, mid-density graphs by a sweep of the arc list serving kS
+    // sources per arc load — then a per-source fold in LDS. Sparse graphs, the u64 form, a
+    // list overflow, or SGN_APSP_LOSS1 take the one-source kernel.
+    int form = lform;
+    if (form) {
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
-      const uint32_t groups = (U + kS - 1) / kS;
-      const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
-      const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
-      const uint32_t* d32 = (const uint32_t*)dD32.p;
-      const uint32_t* a32 = (const uint32_t*)dal32.p;
-      if (kS == 8)
-        hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
-      else
-        hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                           (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+      const float* P = nullptr;
+      if (form == 2) {
+        SGN_HIP(ctx, hipMemsetAsync(dA.p, 0xFF, (size_t)Vp * Vp * 4, st));
+        SGN_HIP(ctx, hipMemsetAsync(dP.p, 0xFF, (size_t)Vp * Vp * 4, st));
+        const dim3 g1(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256)));
+        hipLaunchKernelGGL(arc_lat, g1, dim3(256), 0, st, (uint32_t*)dA.p, Vp, (const uint32_t*)dauv.p,
+                           (const uint64_t*)dal.p, E2);
+        hipLaunchKernelGGL(arc_loss, g1, dim3(256), 0, st, (const uint32_t*)dA.p, (uint32_t*)dP.p, Vp,
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2);
+        hipLaunchKernelGGL(tight_pass, dim3(nb, (U + SQ_T - 1) / SQ_T), dim3(256), 0, st, (const uint32_t*)dD32.p,
+                           (const uint32_t*)dA.p, Vp, (const uint32_t*)dus.p, U, capg, (uint32_t*)dtc.p,
+                           (uint32_t*)dtl.p);
+        P = (const float*)dP.p;
+      } else {
+        const uint32_t groups = (U + kS - 1) / kS;
+        const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
+        const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
+        const uint32_t* d32 = (const uint32_t*)dD32.p;
+        const uint32_t* a32 = (const uint32_t*)dal32.p;
+        if (kS == 8)
+          hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                             (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+        else
+          hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
+                             (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+      }
       hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
-                         (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
+                         (const uint32_t*)dauv.p, (const float*)dap.p, P, (const uint32_t*)dtc.p,
                          (const uint32_t*)dtl.p, capg, cap, (float*)dL.p, (uint32_t*)dit.p);
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
-      // a source with more tight arcs than its global list: redo the phase the one-source way
+      // a source with more tight pairs than its list holds: redo the phase the one-source way
       std::vector<uint32_t> tc(U);
       SGN_HIP(ctx, hipMemcpyAsync(tc.data(), dtc.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
       SGN_HIP(ctx, hipStreamSynchronize(st));
       for (uint32_t x : tc)
-        if (x > capg) multi = false;
-      tm.loss_multi = multi ? (uint32_t)kS : 0u;
+        if (x > capg) form = 0;
     }
-    if (!multi) {
+    tm.loss_multi = form == 1 ? (uint32_t)kS : 0u;
+    tm.loss_dense = form == 2 ? 1u : 0u;
+    if (!form) {
       hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
                          (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
                          (float*)dL.p, (uint32_t*)dit.p);
-      tm.loss_multi = 0;
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
     }
@@ -859,6 +975,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       // a used pair without a finite u32 path: disconnected, or a path of 2^32 - 1 ns or more;
       // the u64 Floyd-Warshall decides
       fast = false;
+      lform = 0;  // the tight forms read the u32 matrix
       SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
       goto latency_phase;
     }
