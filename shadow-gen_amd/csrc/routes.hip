@@ -370,11 +370,14 @@ __global__ void arc_loss(const uint32_t* A, uint32_t* P, uint32_t Vp, const uint
 
 // Tight pairs, dense form: every (u, v) with d[s][u] + A[u][v] == d[s][v] for the used
 // sources s — the equality test of one min-plus product, tiled like sq_pass (64 sources x 64
-// nodes per workgroup, 4 x 4 per thread, K through LDS), so each LDS value serves 4 tests
-// instead of the arc sweep's 2 reads per test. Pairs go to the source's list as u | v << 16.
+// nodes per workgroup, 4 x 4 per thread, K through LDS; each LDS value serves 4 tests). The
+// K loop only counts hits and keeps the last u per (s, v) — no memory traffic, no branch —
+// and the pairs are emitted after it; an (s, v) with several tight u (ties) goes to the tie
+// list, whose u are found by tie_pass. Pairs go to the source's list as u | v << 16.
 __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
                                                   const uint32_t* usrc, uint32_t U, uint32_t capg,
-                                                  uint32_t* tcnt, uint32_t* tlist) {
+                                                  uint32_t* tcnt, uint32_t* tlist, uint32_t* ties,
+                                                  uint32_t tie_cap) {
   __shared__ __attribute__((aligned(16))) uint32_t As[SQ_K][SQ_T + 4];
   __shared__ __attribute__((aligned(16))) uint32_t Bs[SQ_K][SQ_T + 4];
   __shared__ uint32_t srow[SQ_T];
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
   const uint32_t si0 = blockIdx.y * SQ_T, c0 = blockIdx.x * SQ_T;
   if (threadIdx.x < SQ_T) srow[threadIdx.x] = si0 + threadIdx.x < U ? usrc[si0 + threadIdx.x] : 0xFFFFFFFFu;
   __syncthreads();
-  uint32_t dsv[4][4];
+  uint32_t dsv[4][4], cnt[4][4], last[4][4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t r = srow[ty * 4 + i];
@@ -392,6 +395,11 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
     dsv[i][1] = v.y;
     dsv[i][2] = v.z;
     dsv[i][3] = v.w;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      cnt[i][j] = 0;
+      last[i][j] = 0;
+    }
   }
   for (uint32_t k0 = 0; k0 < Vp; k0 += SQ_K) {
     for (int e = threadIdx.x; e < SQ_T * SQ_K / 4; e += 256) {
@@ -407,24 +415,54 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
       *(uint4*)&Bs[kb][nq] = *(const uint4*)&A[(uint64_t)(k0 + kb) * Vp + c0 + nq];
     }
     __syncthreads();
-#pragma unroll 4
+#pragma unroll 8
     for (int k = 0; k < SQ_K; k++) {
       const uint4 a = *(const uint4*)&As[k][ty * 4];
       const uint4 b = *(const uint4*)&Bs[k][tx * 4];
       const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+      const uint32_t u = k0 + k;
 #pragma unroll
       for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          // saturating: INF operands and overflows give SQ_INF, which no reachable d equals
-          if (__builtin_elementwise_add_sat(av[i], bv[j]) == dsv[i][j] && dsv[i][j] != SQ_INF) {
-            const uint32_t si = si0 + ty * 4 + i;
-            const uint32_t pos = atomicAdd(&tcnt[si], 1u);
-            if (pos < capg) tlist[(uint64_t)si * capg + pos] = (k0 + k) | ((c0 + tx * 4 + j) << 16);
-          }
+          // saturating: INF operands and overflows give SQ_INF (unreachable v are skipped below)
+          const bool hit = __builtin_elementwise_add_sat(av[i], bv[j]) == dsv[i][j];
+          cnt[i][j] += hit;
+          last[i][j] = hit ? u : last[i][j];
         }
     }
     __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t si = si0 + ty * 4 + i, v = c0 + tx * 4 + j;
+      if (dsv[i][j] == SQ_INF || cnt[i][j] == 0) continue;
+      if (cnt[i][j] == 1) {
+        const uint32_t pos = atomicAdd(&tcnt[si], 1u);
+        if (pos < capg) tlist[(uint64_t)si * capg + pos] = last[i][j] | (v << 16);
+      } else {
+        const uint32_t t = atomicAdd(&ties[0], 1u);
+        if (t < tie_cap) ties[1 + t] = si | (v << 16);  // U, V <= 13632 < 2^16
+      }
+    }
+}
+
+// The (s, v) with several tight u: one wave each scans u and emits every tight pair.
+__global__ __launch_bounds__(256) void tie_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
+                                                const uint32_t* usrc, uint32_t capg, uint32_t* tcnt,
+                                                uint32_t* tlist, const uint32_t* ties, uint32_t tie_cap) {
+  const uint32_t n = min(ties[0], tie_cap);
+  for (uint32_t x = blockIdx.x * 4 + (threadIdx.x >> 6); x < n; x += gridDim.x * 4) {
+    const uint32_t t = ties[1 + x], si = t & 0xFFFFu, v = t >> 16;
+    const uint32_t* Ds = D + (uint64_t)usrc[si] * Vp;
+    const uint32_t dv = Ds[v];
+    for (uint32_t u = threadIdx.x & 63; u < Vp; u += 64)
+      if (__builtin_elementwise_add_sat(Ds[u], A[(uint64_t)u * Vp + v]) == dv) {
+        const uint32_t pos = atomicAdd(&tcnt[si], 1u);
+        if (pos < capg) tlist[(uint64_t)si * capg + pos] = u | (v << 16);
+      }
   }
 }
 
@@ -839,7 +877,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       if (!kS) lform = 0;
     }
     const size_t lds_sw = (size_t)Vp * kS * 4;
-    DevBuf dtc, dtl, dal32, dA, dP;
+    DevBuf dtc, dtl, dal32, dA, dP, dties;
+    const uint32_t tie_cap = 1u << 20;
     if (lform) {
       SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
       SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
@@ -851,6 +890,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     } else if (lform == 2) {
       SGN_HIP(ctx, hipMalloc(&dA.p, (size_t)Vp * Vp * 4));
       SGN_HIP(ctx, hipMalloc(&dP.p, (size_t)Vp * Vp * 4));
+      SGN_HIP(ctx, hipMalloc(&dties.p, (size_t)(tie_cap + 1) * 4));
     }
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
@@ -899,9 +939,13 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
                            (const uint64_t*)dal.p, E2);
         hipLaunchKernelGGL(arc_loss, g1, dim3(256), 0, st, (const uint32_t*)dA.p, (uint32_t*)dP.p, Vp,
                            (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2);
+        SGN_HIP(ctx, hipMemsetAsync(dties.p, 0, 4, st));
         hipLaunchKernelGGL(tight_pass, dim3(nb, (U + SQ_T - 1) / SQ_T), dim3(256), 0, st, (const uint32_t*)dD32.p,
                            (const uint32_t*)dA.p, Vp, (const uint32_t*)dus.p, U, capg, (uint32_t*)dtc.p,
-                           (uint32_t*)dtl.p);
+                           (uint32_t*)dtl.p, (uint32_t*)dties.p, tie_cap);
+        hipLaunchKernelGGL(tie_pass, dim3(256), dim3(256), 0, st, (const uint32_t*)dD32.p, (const uint32_t*)dA.p,
+                           Vp, (const uint32_t*)dus.p, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p,
+                           (const uint32_t*)dties.p, tie_cap);
         P = (const float*)dP.p;
       } else {
         const uint32_t groups = (U + kS - 1) / kS;
@@ -927,6 +971,11 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipStreamSynchronize(st));
       for (uint32_t x : tc)
         if (x > capg) form = 0;
+      if (form == 2) {
+        uint32_t nties = 0;
+        SGN_HIP(ctx, hipMemcpy(&nties, dties.p, 4, hipMemcpyDeviceToHost));
+        if (nties > tie_cap) form = 0;
+      }
     }
     tm.loss_multi = form == 1 ? (uint32_t)kS : 0u;
     tm.loss_dense = form == 2 ? 1u : 0u;
