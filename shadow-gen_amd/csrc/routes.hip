@@ -371,8 +371,8 @@ __global__ void arc_loss(const uint32_t* A, uint32_t* P, uint32_t Vp, const uint
 // Tight pairs, dense form: every (u, v) with d[s][u] + A[u][v] == d[s][v] for the used
 // sources s — the equality test of one min-plus product, tiled like sq_pass (64 sources x 64
 // nodes per workgroup, 4 x 4 per thread, K through LDS; each LDS value serves 4 tests). The
-// K loop only counts hits and keeps the last u per (s, v) — no memory traffic, no branch —
-// and the pairs are emitted after it; an (s, v) with several tight u (ties) goes to the tie
+// K loop only counts hits and keeps the least tight u per (s, v) — no memory traffic, no
+// branch — and the pairs are emitted after it; an (s, v) with several tight u (ties) goes to the tie
 // list, whose u are found by tie_pass. Pairs go to the source's list as u | v << 16.
 __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
                                                   const uint32_t* usrc, uint32_t U, uint32_t capg,
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
   const uint32_t si0 = blockIdx.y * SQ_T, c0 = blockIdx.x * SQ_T;
   if (threadIdx.x < SQ_T) srow[threadIdx.x] = si0 + threadIdx.x < U ? usrc[si0 + threadIdx.x] : 0xFFFFFFFFu;
   __syncthreads();
-  uint32_t dsv[4][4], cnt[4][4], last[4][4];
+  uint32_t dsv[4][4], cnt[4][4], key[4][4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint32_t r = srow[ty * 4 + i];
@@ -397,8 +397,8 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
     dsv[i][3] = v.w;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      cnt[i][j] = 0;
-      last[i][j] = 0;
+      cnt[i][j] = 0;          // non-tight u seen
+      key[i][j] = 0xFFFFFFFFu; // min of (not tight) << 16 | u: the least tight u, if any
     }
   }
   for (uint32_t k0 = 0; k0 < Vp; k0 += SQ_K) {
@@ -425,10 +425,12 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
       for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          // saturating: INF operands and overflows give SQ_INF (unreachable v are skipped below)
-          const bool hit = __builtin_elementwise_add_sat(av[i], bv[j]) == dsv[i][j];
-          cnt[i][j] += hit;
-          last[i][j] = hit ? u : last[i][j];
+          // d[s][u] + A[u][v] >= d[s][v] at the fixed point (saturating: INF operands and
+          // overflows give SQ_INF), so z = min(sum - d[s][v], 1) is 0 exactly when tight:
+          // plain VALU arithmetic, no compare masks
+          const uint32_t z = min(__builtin_elementwise_add_sat(av[i], bv[j]) - dsv[i][j], 1u);
+          cnt[i][j] += z;
+          key[i][j] = min(key[i][j], (z << 16) | u);
         }
     }
     __syncthreads();
@@ -438,10 +440,11 @@ __global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint3
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const uint32_t si = si0 + ty * 4 + i, v = c0 + tx * 4 + j;
-      if (dsv[i][j] == SQ_INF || cnt[i][j] == 0) continue;
-      if (cnt[i][j] == 1) {
+      const uint32_t tight = Vp - cnt[i][j];
+      if (dsv[i][j] == SQ_INF || tight == 0) continue;
+      if (tight == 1) {
         const uint32_t pos = atomicAdd(&tcnt[si], 1u);
-        if (pos < capg) tlist[(uint64_t)si * capg + pos] = last[i][j] | (v << 16);
+        if (pos < capg) tlist[(uint64_t)si * capg + pos] = (key[i][j] & 0xFFFFu) | (v << 16);
       } else {
         const uint32_t t = atomicAdd(&ties[0], 1u);
         if (t < tie_cap) ties[1 + t] = si | (v << 16);  // U, V <= 13632 < 2^16
