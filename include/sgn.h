@@ -117,9 +117,9 @@ typedef struct sgn_routes_timing {
   uint64_t n_tight_edges;
   uint32_t latency_passes; /* min-plus squaring passes (u32 form), or k-blocks (u64 Floyd-Warshall) */
   uint32_t latency_u64;    /* 1: the u64 Floyd-Warshall form ran (an edge or path >= 2^32 - 1 ns) */
-  uint32_t loss_multi;     /* sources per tight-arc sweep (u32 form, mid-density graphs), else 0 */
-  uint32_t loss_dense;     /* 1: tight pairs by the tiled pass over the arc matrix (dense graphs);
-                              both 0: the one-source loss pass */
+  uint32_t loss_multi;     /* sources per tight-arc sweep (u32 form, non-sparse graphs); 0: the
+                              one-source loss pass */
+  uint32_t reserved;
 } sgn_routes_timing;
 int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
 

@@ -284,19 +284,33 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
 // two 4S-byte reads; arcs are 8 bytes: u | v << 16 and the u32 latency) and sweeps one P-th of the arc list; each arc load now serves S sources
 // instead of one (the single-source sweep re-read the whole arc list once per source, from
 // L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
+// One arc's S tests; du (the S distances to the arc's tail u) stays in registers while the
+// thread's consecutive arcs share u (the arc list is sorted by u).
 template <int S>
 __device__ __forceinline__ void sweep_arc(const uint32_t* row, uint32_t g0, uint32_t uv, uint32_t l, uint32_t e,
-                                          uint32_t capg, uint32_t* tcnt, uint32_t* tlist) {
+                                          uint32_t capg, uint32_t* tcnt, uint32_t* tlist, uint32_t& cu,
+                                          uint32_t (&du)[S]) {
   if (l == SQ_INF) return;  // 2^32 - 1 ns or more: no u32 path is that long, never tight
-  const uint32_t* du = row + (uv & 0xFFFFu) * S;
+  const uint32_t u = uv & 0xFFFFu;
+  if (u != cu) {
+    cu = u;
+#pragma unroll
+    for (int k = 0; k < S; k += 4) {
+      const uint4 x = *(const uint4*)(row + u * S + k);
+      du[k] = x.x;
+      du[k + 1] = x.y;
+      du[k + 2] = x.z;
+      du[k + 3] = x.w;
+    }
+  }
   const uint32_t* dv = row + (uv >> 16) * S;
 #pragma unroll
   for (int k = 0; k < S; k += 4) {
-    const uint4 x = *(const uint4*)(du + k), y = *(const uint4*)(dv + k);
-    const uint32_t a[4] = {x.x, x.y, x.z, x.w}, b[4] = {y.x, y.y, y.z, y.w};
+    const uint4 y = *(const uint4*)(dv + k);
+    const uint32_t b[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (a[j] == SQ_INF || (uint64_t)a[j] + l != (uint64_t)b[j]) continue;
+      if (du[k + j] == SQ_INF || (uint64_t)du[k + j] + l != (uint64_t)b[j]) continue;
       const uint32_t src = g0 + k + j;
       const uint32_t pos = atomicAdd(&tcnt[src], 1u);
       if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
@@ -318,164 +332,37 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
     row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
   }
   __syncthreads();
-  // this workgroup's share of the arc list in 4-arc quads; two quads per thread in flight
-  const uint32_t E4 = E2 / 4;
-  const uint32_t per = (E4 + gridDim.y - 1) / gridDim.y;
-  const uint32_t q0 = blockIdx.y * per, q1 = min(E4, q0 + per);
+  // this workgroup's share of the arc list in runs of 8 consecutive arcs per thread (two
+  // 16-byte loads of each array in flight; consecutive arcs mostly share their tail u)
+  const uint32_t E8 = E2 / 8;
+  const uint32_t per = (E8 + gridDim.y - 1) / gridDim.y;
+  const uint32_t q0 = blockIdx.y * per, q1 = min(E8, q0 + per);
   const uint4* a4 = (const uint4*)auv;
   const uint4* l4 = (const uint4*)al32;
-  for (uint32_t q = q0 + threadIdx.x; q < q1; q += 2 * blockDim.x) {
-    const uint32_t q2 = q + blockDim.x;
-    const bool two = q2 < q1;
-    const uint4 a = a4[q], l = l4[q];
-    uint4 b = make_uint4(0, 0, 0, 0), m = make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF);
-    if (two) {
-      b = a4[q2];
-      m = l4[q2];
-    }
-    sweep_arc<S>(row, g0, a.x, l.x, 4 * q, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, a.y, l.y, 4 * q + 1, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, a.z, l.z, 4 * q + 2, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, a.w, l.w, 4 * q + 3, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, b.x, m.x, 4 * q2, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, b.y, m.y, 4 * q2 + 1, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, b.z, m.z, 4 * q2 + 2, capg, tcnt, tlist);
-    sweep_arc<S>(row, g0, b.w, m.w, 4 * q2 + 3, capg, tcnt, tlist);
+  uint32_t cu = 0xFFFFFFFFu;
+  uint32_t du[S];
+  for (uint32_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const uint4 a = a4[2 * q], b = a4[2 * q + 1], l = l4[2 * q], m = l4[2 * q + 1];
+    const uint32_t e = 8 * q;
+    sweep_arc<S>(row, g0, a.x, l.x, e, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, a.y, l.y, e + 1, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, a.z, l.z, e + 2, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, a.w, l.w, e + 3, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, b.x, m.x, e + 4, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, b.y, m.y, e + 5, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, b.z, m.z, e + 6, capg, tcnt, tlist, cu, du);
+    sweep_arc<S>(row, g0, b.w, m.w, e + 7, capg, tcnt, tlist, cu, du);
   }
   if (blockIdx.y == gridDim.y - 1)
-    for (uint32_t e = 4 * E4 + threadIdx.x; e < E2; e += blockDim.x)
-      sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist);
-}
-
-// Dense form of the arc list (complete-ish graphs): A[u][v] = the least latency of an arc
-// u -> v (u32, SQ_INF: none or >= 2^32 - 1 ns), then P[u][v] = the least loss among the arcs
-// of that latency (only those can be tight; the fold is isotone in the arc's loss, so the
-// least one gives every tight label its minimum).
-__global__ void arc_lat(uint32_t* A, uint32_t Vp, const uint32_t* auv, const uint64_t* al, uint32_t E2) {
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
-    const uint32_t uv = auv[e];
-    const uint32_t l = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
-    atomicMin(&A[(uint64_t)(uv & 0xFFFFu) * Vp + (uv >> 16)], l);
-  }
-}
-__global__ void arc_loss(const uint32_t* A, uint32_t* P, uint32_t Vp, const uint32_t* auv, const uint64_t* al,
-                         const float* ap, uint32_t E2) {
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
-    const uint32_t uv = auv[e];
-    const uint64_t x = (uint64_t)(uv & 0xFFFFu) * Vp + (uv >> 16);
-    const uint32_t l = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
-    if (l == A[x]) atomicMin(&P[x], __float_as_uint(ap[e]));  // losses >= 0: bit order = order
-  }
-}
-
-// Tight pairs, dense form: every (u, v) with d[s][u] + A[u][v] == d[s][v] for the used
-// sources s — the equality test of one min-plus product, tiled like sq_pass (64 sources x 64
-// nodes per workgroup, 4 x 4 per thread, K through LDS; each LDS value serves 4 tests). The
-// K loop only counts hits and keeps the least tight u per (s, v) — no memory traffic, no
-// branch — and the pairs are emitted after it; an (s, v) with several tight u (ties) goes to the tie
-// list, whose u are found by tie_pass. Pairs go to the source's list as u | v << 16.
-__global__ __launch_bounds__(256) void tight_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
-                                                  const uint32_t* usrc, uint32_t U, uint32_t capg,
-                                                  uint32_t* tcnt, uint32_t* tlist, uint32_t* ties,
-                                                  uint32_t tie_cap) {
-  __shared__ __attribute__((aligned(16))) uint32_t As[SQ_K][SQ_T + 4];
-  __shared__ __attribute__((aligned(16))) uint32_t Bs[SQ_K][SQ_T + 4];
-  __shared__ uint32_t srow[SQ_T];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const uint32_t si0 = blockIdx.y * SQ_T, c0 = blockIdx.x * SQ_T;
-  if (threadIdx.x < SQ_T) srow[threadIdx.x] = si0 + threadIdx.x < U ? usrc[si0 + threadIdx.x] : 0xFFFFFFFFu;
-  __syncthreads();
-  uint32_t dsv[4][4], cnt[4][4], key[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t r = srow[ty * 4 + i];
-    const uint4 v = r == 0xFFFFFFFFu ? make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF)
-                                     : *(const uint4*)&D[(uint64_t)r * Vp + c0 + tx * 4];
-    dsv[i][0] = v.x;
-    dsv[i][1] = v.y;
-    dsv[i][2] = v.z;
-    dsv[i][3] = v.w;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      cnt[i][j] = 0;          // non-tight u seen
-      key[i][j] = 0xFFFFFFFFu; // min of (not tight) << 16 | u: the least tight u, if any
-    }
-  }
-  for (uint32_t k0 = 0; k0 < Vp; k0 += SQ_K) {
-    for (int e = threadIdx.x; e < SQ_T * SQ_K / 4; e += 256) {
-      const int m = e >> 3, kq = (e & 7) * 4;
-      const uint32_t r = srow[m];
-      const uint4 a = r == 0xFFFFFFFFu ? make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF)
-                                       : *(const uint4*)&D[(uint64_t)r * Vp + k0 + kq];
-      As[kq][m] = a.x;
-      As[kq + 1][m] = a.y;
-      As[kq + 2][m] = a.z;
-      As[kq + 3][m] = a.w;
-      const int kb = e >> 4, nq = (e & 15) * 4;
-      *(uint4*)&Bs[kb][nq] = *(const uint4*)&A[(uint64_t)(k0 + kb) * Vp + c0 + nq];
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int k = 0; k < SQ_K; k++) {
-      const uint4 a = *(const uint4*)&As[k][ty * 4];
-      const uint4 b = *(const uint4*)&Bs[k][tx * 4];
-      const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-      const uint32_t u = k0 + k;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          // d[s][u] + A[u][v] >= d[s][v] at the fixed point (saturating: INF operands and
-          // overflows give SQ_INF), so z = min(sum - d[s][v], 1) is 0 exactly when tight:
-          // plain VALU arithmetic, no compare masks
-          const uint32_t z = min(__builtin_elementwise_add_sat(av[i], bv[j]) - dsv[i][j], 1u);
-          cnt[i][j] += z;
-          key[i][j] = min(key[i][j], (z << 16) | u);
-        }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t si = si0 + ty * 4 + i, v = c0 + tx * 4 + j;
-      const uint32_t tight = Vp - cnt[i][j];
-      if (dsv[i][j] == SQ_INF || tight == 0) continue;
-      if (tight == 1) {
-        const uint32_t pos = atomicAdd(&tcnt[si], 1u);
-        if (pos < capg) tlist[(uint64_t)si * capg + pos] = (key[i][j] & 0xFFFFu) | (v << 16);
-      } else {
-        const uint32_t t = atomicAdd(&ties[0], 1u);
-        if (t < tie_cap) ties[1 + t] = si | (v << 16);  // U, V <= 13632 < 2^16
-      }
-    }
-}
-
-// The (s, v) with several tight u: one wave each scans u and emits every tight pair.
-__global__ __launch_bounds__(256) void tie_pass(const uint32_t* D, const uint32_t* A, uint32_t Vp,
-                                                const uint32_t* usrc, uint32_t capg, uint32_t* tcnt,
-                                                uint32_t* tlist, const uint32_t* ties, uint32_t tie_cap) {
-  const uint32_t n = min(ties[0], tie_cap);
-  for (uint32_t x = blockIdx.x * 4 + (threadIdx.x >> 6); x < n; x += gridDim.x * 4) {
-    const uint32_t t = ties[1 + x], si = t & 0xFFFFu, v = t >> 16;
-    const uint32_t* Ds = D + (uint64_t)usrc[si] * Vp;
-    const uint32_t dv = Ds[v];
-    for (uint32_t u = threadIdx.x & 63; u < Vp; u += 64)
-      if (__builtin_elementwise_add_sat(Ds[u], A[(uint64_t)u * Vp + v]) == dv) {
-        const uint32_t pos = atomicAdd(&tcnt[si], 1u);
-        if (pos < capg) tlist[(uint64_t)si * capg + pos] = u | (v << 16);
-      }
-  }
+    for (uint32_t e = 8 * E8 + threadIdx.x; e < E2; e += blockDim.x)
+      sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist, cu, du);
 }
 
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
 // then the fixed point as in loss_pass. (tcnt > capg: the caller reruns loss_pass instead.)
-// (P != null: the lists hold packed pairs u | v << 16 and the loss is P[u][v]; else arc indices)
 __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
-                                                 const float* ap, const float* P, const uint32_t* tcnt,
-                                                 const uint32_t* tlist, uint32_t capg, uint32_t cap, float* Lout,
-                                                 uint32_t* iters) {
+                                                 const float* ap, const uint32_t* tcnt, const uint32_t* tlist,
+                                                 uint32_t capg, uint32_t cap, float* Lout, uint32_t* iters) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* L = (float*)smem;
   uint32_t* tuv = (uint32_t*)(L + Vp);
@@ -488,8 +375,8 @@ __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* us
   if (in_lds)
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
       const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
-      tuv[i] = P ? e : auv[e];
-      tp[i] = P ? P[(uint64_t)(e & 0xFFFFu) * Vp + (e >> 16)] : ap[e];
+      tuv[i] = auv[e];
+      tp[i] = ap[e];
     }
   __syncthreads();
   if (threadIdx.x == 0) L[s] = 0.0f;
@@ -506,8 +393,8 @@ __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* us
         pe = tp[i];
       } else {
         const uint32_t e = tlist[(uint64_t)blockIdx.x * capg + i];
-        uv = P ? e : auv[e];
-        pe = P ? P[(uint64_t)(e & 0xFFFFu) * Vp + (e >> 16)] : ap[e];
+        uv = auv[e];
+        pe = ap[e];
       }
       const float lu = L[uv & 0xFFFFu];
       if (lu > 1.0f) continue;
@@ -807,6 +694,26 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         auv.push_back(ed[k] | (es[k] << 16)); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
       }
     }
+    // arcs ordered by their tail u (counting sort; the order is otherwise immaterial: each arc
+    // is tested on its own and the fold's fixed point does not depend on order), so a sweep
+    // thread's consecutive arcs share u
+    {
+      std::vector<uint32_t> start(V + 1, 0);
+      for (uint32_t x : auv) start[(x & 0xFFFFu) + 1]++;
+      for (uint32_t i = 0; i < V; i++) start[i + 1] += start[i];
+      std::vector<uint32_t> a2(auv.size());
+      std::vector<uint64_t> l2(auv.size());
+      std::vector<float> p2(auv.size());
+      for (size_t e = 0; e < auv.size(); e++) {
+        const uint32_t k = start[auv[e] & 0xFFFFu]++;
+        a2[k] = auv[e];
+        l2[k] = al[e];
+        p2[k] = ap[e];
+      }
+      auv.swap(a2);
+      al.swap(l2);
+      ap.swap(p2);
+    }
     const uint32_t E2 = (uint32_t)auv.size();
     std::vector<uint64_t> sl(U);
     std::vector<float> sp(U);
@@ -857,13 +764,9 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     // the loss phase's form and buffers (allocated here, outside the timed build)
     const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
     const size_t lds_fold = (size_t)Vp * 4 + (size_t)cap * 8 + 16;
-    int lform = 0;  // 0 one-source kernel, 1 multi-source arc sweep, 2 dense tiled pass
-    if (fast && !getenv("SGN_APSP_LOSS1") && lds_fold <= 160 * 1024) {
-      if (E2 >= (uint64_t)Vp * Vp / 8 && !getenv("SGN_APSP_SWEEP"))
-        lform = 2;
-      else if (E2 >= 32ull * Vp)
-        lform = 1;
-    }
+    // 0 one-source kernel, 1 multi-source arc sweep (not for sparse graphs: their arc list is
+    // re-read from L2 cheaply source by source)
+    int lform = fast && !getenv("SGN_APSP_LOSS1") && lds_fold <= 160 * 1024 && E2 >= 32ull * Vp ? 1 : 0;
     int kS = 0;  // sources per sweep workgroup: the largest whose rows fit its LDS
     if (lform == 1) {
       for (int k : {8, 4}) {
@@ -880,8 +783,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       if (!kS) lform = 0;
     }
     const size_t lds_sw = (size_t)Vp * kS * 4;
-    DevBuf dtc, dtl, dal32, dA, dP, dties;
-    const uint32_t tie_cap = 1u << 20;
+    DevBuf dtc, dtl, dal32;
     if (lform) {
       SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
       SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
@@ -890,10 +792,6 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       std::vector<uint32_t> al32(E2);
       for (uint32_t e = 0; e < E2; e++) al32[e] = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
       if ((rc = upload(ctx, dal32, al32.data(), E2))) return rc;
-    } else if (lform == 2) {
-      SGN_HIP(ctx, hipMalloc(&dA.p, (size_t)Vp * Vp * 4));
-      SGN_HIP(ctx, hipMalloc(&dP.p, (size_t)Vp * Vp * 4));
-      SGN_HIP(ctx, hipMalloc(&dties.p, (size_t)(tie_cap + 1) * 4));
     }
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
@@ -926,31 +824,13 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipEventRecord(e1, st));
-    // loss phase (u32 form): tight pairs per used source — dense graphs by the tiled equality
-    // pass over the arc matrix, mid-density graphs by a sweep of the arc list serving kS
-    // sources per arc load — then a per-source fold in LDS. Sparse graphs, the u64 form, a
-    // list overflow, or SGN_APSP_LOSS1 take the one-source kernel.
+    // loss phase (u32 form): tight arcs of kS used sources per arc load (dense and mid-density
+    // graphs), then a per-source fold in LDS. Sparse graphs, the u64 form, a list overflow, or
+    // SGN_APSP_LOSS1 take the one-source kernel.
     int form = lform;
     if (form) {
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
-      const float* P = nullptr;
-      if (form == 2) {
-        SGN_HIP(ctx, hipMemsetAsync(dA.p, 0xFF, (size_t)Vp * Vp * 4, st));
-        SGN_HIP(ctx, hipMemsetAsync(dP.p, 0xFF, (size_t)Vp * Vp * 4, st));
-        const dim3 g1(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256)));
-        hipLaunchKernelGGL(arc_lat, g1, dim3(256), 0, st, (uint32_t*)dA.p, Vp, (const uint32_t*)dauv.p,
-                           (const uint64_t*)dal.p, E2);
-        hipLaunchKernelGGL(arc_loss, g1, dim3(256), 0, st, (const uint32_t*)dA.p, (uint32_t*)dP.p, Vp,
-                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2);
-        SGN_HIP(ctx, hipMemsetAsync(dties.p, 0, 4, st));
-        hipLaunchKernelGGL(tight_pass, dim3(nb, (U + SQ_T - 1) / SQ_T), dim3(256), 0, st, (const uint32_t*)dD32.p,
-                           (const uint32_t*)dA.p, Vp, (const uint32_t*)dus.p, U, capg, (uint32_t*)dtc.p,
-                           (uint32_t*)dtl.p, (uint32_t*)dties.p, tie_cap);
-        hipLaunchKernelGGL(tie_pass, dim3(256), dim3(256), 0, st, (const uint32_t*)dD32.p, (const uint32_t*)dA.p,
-                           Vp, (const uint32_t*)dus.p, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p,
-                           (const uint32_t*)dties.p, tie_cap);
-        P = (const float*)dP.p;
-      } else {
+      {
         const uint32_t groups = (U + kS - 1) / kS;
         const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
         const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
@@ -964,7 +844,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
                              (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
       }
       hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
-                         (const uint32_t*)dauv.p, (const float*)dap.p, P, (const uint32_t*)dtc.p,
+                         (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
                          (const uint32_t*)dtl.p, capg, cap, (float*)dL.p, (uint32_t*)dit.p);
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
@@ -974,14 +854,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipStreamSynchronize(st));
       for (uint32_t x : tc)
         if (x > capg) form = 0;
-      if (form == 2) {
-        uint32_t nties = 0;
-        SGN_HIP(ctx, hipMemcpy(&nties, dties.p, 4, hipMemcpyDeviceToHost));
-        if (nties > tie_cap) form = 0;
-      }
     }
-    tm.loss_multi = form == 1 ? (uint32_t)kS : 0u;
-    tm.loss_dense = form == 2 ? 1u : 0u;
+    tm.loss_multi = form ? (uint32_t)kS : 0u;
     if (!form) {
       hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
                          (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,

@@ -99,11 +99,10 @@ def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle):
 
 
 def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
-    """The loss phase's three forms against the oracle and each other: the dense tiled pass
-    (complete graphs), the multi-source arc sweep (SGN_APSP_SWEEP, 96 KB of rows per workgroup
-    at V = 1500), the one-source kernel (SGN_APSP_LOSS1; sparse graphs take it anyway), and a
-    graph whose sources have more tight pairs than a list holds (complete bipartite layers of
-    equal latency: |A| x |B| ties), which falls back to the one-source kernel."""
+    """The loss phase's multi-source arc sweep (complete graphs; 48 KB of rows per workgroup
+    at V = 1500) against the oracle and against the one-source kernel (SGN_APSP_LOSS1; sparse
+    graphs take it anyway), and a graph whose sources have more tight arcs than a list holds
+    (complete bipartite layers of equal latency: |A| x |B| ties), which falls back to it."""
     cases = [sgn.tor_graph(600, seed=3), sgn.tor_graph(1500, seed=4), sgn.random_graph(1500, seed=8, loss_frac=0.5)]
     a, b = 90, 90  # s -> A (1 ms) -> B (1 ms): every A x B arc is tight for s
     src = [0] * a + [1 + i for i in range(a) for _ in range(b)]
@@ -117,24 +116,19 @@ def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
     for k, g in enumerate(cases):
         used = np.arange(len(g.node_id))
         ol, op = oracle.routes(g, used)
-        tables = []
-        for env in ({}, {"SGN_APSP_SWEEP": "1"}, {"SGN_APSP_LOSS1": "1"}):
+        forms = []
+        for env in ({}, {"SGN_APSP_LOSS1": "1"}):
             for key, val in env.items():
                 monkeypatch.setenv(key, val)
             c = ctxf()
             c.routes_build(g, used)
-            t = c.routes_timing()
+            forms.append(c.routes_timing()["loss_multi"])
             for key in env:
                 monkeypatch.delenv(key)
             gl, gp = c.routes_copy()
             assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), (k, env)
-            tables.append((t["loss_dense"], t["loss_multi"]))
-        if k < 2:  # complete: dense by default, the sweep on request, one-source on request
-            assert tables[0][0] == 1 and tables[1][1] >= 4 and tables[2] == (0, 0), tables
-        elif k == 2:  # sparse: one-source always
-            assert all(x == (0, 0) for x in tables), tables
-        else:  # list overflow: one-source
-            assert tables[0] == (0, 0) and tables[1] == (0, 0), tables
+        assert forms[1] == 0
+        assert (forms[0] >= 4) == (k < 2), (k, forms)  # sparse graph / list overflow: one-source
 
 
 def test_apsp_errors(ctxf):

@@ -27,24 +27,20 @@ def run(kind, V):
     return {"graph": kind, "V": V, "arcs": int(t["n_tight_edges"]), "first_build_ms": round(ts[0]["total_ms"], 3),
             **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()},
             "form": "u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring",
-            "loss_form": "dense tiled pass + fold" if t["loss_dense"] else
-                         (f"{t['loss_multi']}-source sweep + fold" if t["loss_multi"] else "one-source pass")}
+            "loss_form": f"{t['loss_multi']}-source sweep + fold" if t["loss_multi"] else "one-source pass"}
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 2:
         print(json.dumps(run(sys.argv[1], int(sys.argv[2]))), flush=True)
         sys.exit(0)
-    for mode in ("default", "sweep", "loss1", "fw"):
+    for mode in ("default", "loss1", "fw"):
         for kind in ("tor", "random"):
             for V in (1000, 2000):
                 env = dict(os.environ)
                 env.pop("SGN_APSP_FW", None)
                 env.pop("SGN_APSP_LOSS1", None)
-                env.pop("SGN_APSP_SWEEP", None)
-                if mode == "sweep":
-                    env["SGN_APSP_SWEEP"] = "1"
-                elif mode == "fw":
+                if mode == "fw":
                     env["SGN_APSP_FW"] = "1"
                 elif mode == "loss1":
                     env["SGN_APSP_LOSS1"] = "1"
