@@ -284,33 +284,19 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
 // two 4S-byte reads; arcs are 8 bytes: u | v << 16 and the u32 latency) and sweeps one P-th of the arc list; each arc load now serves S sources
 // instead of one (the single-source sweep re-read the whole arc list once per source, from
 // L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
-// One arc's S tests; du (the S distances to the arc's tail u) stays in registers while the
-// thread's consecutive arcs share u (the arc list is sorted by u).
 template <int S>
 __device__ __forceinline__ void sweep_arc(const uint32_t* row, uint32_t g0, uint32_t uv, uint32_t l, uint32_t e,
-                                          uint32_t capg, uint32_t* tcnt, uint32_t* tlist, uint32_t& cu,
-                                          uint32_t (&du)[S]) {
+                                          uint32_t capg, uint32_t* tcnt, uint32_t* tlist) {
   if (l == SQ_INF) return;  // 2^32 - 1 ns or more: no u32 path is that long, never tight
-  const uint32_t u = uv & 0xFFFFu;
-  if (u != cu) {
-    cu = u;
-#pragma unroll
-    for (int k = 0; k < S; k += 4) {
-      const uint4 x = *(const uint4*)(row + u * S + k);
-      du[k] = x.x;
-      du[k + 1] = x.y;
-      du[k + 2] = x.z;
-      du[k + 3] = x.w;
-    }
-  }
+  const uint32_t* du = row + (uv & 0xFFFFu) * S;
   const uint32_t* dv = row + (uv >> 16) * S;
 #pragma unroll
   for (int k = 0; k < S; k += 4) {
-    const uint4 y = *(const uint4*)(dv + k);
-    const uint32_t b[4] = {y.x, y.y, y.z, y.w};
+    const uint4 x = *(const uint4*)(du + k), y = *(const uint4*)(dv + k);
+    const uint32_t a[4] = {x.x, x.y, x.z, x.w}, b[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (du[k + j] == SQ_INF || (uint64_t)du[k + j] + l != (uint64_t)b[j]) continue;
+      if (a[j] == SQ_INF || (uint64_t)a[j] + l != (uint64_t)b[j]) continue;
       const uint32_t src = g0 + k + j;
       const uint32_t pos = atomicAdd(&tcnt[src], 1u);
       if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
@@ -332,30 +318,33 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
     row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
   }
   __syncthreads();
-  // this workgroup's share of the arc list in runs of 8 consecutive arcs per thread (two
-  // 16-byte loads of each array in flight; consecutive arcs mostly share their tail u)
-  const uint32_t E8 = E2 / 8;
-  const uint32_t per = (E8 + gridDim.y - 1) / gridDim.y;
-  const uint32_t q0 = blockIdx.y * per, q1 = min(E8, q0 + per);
+  // this workgroup's share of the arc list in 4-arc quads; two quads per thread in flight
+  const uint32_t E4 = E2 / 4;
+  const uint32_t per = (E4 + gridDim.y - 1) / gridDim.y;
+  const uint32_t q0 = blockIdx.y * per, q1 = min(E4, q0 + per);
   const uint4* a4 = (const uint4*)auv;
   const uint4* l4 = (const uint4*)al32;
-  uint32_t cu = 0xFFFFFFFFu;
-  uint32_t du[S];
-  for (uint32_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-    const uint4 a = a4[2 * q], b = a4[2 * q + 1], l = l4[2 * q], m = l4[2 * q + 1];
-    const uint32_t e = 8 * q;
-    sweep_arc<S>(row, g0, a.x, l.x, e, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, a.y, l.y, e + 1, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, a.z, l.z, e + 2, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, a.w, l.w, e + 3, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, b.x, m.x, e + 4, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, b.y, m.y, e + 5, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, b.z, m.z, e + 6, capg, tcnt, tlist, cu, du);
-    sweep_arc<S>(row, g0, b.w, m.w, e + 7, capg, tcnt, tlist, cu, du);
+  for (uint32_t q = q0 + threadIdx.x; q < q1; q += 2 * blockDim.x) {
+    const uint32_t q2 = q + blockDim.x;
+    const bool two = q2 < q1;
+    const uint4 a = a4[q], l = l4[q];
+    uint4 b = make_uint4(0, 0, 0, 0), m = make_uint4(SQ_INF, SQ_INF, SQ_INF, SQ_INF);
+    if (two) {
+      b = a4[q2];
+      m = l4[q2];
+    }
+    sweep_arc<S>(row, g0, a.x, l.x, 4 * q, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.y, l.y, 4 * q + 1, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.z, l.z, 4 * q + 2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, a.w, l.w, 4 * q + 3, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.x, m.x, 4 * q2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.y, m.y, 4 * q2 + 1, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.z, m.z, 4 * q2 + 2, capg, tcnt, tlist);
+    sweep_arc<S>(row, g0, b.w, m.w, 4 * q2 + 3, capg, tcnt, tlist);
   }
   if (blockIdx.y == gridDim.y - 1)
-    for (uint32_t e = 8 * E8 + threadIdx.x; e < E2; e += blockDim.x)
-      sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist, cu, du);
+    for (uint32_t e = 4 * E4 + threadIdx.x; e < E2; e += blockDim.x)
+      sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist);
 }
 
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
@@ -693,26 +682,6 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       if (!g->directed) {
         auv.push_back(ed[k] | (es[k] << 16)); al.push_back(g->edge_latency_ns[k]); ap.push_back(g->edge_loss[k]);
       }
-    }
-    // arcs ordered by their tail u (counting sort; the order is otherwise immaterial: each arc
-    // is tested on its own and the fold's fixed point does not depend on order), so a sweep
-    // thread's consecutive arcs share u
-    {
-      std::vector<uint32_t> start(V + 1, 0);
-      for (uint32_t x : auv) start[(x & 0xFFFFu) + 1]++;
-      for (uint32_t i = 0; i < V; i++) start[i + 1] += start[i];
-      std::vector<uint32_t> a2(auv.size());
-      std::vector<uint64_t> l2(auv.size());
-      std::vector<float> p2(auv.size());
-      for (size_t e = 0; e < auv.size(); e++) {
-        const uint32_t k = start[auv[e] & 0xFFFFu]++;
-        a2[k] = auv[e];
-        l2[k] = al[e];
-        p2[k] = ap[e];
-      }
-      auv.swap(a2);
-      al.swap(l2);
-      ap.swap(p2);
     }
     const uint32_t E2 = (uint32_t)auv.size();
     std::vector<uint64_t> sl(U);
