@@ -290,26 +290,34 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
 
 
 def apsp_roofline(apsp, V, U):
-    """the blocked min-plus latency phase streams the V x V u64 matrix once
-    per k-block (B_fw = 16 V^3 / T); the loss phase reads, per sweep and source, the tight arcs
-    (20 B each) and the V-entry distance row (12 B each): B_loss = U H (20 E_tight + 12 V)."""
+    """SURVEY.md §8(d) per phase, algorithmic bytes of the form that ran:
+    latency — u64 blocked Floyd-Warshall: the V x V u64 matrix read+written per k-block,
+    16 V^3 / T; u32 min-plus squaring: per pass every T x T tile reads its row and column
+    panels, 8 V^3 / T; per-source relaxation (sparse graphs): every sweep reads the arc list
+    (12 B per arc) for every used source, 12 U E sweeps.
+    loss — multi-source sweep (kS sources per arc load): 8 B per arc per source group plus
+    the rows, 8 E ceil(U / kS) + 4 U V; one-source pass: 12 B per arc per source, 12 U E.
+    The arc list is re-read from L2 / MALL, so these are traffic above HBM, not HBM bytes."""
     T = apsp["tile"] or 64
-    if apsp.get("latency_u64", 1):
-        b_fw = 16.0 * V ** 3 / T  # u64 blocked Floyd-Warshall: the matrix read+written per k-block
+    E = apsp["n_tight_edges"]
+    if apsp.get("latency_bf"):
+        b_lat = 12.0 * U * E * max(1, apsp["latency_passes"])
+    elif apsp.get("latency_u64", 1):
+        b_lat = 16.0 * V ** 3 / T
     else:
-        # u32 min-plus squaring: per pass every T x T output tile reads its row and column
-        # panels (2 T V entries of 4 B): 8 V^3 / T bytes per pass
-        b_fw = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
-    b_loss = float(U) * max(1, apsp["loss_iters"]) * (20.0 * apsp["n_tight_edges"] / max(1, U) + 12.0 * V)
+        b_lat = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
+    k = apsp.get("loss_multi", 0)
+    b_loss = 8.0 * E * -(-U // k) + 4.0 * U * V if k else 12.0 * U * E
     out = {}
-    for name, b, ms in (("latency_phase", b_fw, apsp["latency_ms"]), ("loss_phase", b_loss, apsp["loss_ms"])):
+    for name, b, ms in (("latency_phase", b_lat, apsp["latency_ms"]), ("loss_phase", b_loss, apsp["loss_ms"])):
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         out[name] = {"bound": "hbm", "alg_bytes": int(b), "ms": round(ms, 3), "achieved": round(gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5)}
-    out["relaxations_per_s"] = round(V ** 3 / (apsp["latency_ms"] * 1e-3), 1) if apsp["latency_ms"] > 0 else None
-    out["note"] = ("latency phase: u32 min-plus squaring passes (every pass one independent tiled "
-                   "product, VALU-bound: add-with-clamp + min per relaxation) or, for paths of 2^32 ns "
-                   "and more, the u64 Floyd-Warshall (a chain of V dependent pivot steps)")
+    out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
+                   ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else "u32 min-plus squaring"),
+                   "loss": f"{k}-source arc sweep + LDS fold" if k else "one-source arc sweep + LDS fold"}
+    out["note"] = ("the min-plus passes are VALU-bound (add-with-clamp + min per relaxation); the arc "
+                   "sweeps re-read the arc list from L2 / MALL, so their bytes exceed HBM traffic")
     return out
 
 

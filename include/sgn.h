@@ -115,11 +115,13 @@ typedef struct sgn_routes_timing {
   uint32_t loss_iters;  /* sweeps to the fixed point */
   uint32_t tile;        /* min-plus tile edge T */
   uint64_t n_tight_edges;
-  uint32_t latency_passes; /* min-plus squaring passes (u32 form), or k-blocks (u64 Floyd-Warshall) */
+  uint32_t latency_passes; /* min-plus squaring passes (u32 form), k-blocks (u64 Floyd-Warshall),
+                              or relaxation sweeps (latency_bf) */
   uint32_t latency_u64;    /* 1: the u64 Floyd-Warshall form ran (an edge or path >= 2^32 - 1 ns) */
   uint32_t loss_multi;     /* sources per tight-arc sweep (u32 form, non-sparse graphs); 0: the
                               one-source loss pass */
-  uint32_t reserved;
+  uint32_t latency_bf;     /* 1: sparse graph, latencies by per-source relaxation (u64, exact);
+                              latency_passes = its most sweeps */
 } sgn_routes_timing;
 int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
 

@@ -271,6 +271,39 @@ __global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_
   if (__ballot(ch) && (threadIdx.x & 63) == 0) flag[it] = 1;
 }
 
+// Latency phase for sparse graphs: one workgroup per used source relaxes the arc list over
+// its distance row in LDS (u64, 64-bit LDS atomic min) until a sweep changes nothing —
+// Bellman-Ford, exact (integer latencies, all positive), a few sweeps of a short list instead
+// of V^3 min-plus work. Only used sources' rows of D are written (all that is read).
+__global__ __launch_bounds__(512) void bf_pass(uint64_t* D, uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
+                                               const uint64_t* al, uint32_t E2, uint32_t* iters) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned long long* Dr = (unsigned long long*)smem;
+  uint32_t* ch = (uint32_t*)(Dr + Vp);
+  const uint32_t s = usrc[blockIdx.x];
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) Dr[v] = v == s ? 0ULL : FW_INF;
+  uint32_t it = 0;
+  while (true) {
+    if (threadIdx.x == 0) *ch = 0;
+    __syncthreads();
+    bool changed = false;
+    for (uint32_t e = threadIdx.x; e < E2; e += blockDim.x) {
+      const uint32_t uv = auv[e];
+      const unsigned long long du = Dr[uv & 0xFFFFu];
+      if (du >= FW_INF) continue;
+      const unsigned long long nd = du + al[e];  // < 2^63: FW_INF = 2^62 bounds both terms
+      if (nd < Dr[uv >> 16] && nd < atomicMin(&Dr[uv >> 16], nd)) changed = true;
+    }
+    if (changed) *ch = 1;
+    __syncthreads();
+    it++;
+    if (!*ch) break;
+    __syncthreads();
+  }
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) D[(uint64_t)s * Vp + v] = Dr[v];
+  if (threadIdx.x == 0) iters[blockIdx.x] = it;
+}
+
 // D32 -> the u64 matrix the loss pass and the extraction read (2^32 - 1 -> "no path")
 __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -721,9 +754,12 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     uint64_t max_edge = 0;
     for (uint32_t k = 0; k < E; k++)
       if (es[k] != ed[k]) max_edge = std::max(max_edge, g->edge_latency_ns[k]);
-    // latency phase: u32 min-plus squaring when edges fit (exact unless a used pair ends at
+    // latency phase: sparse graphs relax per source (Bellman-Ford in LDS, u64, exact);
+    // otherwise u32 min-plus squaring when edges fit (exact unless a used pair ends at
     // 2^32 - 1 or above: then the u64 Floyd-Warshall redoes it), else Floyd-Warshall
-    bool fast = max_edge < SQ_INF && !getenv("SGN_APSP_FW");
+    const bool bf = E2 < 32ull * Vp && Vp * 8 + 16 <= 64 * 1024 && !getenv("SGN_APSP_FW") &&
+                    !getenv("SGN_APSP_SQ");
+    bool fast = !bf && max_edge < SQ_INF && !getenv("SGN_APSP_FW");
     DevBuf dD32, dflag;
     const uint32_t max_pass = 34;
     if (fast) {
@@ -762,9 +798,14 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       for (uint32_t e = 0; e < E2; e++) al32[e] = al[e] >= SQ_INF ? SQ_INF : (uint32_t)al[e];
       if ((rc = upload(ctx, dal32, al32.data(), E2))) return rc;
     }
+    DevBuf dbfit;
+    if (bf) SGN_HIP(ctx, hipMalloc(&dbfit.p, (size_t)U * 4));
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
-    if (fast) {
+    if (bf) {
+      hipLaunchKernelGGL(bf_pass, dim3(U), dim3(512), (size_t)Vp * 8 + 16, st, D, Vp, (const uint32_t*)dus.p,
+                         (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, (uint32_t*)dbfit.p);
+    } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
       SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, max_pass * 4, st));
       hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
@@ -874,9 +915,15 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
       goto latency_phase;
     }
-    tm.tile = fast ? (uint32_t)SQ_T : (uint32_t)FW_T;
+    tm.tile = bf ? 0u : fast ? (uint32_t)SQ_T : (uint32_t)FW_T;
     tm.latency_passes = fast ? sq_passes : nb;
     tm.latency_u64 = fast ? 0u : 1u;
+    tm.latency_bf = bf ? 1u : 0u;
+    if (bf) {
+      std::vector<uint32_t> bi(U);
+      SGN_HIP(ctx, hipMemcpy(bi.data(), dbfit.p, (size_t)U * 4, hipMemcpyDeviceToHost));
+      tm.latency_passes = *std::max_element(bi.begin(), bi.end());
+    }
     if (res[0] != ~0ULL) {
       const uint64_t i = res[0] / U, j = res[0] % U;
       return set_error(ctx, SGN_EINVAL, "used nodes " + std::to_string(used[i]) + " -> " +

@@ -61,6 +61,7 @@ def test_apsp_random_vs_oracle(ctxf, oracle, V, directed, seed):
     gl, gp = c.routes_copy()
     assert np.array_equal(ol, gl)
     assert np.array_equal(op.view(np.uint32), gp.view(np.uint32))
+    assert c.routes_timing()["latency_bf"] == 1  # sparse: per-source relaxation
 
 
 def test_apsp_complete_graph_vs_oracle(ctxf, oracle):
@@ -80,22 +81,29 @@ def test_apsp_complete_graph_vs_oracle(ctxf, oracle):
     assert np.array_equal(op2.view(np.uint32), gp2.view(np.uint32))
 
 
-def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle):
-    """Paths of 2^32 ns (4.29 s) or more: the u32 min-plus form cannot hold them, the build
-    redoes the latency phase with the u64 Floyd-Warshall; the table is still exact."""
+def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle, monkeypatch):
+    """Paths of 2^32 ns (4.29 s) or more: the u32 min-plus form (forced with SGN_APSP_SQ on this
+    sparse graph) cannot hold them, the build redoes the latency phase with the u64
+    Floyd-Warshall; the sparse graph's own form, per-source relaxation in u64, is exact anyway."""
     V = 40
     g = sgn.random_graph(V, seed=5, lat_lo_us=1_500_000, lat_hi_us=3_500_000)  # 1.5-3.5 s edges
     used = np.arange(V)
     ol, op = oracle.routes(g, used)
     assert ol.max() >= 1 << 32
     c = ctxf()
+    c.routes_build(g, used)  # sparse: per-source relaxation
+    gl, gp = c.routes_copy()
+    assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32))
+    assert c.routes_timing()["latency_bf"] == 1
+    monkeypatch.setenv("SGN_APSP_SQ", "1")
     c.routes_build(g, used)
     gl, gp = c.routes_copy()
     assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32))
-    assert c.routes_timing()["latency_u64"] == 1
+    t = c.routes_timing()
+    assert t["latency_u64"] == 1 and t["latency_bf"] == 0
     c.routes_build(sgn.random_graph(V, seed=5), used)
     t = c.routes_timing()
-    assert t["latency_u64"] == 0 and 1 <= t["latency_passes"] <= 8
+    assert t["latency_u64"] == 0 and 1 <= t["latency_passes"] <= 8 and t["latency_bf"] == 0
 
 
 def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):

@@ -26,7 +26,8 @@ def run(kind, V):
     t = ts[-1]
     return {"graph": kind, "V": V, "arcs": int(t["n_tight_edges"]), "first_build_ms": round(ts[0]["total_ms"], 3),
             **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()},
-            "form": "u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring",
+            "form": "per-source relaxation (u64)" if t["latency_bf"] else
+                    ("u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring"),
             "loss_form": f"{t['loss_multi']}-source sweep + fold" if t["loss_multi"] else "one-source pass"}
 
 
@@ -34,13 +35,16 @@ if __name__ == "__main__":
     if len(sys.argv) > 2:
         print(json.dumps(run(sys.argv[1], int(sys.argv[2]))), flush=True)
         sys.exit(0)
-    for mode in ("default", "loss1", "fw"):
+    for mode in ("default", "sq", "loss1", "fw"):
         for kind in ("tor", "random"):
             for V in (1000, 2000):
                 env = dict(os.environ)
                 env.pop("SGN_APSP_FW", None)
                 env.pop("SGN_APSP_LOSS1", None)
-                if mode == "fw":
+                env.pop("SGN_APSP_SQ", None)
+                if mode == "sq":
+                    env["SGN_APSP_SQ"] = "1"
+                elif mode == "fw":
                     env["SGN_APSP_FW"] = "1"
                 elif mode == "loss1":
                     env["SGN_APSP_LOSS1"] = "1"
