@@ -1301,6 +1301,16 @@ struct HostExec {
     }
   }
 
+  // Is local slot W (0: relay_inet_out, 1: relay_inet_in) due at `now` and the host's next
+  // event? No packet run at `now` (pt: the next due run's time) and every other local event
+  // later by (time, event id).
+  template <int W>
+  __device__ __forceinline__ bool next_local_now(uint64_t pt) const {
+    const uint64_t t = W == 0 ? st0 : st1, e = W == 0 ? se0 : se1;
+    const uint64_t ta = W == 0 ? st1 : st0, ea = W == 0 ? se1 : se0;
+    return t == now && pt > now && (ta > now || (ta == now && ea > e)) && (st2 > now || (st2 == now && se2 > e));
+  }
+
   // ---- Host::execute (host.rs:762-830) over the host's due event runs + local slots ----
   // ev[ord[s0 .. s1)] are the host's runs due before `until` in Shadow's order, (time, src
   // host, src event id) (core/work/event.rs:84-155), in LDS; local events run while their
@@ -1343,6 +1353,7 @@ struct HostExec {
       // inside relay_inet_out's forwarding task: its next step (the one call site of
       // forward_out_step below), no other event of the host
       if (!(fl & F_RO_CONT)) {
+        int run_ls;
         if (pi < s1 && pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           const EvRec& e = ev[ord[pi]];
           pi++;
@@ -1368,22 +1379,31 @@ struct HostExec {
           codel_push_run(src, eid0, ev_payload(e), e.tag, n);
           relay_notify<1>();  // Host::notify_router_has_packets (host.rs:958-960)
           DGT_END(DGT_POP, t0);
-          continue;
+          // the relay_inet_in task at `now` is the host's next event when no packet is due at
+          // `now` (Packet < Local at equal times) and no other local event precedes it by
+          // (time, event id): it runs in this iteration (the same sequence of events; the wave
+          // saves a trip round the loop)
+          if (!next_local_now<1>(pi < s1 ? pt : INVALID)) continue;
+          run_ls = 1;
+        } else {
+          if (lt >= until) break;
+          now = lt;
+          run_ls = ls;
         }
-        if (lt >= until) break;
-        now = lt;
         c_localev++;
-        if (ls == 1) {
-          st1 = INVALID;
-          run_forward_task<1>();
-          continue;
-        }
-        if (ls == 2) {
-          st2 = INVALID;
-          DGT_BEGIN(t0);
-          app_task();
-          DGT_END(DGT_LOAD, t0);
-          continue;
+        if (run_ls != 0) {
+          if (run_ls == 1) {
+            st1 = INVALID;
+            run_forward_task<1>();
+          } else {
+            st2 = INVALID;
+            DGT_BEGIN(t0);
+            app_task();
+            DGT_END(DGT_LOAD, t0);
+          }
+          // a send queued at `now` makes relay_inet_out's task the next event: start it here
+          if (!next_local_now<0>(pi < s1 ? pt : INVALID)) continue;
+          c_localev++;
         }
         // run_forward_task for relay_inet_out (relay/mod.rs:166-187): Idle, then Forwarding
         st0 = INVALID;
