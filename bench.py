@@ -361,11 +361,6 @@ def main():
 
     ctx = sgn.Context(device=local, shard_rank=rank, shard_count=world,
                       flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around the round kernel
-    ctx.routes_build(g, used)
-    apsp_first = ctx.routes_timing()  # includes loading the APSP kernels' code object
-    ctx.routes_build(g, used)         # steady state: the build time proper
-    apsp = ctx.routes_timing()
-    ctx.hosts_set(hosts)
     if world > 1:
         import torch
         idb = (sgn.C.c_uint8 * 128)()
@@ -377,6 +372,29 @@ def main():
         # per-peer exchange slot: 8192 event runs (256 KB) per round; a round sends ~700 runs
         # per peer at 100k hosts per GPU (overflow is detected and reported, never silent)
         ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 13))
+    # with the communicator set, the APSP build is sharded: each GPU computes its block of
+    # used sources and the blocks are exchanged over RCCL
+    ctx.routes_build(g, used)
+    apsp_first = ctx.routes_timing()  # includes loading the APSP kernels' code object
+    ctx.routes_build(g, used)         # steady state: the build time proper
+    apsp = ctx.routes_timing()
+    apsp_shard = None
+    if world > 1:
+        # the sharded table against one built whole on this GPU (SGN_APSP_REPLICATED), bit for bit
+        lat_s, loss_s = ctx.routes_copy()
+        os.environ["SGN_APSP_REPLICATED"] = "1"
+        ctx.routes_build(g, used)
+        whole = ctx.routes_timing()
+        lat_w, loss_w = ctx.routes_copy()
+        del os.environ["SGN_APSP_REPLICATED"]
+        same = bool(np.array_equal(lat_s, lat_w) and np.array_equal(loss_s.view(np.uint32), loss_w.view(np.uint32)))
+        import torch
+        f = torch.tensor([0 if same else 1], dtype=torch.int64)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        apsp_shard = {"shards": apsp["shards"], "equal_on_all_ranks": int(f.item()) == 0,
+                      "replicated_ms": round(whole["total_ms"], 3), "sharded_ms": round(apsp["total_ms"], 3)}
+        ctx.routes_build(g, used)  # the sharded table again for the run
+    ctx.hosts_set(hosts)
     ctx.sim_init(cfg, tr)
 
     def barrier():
@@ -474,6 +492,7 @@ def main():
         "apsp": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in apsp.items()},
         "apsp_first_build_ms": round(apsp_first["total_ms"], 3),
         "apsp_roofline": apsp_roofline(apsp, args.nodes, len(used)),
+        "apsp_sharded": apsp_shard,
         "sim_ms_per_step": None,
         "rounds_timed": rounds,
         "packet_events_timed": ev,
@@ -488,14 +507,14 @@ def main():
     ws, we, act = ctx.window()
     out["sim_time_reached_ms"] = (ws - sgn.SIMULATION_START) / 1e6
     out["sim_ms_per_step"] = out["sim_time_reached_ms"] / (args.steps + args.warmup)
-    ok = True
+    ok = apsp_shard is None or apsp_shard["equal_on_all_ranks"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gpu = {"rounds_timed": rounds, "stats": st1, "window": (ws, we, act),
                "digests": ctx.digests(0, hosts.n)}
         out["cpu_baseline"], par = cpu_baseline(g, used, hosts, cfg, tr, args, gpu)
         out["parity"] = par["ok"]
         out["parity_detail"] = par
-        ok = par["ok"]
+        ok = ok and par["ok"]
     if world > 1 and args.workload == "C" and not args.no_shard_check:
         def unsharded():
             c1 = sgn.Context(device=local)
@@ -508,7 +527,7 @@ def main():
         if rank == 0:
             out["parity"] = par["ok"]
             out["parity_detail"] = par
-            ok = par["ok"]
+            ok = ok and par["ok"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 4
+#define SGN_ABI_VERSION 5
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -122,6 +122,11 @@ typedef struct sgn_routes_timing {
                               one-source loss pass */
   uint32_t latency_bf;     /* 1: sparse graph, latencies by per-source relaxation (u64, exact);
                               latency_passes = its most sweeps */
+  uint32_t shards;         /* blocks the build was split into: the shard count when a
+                              communicator is set (sgn_comm_init before the build; every shard
+                              computes its block of used sources and the blocks are exchanged
+                              over RCCL, so every shard ends with the whole table), else 1 */
+  uint32_t shard_sources;  /* used sources whose rows this process computed */
 } sgn_routes_timing;
 int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
 

@@ -101,6 +101,47 @@ int comm_round_exchange(sgn_ctx* ctx) {
   return 0;
 }
 
+// Sharded APSP (routes.hip): every shard owns a contiguous block of rows (row tiles of the
+// squaring matrix, or used sources of the final table) and the blocks are exchanged with one
+// grouped in-place broadcast per step: shard r is the root of block r, so after the group
+// every shard holds every block (an all-gather of blocks of unequal sizes).
+int comm_bcast_blocks(sgn_ctx* ctx, void* base, size_t unit_bytes, const std::vector<uint64_t>& off) {
+  ncclComm_t comm = (ncclComm_t)ctx->comm;
+  ncclResult_t r = ncclGroupStart();
+  for (uint32_t p = 0; p + 1 < off.size() && r == ncclSuccess; p++) {
+    const size_t bytes = (size_t)(off[p + 1] - off[p]) * unit_bytes;
+    if (!bytes) continue;
+    char* b = (char*)base + (size_t)off[p] * unit_bytes;
+    r = ncclBroadcast(b, b, bytes, ncclUint8, (int)p, comm, ctx->stream);
+  }
+  ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return set_error(ctx, SGN_EDEVICE, std::string("RCCL row exchange: ") +
+                                           ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return 0;
+}
+
+// In-place all-reduces of small device words: n_min u64 by min, then n_max u64 by max
+// (one group).
+int comm_allreduce_minmax(sgn_ctx* ctx, uint64_t* p, size_t n_min, size_t n_max) {
+  ncclComm_t comm = (ncclComm_t)ctx->comm;
+  ncclResult_t r = ncclGroupStart();
+  if (n_min && r == ncclSuccess) r = ncclAllReduce(p, p, n_min, ncclUint64, ncclMin, comm, ctx->stream);
+  if (n_max && r == ncclSuccess)
+    r = ncclAllReduce(p + n_min, p + n_min, n_max, ncclUint64, ncclMax, comm, ctx->stream);
+  ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-reduce: ") +
+                                           ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return 0;
+}
+
+int comm_allreduce_max_u32(sgn_ctx* ctx, uint32_t* p, size_t n) {
+  ncclResult_t r = ncclAllReduce(p, p, n, ncclUint32, ncclMax, (ncclComm_t)ctx->comm, ctx->stream);
+  if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-reduce: ") + ncclGetErrorString(r));
+  return 0;
+}
+
 }  // namespace sgn
 
 // ------------------------------------------------------------------------------------

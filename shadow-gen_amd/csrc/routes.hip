@@ -218,12 +218,13 @@ __global__ void sq_edges(uint32_t* D, uint32_t Vp, const uint32_t* eu, const uin
 // One pass, 64 x 64 output tile per workgroup of 256 threads, 4 x 4 consecutive entries per
 // thread; K in steps of 32 through LDS (A transposed so both operands are 16-byte reads).
 // flag[it] = 1 if anything changed; the pass returns at once when pass it - 1 changed nothing.
-__global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_t* flag, int it) {
+// rt0: the first row tile of this launch (a shard's block of rows, gridDim.y tiles)
+__global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_t* flag, int it, uint32_t rt0) {
   if (it > 0 && __hip_atomic_load(&flag[it - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   __shared__ __attribute__((aligned(16))) uint32_t As[SQ_K][SQ_T + 4];
   __shared__ __attribute__((aligned(16))) uint32_t Bs[SQ_K][SQ_T + 4];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const uint64_t r0 = (uint64_t)blockIdx.y * SQ_T, c0 = (uint64_t)blockIdx.x * SQ_T;
+  const uint64_t r0 = (uint64_t)(blockIdx.y + rt0) * SQ_T, c0 = (uint64_t)blockIdx.x * SQ_T;
   uint32_t acc[4][4], orig[4][4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -542,12 +543,13 @@ __global__ __launch_bounds__(512) void loss_pass(const uint64_t* D, uint32_t Vp,
 // The U x U table straight into the engine's device buffers: latency from D, loss from the
 // loss rows, each used node's (n,n) entry replaced by its single self-loop edge
 // (graph/mod.rs:209-215); res = {first disconnected pair index, min latency, max latency}.
+// Rows [row0, row1) only (a shard's block of used sources; the whole table unsharded).
 __global__ void extract(const uint64_t* D, uint32_t Vp, const float* Lrows, const uint32_t* uidx,
                         uint32_t U, const uint64_t* self_lat, const float* self_loss,
-                        uint64_t* lat, float* loss, unsigned long long* res) {
-  const uint64_t n = (uint64_t)U * U;
+                        uint64_t* lat, float* loss, unsigned long long* res, uint32_t row0, uint32_t row1) {
+  const uint64_t n = (uint64_t)U * row1;
   uint64_t mn = ~0ULL, mx = 0, bad = ~0ULL;
-  for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n;
+  for (uint64_t x = (uint64_t)U * row0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n;
        x += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t i = (uint32_t)(x / U), j = (uint32_t)(x % U);
     uint64_t l;
@@ -800,11 +802,41 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     DevBuf dbfit;
     if (bf) SGN_HIP(ctx, hipMalloc(&dbfit.p, (size_t)U * 4));
+    // Sharded build. With an RCCL communicator (sgn_comm_init before the build)
+    // every shard computes a contiguous block of the used sources' rows — and in the squaring
+    // form a block of row tiles per pass, exchanged after each pass — and the table's blocks are
+    // exchanged at the end, so every shard holds the whole table; all shards must call
+    // sgn_routes_build with the same graph. The u64 Floyd-Warshall (a chain of pivot steps)
+    // runs whole on every shard. SGN_APSP_REPLICATED=1: every shard builds the table alone.
+    // SGN_APSP_VSHARDS=n without a communicator (a test hook): one process runs the n blocks
+    // in turn over one buffer, which checks the block arithmetic on one GPU.
+    uint32_t nsh = 1, me = 0;
+    bool rccl = false;
+    if (ctx->comm && ctx->nranks > 1 && !getenv("SGN_APSP_REPLICATED")) {
+      nsh = ctx->nranks;
+      me = ctx->rank;
+      rccl = true;
+    } else if (const char* v = getenv("SGN_APSP_VSHARDS")) {
+      nsh = (uint32_t)std::max(1, std::min(atoi(v), 1024));
+    }
+    const uint32_t sh_first = rccl ? me : 0, sh_last = rccl ? me + 1 : nsh;
+    std::vector<uint64_t> soff(nsh + 1), toff(nsh + 1);  // used-source blocks, row-tile blocks
+    for (uint32_t r = 0; r <= nsh; r++) {
+      soff[r] = (uint64_t)U * r / nsh;
+      toff[r] = (uint64_t)nb * r / nsh;
+    }
+    tm.shards = nsh;
+    tm.shard_sources = (uint32_t)(soff[sh_last] - soff[sh_first]);
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
-    if (bf) {
-      hipLaunchKernelGGL(bf_pass, dim3(U), dim3(512), (size_t)Vp * 8 + 16, st, D, Vp, (const uint32_t*)dus.p,
-                         (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2, (uint32_t*)dbfit.p);
+    if (bf) {  // per source: a shard's block needs no exchange until the table
+      for (uint32_t r = sh_first; r < sh_last; r++) {
+        const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
+        if (ns)
+          hipLaunchKernelGGL(bf_pass, dim3(ns), dim3(512), (size_t)Vp * 8 + 16, st, D, Vp,
+                             (const uint32_t*)dus.p + s0, (const uint32_t*)dauv.p, (const uint64_t*)dal.p, E2,
+                             (uint32_t*)dbfit.p + s0);
+      }
     } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
       SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, max_pass * 4, st));
@@ -816,8 +848,22 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       uint32_t passes = 1;
       while ((1u << (passes - 1)) < Vp) passes++;
       passes = std::min(passes + 1, max_pass);
-      for (uint32_t it = 0; it < passes; it++)
-        hipLaunchKernelGGL(sq_pass, dim3(nb, nb), dim3(256), 0, st, D32, Vp, (uint32_t*)dflag.p, (int)it);
+      for (uint32_t it = 0; it < passes; it++) {
+        for (uint32_t r = sh_first; r < sh_last; r++) {
+          const uint32_t t0 = (uint32_t)toff[r], nt = (uint32_t)(toff[r + 1] - t0);
+          if (nt)
+            hipLaunchKernelGGL(sq_pass, dim3(nb, nt), dim3(256), 0, st, D32, Vp, (uint32_t*)dflag.p, (int)it, t0);
+        }
+        if (rccl) {  // every shard's new rows to all, and whether any shard changed a row
+          if ((rc = comm_bcast_blocks(ctx, D32, (size_t)SQ_T * Vp * 4, toff)) ||
+              (rc = comm_allreduce_max_u32(ctx, (uint32_t*)dflag.p + it, 1)))
+            return rc;
+          uint32_t f = 0;
+          SGN_HIP(ctx, hipMemcpyAsync(&f, (uint32_t*)dflag.p + it, 4, hipMemcpyDeviceToHost, st));
+          SGN_HIP(ctx, hipStreamSynchronize(st));
+          if (!f) break;
+        }
+      }
       hipLaunchKernelGGL(sq_widen, dim3(2048), dim3(256), 0, st, D32, D, (uint64_t)Vp * Vp);
     } else {
       hipLaunchKernelGGL(fw_init, dim3(2048), dim3(256), 0, st, D, Vp);
@@ -840,22 +886,27 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     int form = lform;
     if (form) {
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
-      {
-        const uint32_t groups = (U + kS - 1) / kS;
+      for (uint32_t r = sh_first; r < sh_last; r++) {
+        const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
+        if (!ns) continue;
+        const uint32_t groups = (ns + kS - 1) / kS;
         const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(64, (2048 + groups - 1) / groups));
         const dim3 grid(groups, std::min<uint32_t>(parts, std::max<uint32_t>(1, E2 / 4096)));
         const uint32_t* d32 = (const uint32_t*)dD32.p;
         const uint32_t* a32 = (const uint32_t*)dal32.p;
+        const uint32_t* us = (const uint32_t*)dus.p + s0;
+        uint32_t* tcs = (uint32_t*)dtc.p + s0;
+        uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
         if (kS == 8)
-          hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                             (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+          hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns,
+                             (const uint32_t*)dauv.p, a32, E2, capg, tcs, tls);
         else
-          hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, (const uint32_t*)dus.p, U,
-                             (const uint32_t*)dauv.p, a32, E2, capg, (uint32_t*)dtc.p, (uint32_t*)dtl.p);
+          hipLaunchKernelGGL(loss_sweep<4>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns,
+                             (const uint32_t*)dauv.p, a32, E2, capg, tcs, tls);
+        hipLaunchKernelGGL(loss_fold, dim3(ns), dim3(256), lds_fold, st, Vp, us, (const uint32_t*)dauv.p,
+                           (const float*)dap.p, (const uint32_t*)tcs, (const uint32_t*)tls, capg, cap,
+                           (float*)dL.p + (size_t)s0 * Vp, (uint32_t*)dit.p + s0);
       }
-      hipLaunchKernelGGL(loss_fold, dim3(U), dim3(256), lds_fold, st, Vp, (const uint32_t*)dus.p,
-                         (const uint32_t*)dauv.p, (const float*)dap.p, (const uint32_t*)dtc.p,
-                         (const uint32_t*)dtl.p, capg, cap, (float*)dL.p, (uint32_t*)dit.p);
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
       // a source with more tight pairs than its list holds: redo the phase the one-source way
@@ -867,16 +918,29 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     tm.loss_multi = form ? (uint32_t)kS : 0u;
     if (!form) {
-      hipLaunchKernelGGL(loss_pass, dim3(U), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p,
-                         (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
-                         (float*)dL.p, (uint32_t*)dit.p);
+      for (uint32_t r = sh_first; r < sh_last; r++) {
+        const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
+        if (ns)
+          hipLaunchKernelGGL(loss_pass, dim3(ns), dim3(512), lds2, st, D, Vp, (const uint32_t*)dus.p + s0,
+                             (const uint32_t*)dauv.p, (const uint64_t*)dal.p, (const float*)dap.p, E2, cap,
+                             (float*)dL.p + (size_t)s0 * Vp, (uint32_t*)dit.p + s0);
+      }
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
     }
-    hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
-                       (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p, (const float*)dsp.p,
-                       ctx->d_lat, ctx->d_loss, (unsigned long long*)dres.p);
+    for (uint32_t r = sh_first; r < sh_last; r++)
+      if (soff[r + 1] > soff[r])
+        hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
+                           (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p, (const float*)dsp.p,
+                           ctx->d_lat, ctx->d_loss, (unsigned long long*)dres.p, (uint32_t)soff[r],
+                           (uint32_t)soff[r + 1]);
     SGN_HIP(ctx, hipGetLastError());
+    if (rccl) {  // the table's blocks to every shard; res = {min bad pair, min, max} over shards
+      if ((rc = comm_bcast_blocks(ctx, ctx->d_lat, (size_t)U * 8, soff)) ||
+          (rc = comm_bcast_blocks(ctx, ctx->d_loss, (size_t)U * 4, soff)) ||
+          (rc = comm_allreduce_minmax(ctx, (uint64_t*)dres.p, 2, 1)))
+        return rc;
+    }
     unsigned long long res[3];
     SGN_HIP(ctx, hipMemcpyAsync(res, dres.p, sizeof(res), hipMemcpyDeviceToHost, st));
     SGN_HIP(ctx, hipEventRecord(e3, st));

@@ -414,6 +414,9 @@ void time_collect(sgn_ctx* ctx);
 // comm.cpp
 void comm_destroy(sgn_ctx* ctx);
 int comm_round_exchange(sgn_ctx* ctx);
+int comm_bcast_blocks(sgn_ctx* ctx, void* base, size_t unit_bytes, const std::vector<uint64_t>& off);
+int comm_allreduce_minmax(sgn_ctx* ctx, uint64_t* p, size_t n_min, size_t n_max);
+int comm_allreduce_max_u32(sgn_ctx* ctx, uint32_t* p, size_t n);
 }  // namespace sgn
 
 #define SGN_HIP(ctx, call)                                   \

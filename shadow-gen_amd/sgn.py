@@ -167,7 +167,8 @@ class RoutesTiming(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("latency_ms", C.c_double), ("loss_ms", C.c_double),
                 ("loss_iters", C.c_uint32), ("tile", C.c_uint32), ("n_tight_edges", C.c_uint64),
                 ("latency_passes", C.c_uint32), ("latency_u64", C.c_uint32),
-                ("loss_multi", C.c_uint32), ("latency_bf", C.c_uint32)]
+                ("loss_multi", C.c_uint32), ("latency_bf", C.c_uint32),
+                ("shards", C.c_uint32), ("shard_sources", C.c_uint32)]
 
 
 class EngineInfo(C.Structure):

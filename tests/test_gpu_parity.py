@@ -139,6 +139,41 @@ def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
         assert (forms[0] >= 4) == (k < 2), (k, forms)  # sparse graph / list overflow: one-source
 
 
+@pytest.mark.parametrize("n_shards", [2, 3, 8])
+def test_apsp_sharded_blocks_equal_whole(ctxf, oracle, monkeypatch, n_shards):
+    """The sharded build's block arithmetic (every shard computes a block of used
+    sources, and a block of row tiles per squaring pass) on one GPU: SGN_APSP_VSHARDS runs the n
+    blocks in turn over one buffer, through every form — per-source relaxation, squaring with
+    the multi-source sweep, the one-source loss pass, the u64 Floyd-Warshall fallback — with
+    uneven blocks, blocks without a row tile (V <= 64), and more shards than used sources.
+    The RCCL exchange between the blocks runs in the multi-GPU bench (bench.py shard_check)."""
+    Vl = 40
+    long_g = sgn.random_graph(Vl, seed=5, lat_lo_us=1_500_000, lat_hi_us=3_500_000)
+    cases = [(sgn.random_graph(333, seed=4, loss_frac=0.5), np.arange(0, 333, 2), {}),
+             (sgn.tor_graph(600, seed=3), np.arange(600), {}),
+             (sgn.tor_graph(200, seed=9), np.arange(200), {"SGN_APSP_LOSS1": "1"}),
+             (long_g, np.arange(Vl), {"SGN_APSP_SQ": "1"}),
+             (sgn.tor_graph(50, seed=2), np.array([3, 17, 41]), {})]
+    for k, (g, used, env) in enumerate(cases):
+        ol, op = oracle.routes(g, used)
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        c = ctxf()
+        c.routes_build(g, used)
+        whole = c.routes_timing()
+        monkeypatch.setenv("SGN_APSP_VSHARDS", str(n_shards))
+        c.routes_build(g, used)
+        t = c.routes_timing()
+        monkeypatch.delenv("SGN_APSP_VSHARDS")
+        for key in env:
+            monkeypatch.delenv(key)
+        gl, gp = c.routes_copy()
+        assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), k
+        assert whole["shards"] == 1 and t["shards"] == n_shards and t["shard_sources"] == len(used)
+        for f in ("latency_bf", "latency_u64", "loss_multi"):
+            assert t[f] == whole[f], (k, f)
+
+
 def test_apsp_errors(ctxf):
     c = ctxf()
     g = sgn.GraphArrays([0, 1], [0, 0, 1], [1, 0, 1], [5, 3, 3], [0, 0, 0], False)
