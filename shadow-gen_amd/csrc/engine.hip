@@ -83,6 +83,37 @@ constexpr uint64_t SIMTIME_MAX = 17500059273709551614ULL;
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) {
   return (x << k) | (x >> (64 - k));
 }
+// xoshiro256++'s operations on 32-bit halves for gfx950's VALU: a 64-bit rotate is two
+// v_alignbit_b32 (the compiler's shift pair + or takes three), and a ^ b ^ c is one
+// v_bitop3_b32 per half (LUT 0x96) where the compiler emits two v_xor_b32.
+__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+template <int K>  // rotate left by K, 0 < K < 64, K != 32
+__device__ __forceinline__ uint64_t rotl64c(uint64_t x) {
+  static_assert(K > 0 && K < 64 && K != 32, "rotate amount");
+  if constexpr (K < 32)
+    return mk64(__builtin_amdgcn_alignbit(lo32(x), hi32(x), 32 - K), __builtin_amdgcn_alignbit(hi32(x), lo32(x), 32 - K));
+  else
+    return mk64(__builtin_amdgcn_alignbit(hi32(x), lo32(x), 64 - K), __builtin_amdgcn_alignbit(lo32(x), hi32(x), 64 - K));
+}
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return mk64(__builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), 0x96),
+              __builtin_amdgcn_bitop3_b32(hi32(a), hi32(b), hi32(c), 0x96));
+}
+// one xoshiro256++ step (rand_xoshiro 0.7.0 Xoshiro256PlusPlus::next_u64) on state s0..s3
+__device__ __forceinline__ void xoshiro_step(uint64_t& s0, uint64_t& s1, uint64_t& s2, uint64_t& s3) {
+  // s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= s1 << 17 (old s1); s3 = rotl(s3, 45)
+  const uint64_t t = s1 << 17;
+  const uint64_t n1 = xor3_64(s1, s2, s0);
+  const uint64_t n0 = xor3_64(s0, s3, s1);
+  const uint64_t n2 = xor3_64(s2, s0, t);
+  s3 = rotl64c<45>(s3 ^ s1);
+  s0 = n0;
+  s1 = n1;
+  s2 = n2;
+}
+__device__ __forceinline__ uint64_t xoshiro_out(uint64_t s0, uint64_t s3) { return rotl64c<23>(s0 + s3) + s0; }
 __device__ __forceinline__ uint64_t sat_sub(uint64_t a, uint64_t b) { return a > b ? a - b : 0; }
 __device__ __forceinline__ uint64_t mul_sat(uint64_t a, uint64_t b, uint64_t cap) {
   uint64_t hi = __umul64hi(a, b);
@@ -434,25 +465,11 @@ struct HostExec {
 
   // ---- Xoshiro256++ (rand_xoshiro 0.7.0) + rand 0.9.2 StandardUniform f64 ----
   __device__ __forceinline__ uint64_t rng_next() {
-    const uint64_t result = rotl64(r0 + r3, 23) + r0;
-    const uint64_t t = r1 << 17;
-    r2 ^= r0;
-    r3 ^= r1;
-    r1 ^= r2;
-    r0 ^= r3;
-    r2 ^= t;
-    r3 = rotl64(r3, 45);
+    const uint64_t result = xoshiro_out(r0, r3);
+    xoshiro_step(r0, r1, r2, r3);
     return result;
   }
-  __device__ __forceinline__ void rng_skip() {  // rng_next without its output
-    const uint64_t t = r1 << 17;
-    r2 ^= r0;
-    r3 ^= r1;
-    r1 ^= r2;
-    r0 ^= r3;
-    r2 ^= t;
-    r3 = rotl64(r3, 45);
-  }
+  __device__ __forceinline__ void rng_skip() { xoshiro_step(r0, r1, r2, r3); }  // rng_next without its output
   __device__ __forceinline__ double rng_f64() {
     return (double)(rng_next() >> 11) * 0x1.0p-53;
   }
