@@ -22,7 +22,7 @@ def per_dispatch(counter):
     for r in rows:
         if ("k_rounds" in r["Kernel_Name"] or "k_execute" in r["Kernel_Name"]) and \
                 r["Counter_Name"] == counter:
-            kern = r["Kernel_Name"].split("(")[0].split("::")[-1]
+            kern = r["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]  # template args dropped
             k = int(r["Dispatch_Id"])
             vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
     v = [vals[k] for k in sorted(vals)]
