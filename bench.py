@@ -335,6 +335,11 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
                     help="wall budget of the CPU mode samples after the parity run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU machine: every rank on device 0, each "
+                         "with its own NCCL_HOSTID, so RCCL accepts the ranks (as if on different hosts) "
+                         "and moves the exchange over its socket transport; correctness only, not a "
+                         "scaling measurement")
     ap.add_argument("--no-shard-check", action="store_true",
                     help="N > 1: skip the unsharded re-run on rank 0 that checks the sharded results")
     args = ap.parse_args()
@@ -342,6 +347,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_gpu:
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"sgn-one-gpu-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -486,7 +496,7 @@ def main():
                          }[args.workload],
             "hosts_per_gpu": args.hosts, "hosts_total": n_total, "graph_nodes": args.nodes,
             "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
-            "parallelism": f"host-shard x{world}",
+            "parallelism": f"host-shard x{world}" + (" (one-GPU rehearsal: all ranks on device 0, RCCL socket transport)" if args.one_gpu else ""),
         },
         "apsp_build_ms": round(apsp["total_ms"], 3),
         "apsp": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in apsp.items()},
