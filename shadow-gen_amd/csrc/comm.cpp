@@ -8,9 +8,9 @@
 //      32-byte message per peer: {runs sent to it, this shard's min next event including
 //      the runs it exported, its min used latency},
 //   2. ONE grouped ncclSend/ncclRecv moves each peer's fixed-size run slot and message,
-//   3. k_import files the received runs into the local calendar,
-//   4. k_advance reduces the n messages (the global min: what an all-reduce would give)
-//      and moves the window — every shard computes the same window.
+//   3. k_import files the received runs into the local calendar, and its last block
+//      reduces the n messages (the global min: what an all-reduce would give) and moves
+//      the window — every shard computes the same window.
 // Every produced event has time >= the window end (worker.rs:386-390), so nothing needs
 // to cross shards inside a round.
 
@@ -26,7 +26,6 @@
 namespace sgn {
 void launch_execute(sgn_ctx* ctx);
 void launch_import(sgn_ctx* ctx);
-void launch_advance(sgn_ctx* ctx);
 }  // namespace sgn
 
 using namespace sgn;
@@ -77,8 +76,8 @@ namespace sgn {
 int comm_round_exchange(sgn_ctx* ctx) {
   // k_execute's last wave has already done the local round edge and written this shard's
   // message for every peer (run count, local min next event incl. exported runs, local min
-  // used latency): ONE grouped send/recv moves runs and messages, then every shard imports
-  // and reduces the messages itself (no all-reduce, no memsets).
+  // used latency): ONE grouped send/recv moves runs and messages, then one kernel on every
+  // shard imports the runs and reduces the messages (no all-reduce, no memsets).
   DevSim& S = ctx->S;
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   hipStream_t st = ctx->stream;
@@ -97,7 +96,6 @@ int comm_round_exchange(sgn_ctx* ctx) {
     return set_error(ctx, SGN_EDEVICE, std::string("RCCL exchange: ") +
                                            ncclGetErrorString(r != ncclSuccess ? r : r2));
   launch_import(ctx);
-  launch_advance(ctx);
   return 0;
 }
 
@@ -208,7 +206,6 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       sgn_ctx* c = ctxs[i];
       SGN_HIP(c, hipSetDevice(c->device));
       launch_import(c);
-      launch_advance(c);
       SGN_HIP(c, hipStreamSynchronize(c->stream));
     }
   }

@@ -14,7 +14,7 @@
 //            round (controller.rs:88-112) — run by the last wave to arrive
 // Kernels: k_rounds (single shard, persistent: up to 128 rounds per launch with an atomic
 // grid barrier per round), k_execute (one round per launch: sgn_round, multi-shard) with
-// k_import / k_advance around the RCCL exchange (comm.cpp), k_inject
+// k_import after the RCCL exchange (comm.cpp; its last block advances the window), k_inject
 // (sgn_submit), k_rng (sgn_rng_*). The window lives in device memory (Ctrl), so rounds run
 // back to back without a host round trip.
 //
@@ -1456,7 +1456,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
 // local != 0 (multi-shard): instead of moving the window, the shard's {min next event, min
 // used latency} and its per-peer run counts go into the round-edge messages (comm.cpp sends
-// them with the runs; k_advance reduces them on every shard).
+// them with the runs; k_import's last block reduces them on every shard).
 __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uint64_t ws,
                                uint64_t we, uint32_t ks, uint32_t slab_b1, int local = 0) {
   SGN_GLB Ctrl* C = S.ctrl;
@@ -2147,13 +2147,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   }
 }
 
-// Bucket bookkeeping + local minimum. With advance != 0 (single shard) also moves the
-// window; multi-shard runs reduce C->round_min/min_used across ranks first.
-// Multi-shard: window advance from the all-reduced {min_next, min_used}.
-// the global {min next event, min used latency} from every shard's round-edge message
-__global__ void k_advance(DevSim S) {
-  Ctrl* C = S.ctrl;
-  if (!C->active || threadIdx.x != 0) return;
+// Multi-shard round edge, after the exchange: the runs other shards sent this round into the
+// local calendar, then the window advance from every shard's message. k_execute's last wave
+// already did the local bucket bookkeeping, so every run goes to its bucket's current slab
+// set (runs for the window's last bucket into the spare slab, like local sends).
+// The advance (Controller::manager_finished_current_round, controller.rs:88-112, over the
+// global {min next event, min used latency}: each message's minimum counts every pending
+// event of its shard, exported runs included, so the min over messages is what an all-reduce
+// would give) is done by the LAST block to finish: every block has read the window that just
+// ran before it counts itself in, so no block sees the new one. One kernel per round edge.
+__device__ __forceinline__ void advance_window(const DevSim& S, Ctrl* C) {
   uint64_t m = INVALID, mu = INVALID;
   for (uint32_t p = 0; p < S.n_ranks; p++) {
     const uint64_t a = S.xmsg_in[4 * (size_t)p + 1], b = S.xmsg_in[4 * (size_t)p + 2];
@@ -2164,6 +2167,7 @@ __global__ void k_advance(DevSim S) {
   if (S.dynamic && mu != INVALID && mu < C->min_used) C->min_used = mu;
   const uint64_t min_next = m == INVALID ? EMU_MAX : m;
   C->last_min_next = min_next;
+  // Runahead::get (runahead.rs:44-57)
   uint64_t ra = (S.dynamic && C->min_used != INVALID) ? C->min_used : S.min_possible;
   ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
   uint64_t ne = min_next + ra;
@@ -2177,15 +2181,11 @@ __global__ void k_advance(DevSim S) {
   C->rounds++;
 }
 
-// Multi-shard: file received runs into the local calendar (after k_execute, so runs for
-// the window's last bucket go to the spare slab like local sends).
-// Multi-shard: the runs other shards sent this round into the calendar. Runs at or after
-// this round's window end: the bucket bookkeeping of the round edge already ran (k_execute's
-// last wave), so every run goes to its bucket's current slab set.
+constexpr uint32_t kImportBlocks = 128;
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
-  if (!C->active) return;
-  // the window that just ran is still C->ws (k_advance follows): the same horizon as sends
+  if (!C->active) return;  // every block reads the same value: nothing changes it before all count in
+  // the window that just ran (still C->ws): the same horizon as sends
   const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
     if (r == S.rank) continue;
@@ -2207,6 +2207,13 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
         C->overflow_info = e.dst;
     }
   }
+  __shared__ uint32_t last;
+  __syncthreads();  // this block's reads of C->ws are done
+  if (threadIdx.x == 0) last = atomicAdd(&C->imp_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  C->imp_done = 0;
+  advance_window(S, C);
 }
 
 // CoDel control-law self test (f64 sqrt/div/round on the device vs the host).
@@ -2312,8 +2319,8 @@ T* dalloc(sgn_ctx* ctx, size_t n) {
   return (T*)dev_alloc(ctx, n * sizeof(T));
 }
 
-enum { K_EXECUTE = 0, K_IMPORT, K_ADVANCE, K_NUM };
-const char* kKernelNames[K_NUM] = {"k_execute", "k_import", "k_advance"};
+enum { K_EXECUTE = 0, K_IMPORT, K_NUM };
+const char* kKernelNames[K_NUM] = {"k_execute", "k_import"};
 
 int launch_round(sgn_ctx* ctx);
 
@@ -2414,8 +2421,7 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
   ctx->graph_timed.clear();
   if (!all && !exec) return 0;
-  const void* fn[K_NUM] = {execute_fn(ctx->S.tkind), (const void*)k_import,
-                           (const void*)k_advance};
+  const void* fn[K_NUM] = {execute_fn(ctx->S.tkind), (const void*)k_import};
   size_t n = 0;
   SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
   std::vector<hipGraphNode_t> nodes(n);
@@ -2889,7 +2895,11 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   // lives on the device; kernels of rounds past the end return at once). On a single
   // shard a full batch is one hipGraph replay: the round's launches are captured once.
   const uint64_t batch = 32;
-  const bool graph = ctx->nranks == 1 && ctx->use_graph;
+  // multi-shard over RCCL too: the captured batch holds each round's k_execute, the grouped
+  // send/recv (RCCL records its kernels in the graph) and k_import, so a batch costs one
+  // launch instead of ~3 + 2·(n_ranks-1) host calls per round (SGN_GRAPH=0: eager rounds)
+  const bool graph = ctx->use_graph && (ctx->nranks == 1 || ctx->comm) &&
+                     !(getenv("SGN_GRAPH") && atoi(getenv("SGN_GRAPH")) == 0);
   if (ctx->nranks == 1 && ctx->persist_grid) {
     // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside)
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
@@ -3455,10 +3465,8 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
 // hooks used by comm.cpp
 namespace sgn {
 void launch_execute(sgn_ctx* ctx) { launch_k_execute(ctx, ctx->stream); }
+// k_import files the received runs and its last block advances the window
 void launch_import(sgn_ctx* ctx) {
-  hipLaunchKernelGGL(k_import, dim3(256), dim3(256), 0, ctx->stream, ctx->S);
-}
-void launch_advance(sgn_ctx* ctx) {
-  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, ctx->stream, ctx->S);
+  hipLaunchKernelGGL(k_import, dim3(kImportBlocks), dim3(256), 0, ctx->stream, ctx->S);
 }
 }  // namespace sgn

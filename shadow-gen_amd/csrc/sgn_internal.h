@@ -88,7 +88,7 @@ struct Ctrl {
   uint64_t round_min;     // atomicMin: next local event over owned hosts
   uint64_t min_used;      // Runahead::min_used_latency (atomicMin), INVALID = None
   uint32_t keep_slab;     // spare slab: receives the window's last bucket this round
-  uint32_t pad0;
+  uint32_t imp_done;      // multi-shard: k_import blocks finished this round (the last one advances)
   uint64_t keep_min;      // min time placed in the spare slab this round
   uint64_t last_min_next; // min_next_event_time of the last finished round
   uint64_t rounds;

@@ -1,0 +1,38 @@
+"""The multi-shard path over real RCCL on a one-GPU box.
+
+RCCL refuses two ranks on one device ("Duplicate GPU detected") unless they look like
+different hosts: `bench.py --one-gpu` gives every rank its own NCCL_HOSTID, so two processes
+on device 0 form a communicator whose exchange runs over RCCL's socket transport. Everything
+the N-GPU run does then executes for real: the sharded APSP (row blocks broadcast over RCCL,
+checked against a table built whole on every rank), per-round grouped ncclSend/ncclRecv of the
+exchange slots and messages, k_import with the window advance, the graph-captured round
+batches (or eager rounds with SGN_GRAPH=0), and bench's shard_check, which re-runs all hosts
+unsharded on rank 0 and compares every counter, the window and every host's digests bit for
+bit. Timing from this transport means nothing; the driver's multi-GPU bench measures xGMI.
+"""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+@pytest.mark.parametrize("graph,port", [("1", 29541), ("0", 29542)])
+def test_rccl_two_ranks_one_gpu_match_unsharded(graph, port):
+    env = dict(os.environ, SGN_GRAPH=graph, NCCL_DEBUG="WARN", TMPDIR="/tmp")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "20000", "--rounds-per-step", "70"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    assert line["apsp_sharded"]["equal_on_all_ranks"] is True
+    assert line["parity"] is True, line.get("parity_detail")
+    assert line["parity_detail"]["hosts_compared"] == 40_000
+    assert line["rounds_timed"] == 140
