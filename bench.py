@@ -514,6 +514,13 @@ def main():
         "engine": {k: info[k] for k in ("calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity",
                                         "persistent_grid", "persistent_fallbacks")},
     }
+    if world > 1:
+        # the round exchange: per-peer slot, runs per peer a round moves now
+        # (2x the largest per-peer count seen, a power of two), rounds held and completed with
+        # the whole slot, and bytes this rank sent to peers per round since sim_init
+        out["exchange"] = {"slot_runs": info["exchange_slot_runs"], "send_runs": info["exchange_send_runs"],
+                           "hwm_runs": info["exchange_hwm_runs"], "spills": info["exchange_spills"],
+                           "bytes_per_round": round(info["exchange_bytes"] / max(1, st1["rounds"]))}
     ws, we, act = ctx.window()
     out["sim_time_reached_ms"] = (ws - sgn.SIMULATION_START) / 1e6
     out["sim_ms_per_step"] = out["sim_time_reached_ms"] / (args.steps + args.warmup)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 5
+#define SGN_ABI_VERSION 6
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -412,6 +412,15 @@ typedef struct sgn_engine_info {
   uint64_t persistent_grid;     /* workgroups of the persistent round kernel (0: per-round) */
   uint64_t persistent_fallbacks;/* persistent launches refused by the residency census */
   uint64_t device_bytes;        /* device memory held by the simulation */
+  /* multi-shard round exchange (0 on one shard): per-peer slot capacity, runs per peer the
+   * current rounds' send/recv move (sized from the high-water mark; a round that needs more
+   * is held and completed with a full-slot exchange), the largest per-peer run count of any
+   * round so far, rounds completed that way, and bytes sent to peers since sim_init */
+  uint64_t exchange_slot_runs;
+  uint64_t exchange_send_runs;
+  uint64_t exchange_hwm_runs;
+  uint64_t exchange_spills;
+  uint64_t exchange_bytes;
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

@@ -153,6 +153,9 @@ void sgn_destroy(sgn_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  // a captured batch holds RCCL work of the communicator: release it first (RCCL keeps the
+  // communicator's captured resources alive until the graph is gone)
+  drop_graph(ctx);
   comm_destroy(ctx);
   delete ctx;
 }

@@ -73,21 +73,23 @@ int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES], uint64_t sl
 }  // extern "C"
 
 namespace sgn {
-int comm_round_exchange(sgn_ctx* ctx) {
-  // k_execute's last wave has already done the local round edge and written this shard's
-  // message for every peer (run count, local min next event incl. exported runs, local min
-  // used latency): ONE grouped send/recv moves runs and messages, then one kernel on every
-  // shard imports the runs and reduces the messages (no all-reduce, no memsets).
+int ctrl_sync(sgn_ctx* ctx);  // engine.hip: the control block to the host, overflow check
+
+uint64_t comm_round_bytes(const sgn_ctx* ctx) {
+  return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)ctx->xsz_cur * sizeof(EvRec) + 32) : 0;
+}
+
+// ONE grouped send/recv: the first sz runs of each peer's slot and the 32-byte message
+static int exchange(sgn_ctx* ctx, uint32_t sz) {
   DevSim& S = ctx->S;
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   hipStream_t st = ctx->stream;
-  const size_t slot_bytes = (size_t)S.xslot * sizeof(EvRec);
+  const size_t bytes = (size_t)sz * sizeof(EvRec);
   ncclResult_t r = ncclGroupStart();
   for (uint32_t p = 0; p < S.n_ranks && r == ncclSuccess; p++) {
     if (p == S.rank) continue;
-    r = ncclSend(S.xout + (size_t)p * S.xslot, slot_bytes, ncclUint8, (int)p, comm, st);
-    if (r == ncclSuccess)
-      r = ncclRecv(S.xin + (size_t)p * S.xslot, slot_bytes, ncclUint8, (int)p, comm, st);
+    r = ncclSend(S.xout + (size_t)p * S.xslot, bytes, ncclUint8, (int)p, comm, st);
+    if (r == ncclSuccess) r = ncclRecv(S.xin + (size_t)p * S.xslot, bytes, ncclUint8, (int)p, comm, st);
     if (r == ncclSuccess) r = ncclSend(S.xmsg_out + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
     if (r == ncclSuccess) r = ncclRecv(S.xmsg_in + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
   }
@@ -95,8 +97,42 @@ int comm_round_exchange(sgn_ctx* ctx) {
   if (r != ncclSuccess || r2 != ncclSuccess)
     return set_error(ctx, SGN_EDEVICE, std::string("RCCL exchange: ") +
                                            ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return 0;
+}
+
+int comm_round_exchange(sgn_ctx* ctx) {
+  // k_execute's last wave has already done the local round edge and written this shard's
+  // message for every peer (run count, local min next event incl. exported runs, local min
+  // used latency, its largest per-peer count): ONE grouped send/recv moves the first
+  // xsz_cur runs of every slot and the messages, then one kernel on every shard imports the
+  // runs and reduces the messages (no all-reduce, no memsets). xsz_cur follows the largest
+  // per-peer count seen (x2, a power of two), so a round moves about what it produced
+  // instead of the whole slot.
+  if (int rc = exchange(ctx, ctx->xsz_cur)) return rc;
+  if (!ctx->capturing) ctx->x_bytes += comm_round_bytes(ctx);
   launch_import(ctx);
   return 0;
+}
+
+// A round some shard produced more than xsz_cur runs for a peer in was held by k_import on
+// every shard (each compares the same maxima). The send/recv of the rounds after it in the
+// batch moved the same slots again and their kernels returned at once. Complete it: the
+// whole slots, k_import again (which advances the window), and a larger exchange size.
+int comm_complete_spill(sgn_ctx* ctx) {
+  DevSim& S = ctx->S;
+  hipStream_t st = ctx->stream;
+  SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xsz, (int)S.xslot, 1, st));
+  SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xspill, 0, 1, st));
+  if (int rc = exchange(ctx, S.xslot)) return rc;
+  ctx->x_bytes += (uint64_t)(ctx->nranks - 1) * ((uint64_t)S.xslot * sizeof(EvRec) + 32);
+  launch_import(ctx);
+  uint64_t want = std::max<uint64_t>(2 * ctx->h_ctrl->xhwm, kXszInit);
+  uint64_t sz = kXszInit;
+  while (sz < want) sz <<= 1;
+  ctx->xsz_cur = (uint32_t)std::min<uint64_t>(sz, S.xslot);
+  SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xsz, (int)ctx->xsz_cur, 1, st));
+  ctx->x_spills++;
+  return ctrl_sync(ctx);
 }
 
 // Sharded APSP (routes.hip): every shard owns a contiguous block of rows (row tiles of the

@@ -1502,13 +1502,20 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     m = nb1 < m ? nb1 : m;
     m = wn < m ? wn : m;
     if (local) {
+      // word 3: this shard's largest per-peer run count this round (every shard compares the
+      // maxima of all shards with the exchange size: the same decision everywhere)
+      uint64_t xmax = 0;
+      for (uint32_t p = 0; p < S.n_ranks; p++) {
+        const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
+        xmax = cnt > xmax ? cnt : xmax;
+      }
       for (uint32_t p = 0; p < S.n_ranks; p++) {
         const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
         SGN_GLB uint64_t* o = (p == S.rank ? S.xmsg_in : S.xmsg_out) + 4 * (size_t)p;
         st_dev(o, cnt);
         st_dev(o + 1, m);
         st_dev(o + 2, mu);
-        st_dev(o + 3, (uint64_t)0);
+        st_dev(o + 3, xmax);
       }
       return;
     }
@@ -1881,7 +1888,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   // kernel argument would pin ~90 scalar registers for the whole kernel)
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
-  if (!C->active) return;
+  if (!C->active || C->xspill) return;  // multi-shard: a held round waits for the host
   SGN_EXEC_LDS(X)
   const uint64_t ws = C->ws, we = C->we;
   const uint32_t ks = C->keep_slab;
@@ -2184,10 +2191,23 @@ __device__ __forceinline__ void advance_window(const DevSim& S, Ctrl* C) {
 constexpr uint32_t kImportBlocks = 128;
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
-  if (!C->active) return;  // every block reads the same value: nothing changes it before all count in
+  // every block reads the same values: nothing changes them before all blocks count in
+  if (!C->active || C->xspill) return;
+  // The send/recv moved the first C->xsz runs of each slot. If any shard had more for some
+  // peer (the messages carry every shard's maximum), the round is held on every shard alike:
+  // nothing is imported, the window stays, and the host completes the round with a
+  // full-slot exchange and this kernel again (comm_complete_spill). Counts above the slot
+  // itself are an overflow the sender already reported.
+  uint64_t gm = 0;
+  for (uint32_t r = 0; r < S.n_ranks; r++) {
+    const uint64_t x = S.xmsg_in[4 * (size_t)r + 3];
+    gm = x > gm ? x : gm;
+  }
+  const uint32_t sz = C->xsz;
+  const bool hold = gm > sz && sz < S.xslot;
   // the window that just ran (still C->ws): the same horizon as sends
   const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
-  for (uint32_t r = 0; r < S.n_ranks; r++) {
+  for (uint32_t r = 0; r < S.n_ranks && !hold; r++) {
     if (r == S.rank) continue;
     const uint32_t n = (uint32_t)min(S.xmsg_in[4 * (size_t)r], (uint64_t)S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -2213,6 +2233,11 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   __syncthreads();
   if (!last || threadIdx.x != 0) return;
   C->imp_done = 0;
+  if (gm > C->xhwm) C->xhwm = gm;
+  if (hold) {
+    C->xspill = 1;
+    return;
+  }
   advance_window(S, C);
 }
 
@@ -2513,14 +2538,21 @@ void time_collect(sgn_ctx* ctx) {
   ctx->ev_next = 0;
 }
 
-void free_sim(sgn_ctx* ctx) {
+int ctrl_sync(sgn_ctx* ctx) { return sync_ctrl(ctx); }
+
+void drop_graph(sgn_ctx* ctx) {
   if (ctx->gexec) hipGraphExecDestroy(ctx->gexec);
   if (ctx->graph) hipGraphDestroy(ctx->graph);
   ctx->gexec = nullptr;
   ctx->graph = nullptr;
   ctx->gbatch = 0;
+  ctx->gsz = 0;
   ctx->graph_timed.clear();
   ctx->graph_pending = false;
+}
+
+void free_sim(sgn_ctx* ctx) {
+  drop_graph(ctx);
   for (void* p : ctx->allocs) hipFree(p);
   ctx->allocs.clear();
   ctx->sim_bytes = 0;
@@ -2806,6 +2838,17 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
   c.prev_we = SIM_START;
+  // multi-shard exchange size: RCCL rounds start at min(slot, kXszInit) runs per peer and
+  // grow with the high-water mark; a local shard group copies counts, so it uses the slot
+  ctx->xsz_cur = ctx->nranks > 1 ? (ctx->comm_local ? (uint32_t)ctx->xslot
+                                                    : (uint32_t)std::min<uint64_t>(ctx->xslot, kXszInit))
+                                 : 0;
+  // test hook: a small first size makes the first rounds hold and complete (spill path)
+  if (const char* e = getenv("SGN_XSZ_INIT"))
+    if (ctx->nranks > 1 && !ctx->comm_local)
+      ctx->xsz_cur = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ctx->xslot, (uint64_t)atoll(e)));
+  ctx->x_spills = ctx->x_bytes = 0;
+  c.xsz = ctx->xsz_cur;
   S.ctrl = (decltype(S.ctrl))dalloc<Ctrl>(ctx, 1);
   if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
@@ -2879,6 +2922,7 @@ int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
   if (!ctx->h_ctrl->active) return set_error(ctx, SGN_ESTATE, "simulation already finished");
   if ((rc = launch_round(ctx))) return rc;
   rc = sync_ctrl(ctx);
+  if (!rc && ctx->h_ctrl->xspill) rc = comm_complete_spill(ctx);
   if (min_next) *min_next = ctx->h_ctrl->last_min_next;
   return rc;
 }
@@ -2930,9 +2974,18 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
     return 0;
   }
-  while (ctx->h_ctrl->active && enq < max_rounds) {
-    const uint64_t n = std::min<uint64_t>(batch, max_rounds - enq);
+  // rounds are counted as they complete: a multi-shard round held for a full-slot exchange
+  // (comm_complete_spill) turns the rest of its batch into no-ops, which are not rounds
+  uint64_t done = 0;
+  static const bool dbg = getenv("SGN_DEBUG_RUN") != nullptr;
+  while (ctx->h_ctrl->active && done < max_rounds) {
+    const uint64_t n = std::min<uint64_t>(batch, max_rounds - done);
+    if (dbg)
+      fprintf(stderr, "[sgn r%u] batch n=%llu done=%llu graph=%d gexec=%d gsz=%u xsz=%u spills=%llu\n", ctx->rank,
+              (unsigned long long)n, (unsigned long long)done, (int)graph, ctx->gexec != nullptr, ctx->gsz,
+              ctx->xsz_cur, (unsigned long long)ctx->x_spills);
     if (graph && n == batch) {
+      if (ctx->gexec && ctx->gsz != ctx->xsz_cur) drop_graph(ctx);  // the send size changed
       if (!ctx->gexec) {
         ctx->ev_pending.clear();
         ctx->ev_next = 0;
@@ -2949,15 +3002,24 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
         if ((rc = add_timing_nodes(ctx, g))) return rc;
         SGN_HIP(ctx, hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0));
         ctx->gbatch = batch;
+        ctx->gsz = ctx->xsz_cur;
       }
       SGN_HIP(ctx, hipGraphLaunch(ctx->gexec, ctx->stream));
       ctx->graph_pending = !ctx->graph_timed.empty();
+      ctx->x_bytes += n * comm_round_bytes(ctx);
     } else {
       for (uint64_t i = 0; i < n; i++)
         if ((rc = launch_round(ctx))) return rc;
     }
-    enq += n;
     if ((rc = sync_ctrl(ctx))) return rc;
+    if (dbg)
+      fprintf(stderr, "[sgn r%u] synced rounds=%llu spill=%u hwm=%llu\n", ctx->rank,
+              (unsigned long long)(ctx->h_ctrl->rounds - r_start), ctx->h_ctrl->xspill,
+              (unsigned long long)ctx->h_ctrl->xhwm);
+    if (ctx->h_ctrl->xspill && (rc = comm_complete_spill(ctx))) return rc;
+    if (dbg && ctx->h_ctrl->xspill == 0) fprintf(stderr, "[sgn r%u] after: rounds=%llu\n", ctx->rank,
+                                                 (unsigned long long)(ctx->h_ctrl->rounds - r_start));
+    done = ctx->h_ctrl->rounds - r_start;
   }
   if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
   return 0;
@@ -3112,6 +3174,11 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   out->persistent_grid = ctx->persist_grid;
   out->persistent_fallbacks = ctx->persist_fallbacks;
   out->device_bytes = ctx->sim_bytes;
+  out->exchange_slot_runs = ctx->nranks > 1 ? ctx->xslot : 0;
+  out->exchange_send_runs = ctx->xsz_cur;
+  out->exchange_hwm_runs = ctx->h_ctrl ? ctx->h_ctrl->xhwm : 0;
+  out->exchange_spills = ctx->x_spills;
+  out->exchange_bytes = ctx->x_bytes;
   return 0;
 }
 

@@ -102,6 +102,12 @@ struct Ctrl {
   // workgroups that started, and the verdict (1 = whole grid resident, 2 = not: every
   // workgroup left before touching simulation state; the host falls back to k_execute)
   uint32_t res_arrive, res_verdict;
+  // multi-shard exchange sizing: runs per peer the round's RCCL send/recv moves (set by the
+  // host per batch; a slot holds up to xslot), 1 while a round is held because some shard
+  // had more runs for a peer than that (the host completes it with a full-slot exchange),
+  // and the largest per-peer run count any shard produced in a round so far
+  uint32_t xsz, xspill;
+  uint64_t xhwm;
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -375,6 +381,9 @@ struct sgn_ctx {
   bool comm_local = false;           // local shard group (sgn_comm_init_local)
   std::vector<sgn_ctx*> group;       // ... its contexts, shard order
   uint64_t xslot = 0;
+  uint32_t xsz_cur = 0;    // runs per peer the current rounds' send/recv move (<= xslot)
+  uint64_t x_spills = 0;   // rounds completed by a full-slot exchange
+  uint64_t x_bytes = 0;    // bytes sent to peers by the round exchange (runs + messages)
 
   // kernel timing
   struct KT {
@@ -391,6 +400,7 @@ struct sgn_ctx {
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
   uint64_t gbatch = 0;
+  uint32_t gsz = 0;        // multi-shard: the exchange size the captured batch sends
   std::vector<std::pair<int, size_t>> graph_timed;
   bool graph_pending = false;
   bool use_graph = true;
@@ -406,6 +416,12 @@ int set_error(sgn_ctx* ctx, int code, const std::string& msg);
 int hip_fail(sgn_ctx* ctx, hipError_t e, const char* what);
 void* dev_alloc(sgn_ctx* ctx, size_t bytes, bool zero = true);
 void free_sim(sgn_ctx* ctx);
+void drop_graph(sgn_ctx* ctx);  // the captured batch of rounds, if any
+// multi-shard exchange (comm.cpp): runs per peer the first RCCL rounds move; bytes one
+// round sends to peers; completion of a held round with a full-slot exchange
+constexpr uint32_t kXszInit = 512;
+uint64_t comm_round_bytes(const sgn_ctx* ctx);
+int comm_complete_spill(sgn_ctx* ctx);
 int ensure_host_routes(sgn_ctx* ctx);
 // timing helpers around a launch
 void time_begin(sgn_ctx* ctx, int kernel);

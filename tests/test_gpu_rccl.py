@@ -22,9 +22,13 @@ pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
-@pytest.mark.parametrize("graph,port", [("1", 29541), ("0", 29542)])
-def test_rccl_two_ranks_one_gpu_match_unsharded(graph, port):
+# xsz: the exchange size the first rounds move per peer (SGN_XSZ_INIT); 16 runs make the
+# early rounds exceed it, so they are held and completed with the whole slot (spill path)
+@pytest.mark.parametrize("graph,xsz,port", [("1", "", 29541), ("0", "", 29542), ("1", "16", 29543)])
+def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port):
     env = dict(os.environ, SGN_GRAPH=graph, NCCL_DEBUG="WARN", TMPDIR="/tmp")
+    if xsz:
+        env["SGN_XSZ_INIT"] = xsz
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "20000", "--rounds-per-step", "70"]
@@ -36,3 +40,7 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, port):
     assert line["parity"] is True, line.get("parity_detail")
     assert line["parity_detail"]["hosts_compared"] == 40_000
     assert line["rounds_timed"] == 140
+    x = line["exchange"]
+    assert x["hwm_runs"] > 0 and x["send_runs"] >= min(x["slot_runs"], x["hwm_runs"])
+    if xsz:
+        assert x["spills"] >= 1
