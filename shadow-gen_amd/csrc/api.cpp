@@ -140,6 +140,8 @@ int sgn_create(sgn_ctx** out, const sgn_create_opts* opts) {
   c->rank = o.shard_rank;
   c->nranks = o.shard_count;
   c->flags = o.flags;
+  // experiment hook: no HIP-event timing at all (graph batches without event-record nodes)
+  if (getenv("SGN_NO_TIMING")) c->flags &= ~(uint32_t)(SGN_CREATE_TIME_KERNELS | SGN_CREATE_TIME_EXECUTE);
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     g_create_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     delete c;

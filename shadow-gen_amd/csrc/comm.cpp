@@ -76,22 +76,23 @@ namespace sgn {
 int ctrl_sync(sgn_ctx* ctx);  // engine.hip: the control block to the host, overflow check
 
 uint64_t comm_round_bytes(const sgn_ctx* ctx) {
-  return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)ctx->xsz_cur * sizeof(EvRec) + 32) : 0;
+  return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)(1 + ctx->xsz_cur) * sizeof(EvRec)) : 0;
 }
 
-// ONE grouped send/recv: the first sz runs of each peer's slot and the 32-byte message
+// ONE grouped send/recv: per peer one message of the 32-byte round-edge record and the first
+// sz runs of its slot (one send and one receive per peer)
 static int exchange(sgn_ctx* ctx, uint32_t sz) {
   DevSim& S = ctx->S;
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   hipStream_t st = ctx->stream;
-  const size_t bytes = (size_t)sz * sizeof(EvRec);
+  // a peer's block: the message (one 32-byte record), then the runs
+  const size_t bytes = (size_t)(1 + sz) * sizeof(EvRec);
+  const size_t blk = (size_t)S.xslot + 1;
   ncclResult_t r = ncclGroupStart();
   for (uint32_t p = 0; p < S.n_ranks && r == ncclSuccess; p++) {
     if (p == S.rank) continue;
-    r = ncclSend(S.xout + (size_t)p * S.xslot, bytes, ncclUint8, (int)p, comm, st);
-    if (r == ncclSuccess) r = ncclRecv(S.xin + (size_t)p * S.xslot, bytes, ncclUint8, (int)p, comm, st);
-    if (r == ncclSuccess) r = ncclSend(S.xmsg_out + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
-    if (r == ncclSuccess) r = ncclRecv(S.xmsg_in + 4 * (size_t)p, 4, ncclUint64, (int)p, comm, st);
+    r = ncclSend(S.xout + p * blk, bytes, ncclUint8, (int)p, comm, st);
+    if (r == ncclSuccess) r = ncclRecv(S.xin + p * blk, bytes, ncclUint8, (int)p, comm, st);
   }
   ncclResult_t r2 = ncclGroupEnd();
   if (r != ncclSuccess || r2 != ncclSuccess)
@@ -124,7 +125,7 @@ int comm_complete_spill(sgn_ctx* ctx) {
   SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xsz, (int)S.xslot, 1, st));
   SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xspill, 0, 1, st));
   if (int rc = exchange(ctx, S.xslot)) return rc;
-  ctx->x_bytes += (uint64_t)(ctx->nranks - 1) * ((uint64_t)S.xslot * sizeof(EvRec) + 32);
+  ctx->x_bytes += (uint64_t)(ctx->nranks - 1) * ((uint64_t)(1 + S.xslot) * sizeof(EvRec));
   launch_import(ctx);
   uint64_t want = std::max<uint64_t>(2 * ctx->h_ctrl->xhwm, kXszInit);
   uint64_t sz = kXszInit;
@@ -224,18 +225,15 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
     // message b (what comm_round_exchange's grouped send/recv does)
     for (uint32_t a = 0; a < n; a++) {
       sgn_ctx* A = ctxs[a];
-      std::vector<uint64_t> msg((size_t)n * 4);
-      SGN_HIP(A, hipMemcpy(msg.data(), (const void*)A->S.xmsg_out, msg.size() * 8, hipMemcpyDeviceToHost));
+      const size_t blk = (size_t)A->S.xslot + 1;
       for (uint32_t b = 0; b < n; b++) {
         if (b == a) continue;
         sgn_ctx* B = ctxs[b];
-        const uint64_t k = std::min<uint64_t>(msg[4 * (size_t)b], A->xslot);
-        if (k)
-          SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * B->S.xslot),
-                               (const void*)(A->S.xout + (size_t)b * A->S.xslot),
-                               (size_t)k * sizeof(EvRec), hipMemcpyDefault));
-        SGN_HIP(B, hipMemcpy((void*)(B->S.xmsg_in + 4 * (size_t)a), &msg[4 * (size_t)b], 32,
-                             hipMemcpyHostToDevice));
+        uint64_t msg[4];
+        SGN_HIP(A, hipMemcpy(msg, (const void*)(A->S.xout + (size_t)b * blk), 32, hipMemcpyDeviceToHost));
+        const uint64_t k = std::min<uint64_t>(msg[0], A->xslot);
+        SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * blk), (const void*)(A->S.xout + (size_t)b * blk),
+                             (size_t)(1 + k) * sizeof(EvRec), hipMemcpyDefault));
       }
     }
     for (uint32_t i = 0; i < n; i++) {

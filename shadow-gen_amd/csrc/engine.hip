@@ -1132,7 +1132,7 @@ struct HostExec {
       }
       atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
       pos = atomicAdd(&S.xout_n[lo], nrec);
-      dstp = S.xout + (size_t)lo * S.xslot;
+      dstp = S.xout + (size_t)lo * (S.xslot + 1) + 1;  // record 0 of a peer's block: the message
       cap = S.xslot;
     }
     if (pos + nrec > cap) {
@@ -1511,7 +1511,9 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
       }
       for (uint32_t p = 0; p < S.n_ranks; p++) {
         const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
-        SGN_GLB uint64_t* o = (p == S.rank ? S.xmsg_in : S.xmsg_out) + 4 * (size_t)p;
+        // record 0 of the peer's outgoing block (travels with the runs); this shard's own in
+        // its incoming block, where k_import reads every shard's message
+        SGN_GLB uint64_t* o = (SGN_GLB uint64_t*)((p == S.rank ? S.xin : S.xout) + (size_t)p * (S.xslot + 1));
         st_dev(o, cnt);
         st_dev(o + 1, m);
         st_dev(o + 2, mu);
@@ -2166,7 +2168,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 __device__ __forceinline__ void advance_window(const DevSim& S, Ctrl* C) {
   uint64_t m = INVALID, mu = INVALID;
   for (uint32_t p = 0; p < S.n_ranks; p++) {
-    const uint64_t a = S.xmsg_in[4 * (size_t)p + 1], b = S.xmsg_in[4 * (size_t)p + 2];
+    const uint64_t* msg = (const uint64_t*)(S.xin + (size_t)p * (S.xslot + 1));
+    const uint64_t a = msg[1], b = msg[2];
     m = a < m ? a : m;
     mu = b < mu ? b : mu;
     S.xout_n[p] = 0;  // the next round's sends count from zero
@@ -2200,7 +2203,7 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   // itself are an overflow the sender already reported.
   uint64_t gm = 0;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
-    const uint64_t x = S.xmsg_in[4 * (size_t)r + 3];
+    const uint64_t x = ((const uint64_t*)(S.xin + (size_t)r * (S.xslot + 1)))[3];
     gm = x > gm ? x : gm;
   }
   const uint32_t sz = C->xsz;
@@ -2209,10 +2212,11 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
   for (uint32_t r = 0; r < S.n_ranks && !hold; r++) {
     if (r == S.rank) continue;
-    const uint32_t n = (uint32_t)min(S.xmsg_in[4 * (size_t)r], (uint64_t)S.xslot);
+    const EvRec* blk = S.xin + (size_t)r * (S.xslot + 1);  // message, then the runs
+    const uint32_t n = (uint32_t)min(((const uint64_t*)blk)[0], (uint64_t)S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
-      const EvRec e = S.xin[(size_t)r * S.xslot + i];
+      const EvRec e = blk[1 + i];
       if (e.time >= hz) {
         if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = e.dst;
         continue;
@@ -2352,6 +2356,7 @@ int launch_round(sgn_ctx* ctx);
 // dynamic LDS of k_execute / k_rounds: CAP event runs + two u16 index arrays
 inline size_t exec_lds_bytes(uint32_t cap) { return (size_t)cap * (sizeof(EvRec) + 4); }
 constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then a host sync)
+constexpr uint64_t kTimeEvery = 8;        // per-round launches: one timed in kTimeEvery
 
 }  // namespace
 
@@ -2399,9 +2404,13 @@ int launch_round(sgn_ctx* ctx) {
   if (ctx->nranks > 1 && !ctx->comm)
     return set_error(ctx, SGN_ESTATE, "multi-shard round without an RCCL communicator");
   hipStream_t st = ctx->stream;
-  time_begin(ctx, K_EXECUTE);
+  // per-round launches time one round in kTimeEvery: an event record is a barrier packet
+  // with a cache write-back, and around every launch it cost 20 % of the rounds (eager) or
+  // 45 % (graph batches) on config C; a sample gives the kernel's average duration
+  const bool timed = ctx->capturing || (ctx->t_seq++ % kTimeEvery) == 0;
+  if (timed) time_begin(ctx, K_EXECUTE);
   launch_k_execute(ctx, st);
-  time_end(ctx);
+  if (timed) time_end(ctx);
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
     int rc = comm_round_exchange(ctx);
@@ -2452,6 +2461,7 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   std::vector<hipGraphNode_t> nodes(n);
   SGN_HIP(ctx, hipGraphGetNodes(g, nodes.data(), &n));
   size_t ev = 0;
+  uint32_t tseen[K_NUM] = {};
   for (hipGraphNode_t node : nodes) {
     hipGraphNodeType t;
     SGN_HIP(ctx, hipGraphNodeGetType(node, &t));
@@ -2462,6 +2472,7 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
     for (int k = 0; k < K_NUM; k++)
       if (p.func == fn[k]) kid = k;
     if (kid < 0 || (!all && kid != K_EXECUTE)) continue;
+    if ((tseen[kid]++ % kTimeEvery) != 0) continue;  // a sample (launch_round's note)
     if (ev >= ctx->ev_pool.size()) {
       hipEvent_t a, b;
       SGN_HIP(ctx, hipEventCreate(&a));
@@ -2819,13 +2830,11 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     if (!ctx->comm && !ctx->comm_local)
       return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init (or sgn_comm_init_local) before sgn_sim_init");
     S.xslot = (uint32_t)ctx->xslot;
-    S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
-    S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * ctx->xslot);
+    // per peer a block of 1 + xslot records: the 32-byte round-edge message, then the runs
+    S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + 1));
+    S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + 1));
     S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
-    S.xmsg_out = (decltype(S.xmsg_out))dalloc<uint64_t>(ctx, ctx->nranks * 4);
-    S.xmsg_in = (decltype(S.xmsg_in))dalloc<uint64_t>(ctx, ctx->nranks * 4);
-    if (!S.xmsg_out || !S.xmsg_in) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
   }
   Ctrl c{};
@@ -2939,11 +2948,14 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   // lives on the device; kernels of rounds past the end return at once). On a single
   // shard a full batch is one hipGraph replay: the round's launches are captured once.
   const uint64_t batch = 32;
-  // multi-shard over RCCL too: the captured batch holds each round's k_execute, the grouped
-  // send/recv (RCCL records its kernels in the graph) and k_import, so a batch costs one
-  // launch instead of ~3 + 2·(n_ranks-1) host calls per round (SGN_GRAPH=0: eager rounds)
+  // SGN_GRAPH=1: a full batch is captured once as a hipGraph and replayed (multi-shard over
+  // RCCL too: each round's k_execute, the grouped send/recv — RCCL records its kernels in the
+  // graph — and k_import). Off by default: measured on config C with per-round launches,
+  // replays are no faster than eager launches (38.9 vs 38.9 us per round untimed), and the
+  // event-record nodes that time a sample of the rounds slow the replay (1.35 vs 1.47 G
+  // packet events/s); the host enqueues eager rounds faster than the GPU runs them.
   const bool graph = ctx->use_graph && (ctx->nranks == 1 || ctx->comm) &&
-                     !(getenv("SGN_GRAPH") && atoi(getenv("SGN_GRAPH")) == 0);
+                     getenv("SGN_GRAPH") && atoi(getenv("SGN_GRAPH")) == 1;
   if (ctx->nranks == 1 && ctx->persist_grid) {
     // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside)
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {

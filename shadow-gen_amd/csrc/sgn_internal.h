@@ -296,16 +296,16 @@ struct DevSim {
   // EXTERNAL traffic: interface deliveries and drops for the CPU-side applications
   SGN_GLB sgn_drain_rec* drain;
   uint64_t drain_cap;
-  // multi-GPU exchange: out slot r holds events for rank r
+  // multi-GPU exchange: xout block r (1 + xslot records) goes to rank r, xin block r came
+  // from it. Record 0 of a block is the round-edge message, 4 u64: {runs sent to that peer,
+  // the sender's min next event (incl. the runs it exported this round), its min used
+  // latency, its largest per-peer run count}; runs follow from record 1. This shard's own
+  // message is record 0 of its own xin block.
   SGN_GLB EvRec* xout;
-  SGN_GLB uint32_t* xout_n;  // [n_ranks]
+  SGN_GLB uint32_t* xout_n;  // [n_ranks] runs appended per peer this round
   SGN_GLB EvRec* xin;
-  SGN_GLB uint32_t* xin_n;   // [n_ranks] (received counts)
-  // round-edge messages, 4 u64 per peer: {runs sent to it, local min next event (incl. the
-  // runs exported this round), local min used latency, 0}; xmsg_in[rank] is this shard's own
-  SGN_GLB uint64_t* xmsg_out;  // [n_ranks * 4]
-  SGN_GLB uint64_t* xmsg_in;   // [n_ranks * 4]
-  uint32_t xslot;    // events per slot
+  SGN_GLB uint32_t* xin_n;   // (unused)
+  uint32_t xslot;    // run capacity per peer block
   uint32_t rank;
   SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
@@ -395,6 +395,7 @@ struct sgn_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<std::pair<int, size_t>> ev_pending;  // (kernel, pool index)
   size_t ev_next = 0;
+  uint64_t t_seq = 0;  // per-round launches so far (a sample of them is timed)
 
   // a batch of rounds captured once as a hipGraph and replayed (single shard)
   hipGraph_t graph = nullptr;

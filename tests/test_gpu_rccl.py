@@ -6,7 +6,7 @@ on device 0 form a communicator whose exchange runs over RCCL's socket transport
 the N-GPU run does then executes for real: the sharded APSP (row blocks broadcast over RCCL,
 checked against a table built whole on every rank), per-round grouped ncclSend/ncclRecv of the
 exchange slots and messages, k_import with the window advance, the graph-captured round
-batches (or eager rounds with SGN_GRAPH=0), and bench's shard_check, which re-runs all hosts
+batches (SGN_GRAPH=1) or eager rounds (the default), and bench's shard_check, which re-runs all hosts
 unsharded on rank 0 and compares every counter, the window and every host's digests bit for
 bit. Timing from this transport means nothing; the driver's multi-GPU bench measures xGMI.
 """
