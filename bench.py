@@ -53,7 +53,7 @@ def build_workload(n_hosts, V, seed=1):
                           req_payload=64, servers=servers,
                           file_bytes=(50 * 1024, 1024 * 1024, 5 * 1024 * 1024))
     cfg = sgn.make_config(3600 * 1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64,
-                          codel_cap=4096, event_capacity=1 << 24)
+                          codel_cap=64, event_capacity=1 << 24)
     return g, used, hosts, cfg, tr
 
 
@@ -68,7 +68,7 @@ def build_workload_b(n_hosts, V, seed=1):
     hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), (np.arange(n_hosts) % V).astype(np.uint32), bw, bw, seeds)
     tr = sgn.make_traffic(sgn.TRAFFIC_PERIODIC, flow_seed=7, period_ns=10_000_000,
                           start_jitter_ns=10_000_000, payload_len=1024, unknown_dst_permille=1)
-    cfg = sgn.make_config(10_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64, codel_cap=4096,
+    cfg = sgn.make_config(10_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64, codel_cap=64,
                           event_capacity=1 << 22)
     return g, used, hosts, cfg, tr
 
@@ -382,7 +382,9 @@ def main():
         # per-peer exchange slot: capacity 8192 event runs per round; a round moves only the
         # high-water size (2x the largest per-peer count seen), ~700-1800 runs per
         # peer at 100k hosts per GPU (overflow of the slot is detected and reported)
-        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 13))
+        # D (every host sends every 1 ms, 7/8 of it to other shards): ~1e6 x 7/8 / 7 runs per
+        # peer per round at 1M hosts per GPU, so its slot holds 2^18 runs (8 MB per peer)
+        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 18 if args.workload == "D" else 1 << 13))
     # with the communicator set, the APSP build is sharded: each GPU computes its block of
     # used sources and the blocks are exchanged over RCCL
     ctx.routes_build(g, used)
@@ -517,7 +519,8 @@ def main():
         "max_slab_fill": st1["max_pending_events"],
         "hbm_footprint_bytes": info["device_bytes"],
         "engine": {k: info[k] for k in ("calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity",
-                                        "persistent_grid", "persistent_fallbacks")},
+                                        "persistent_grid", "persistent_fallbacks", "codel_pages",
+                                        "codel_page_allocs")},
     }
     if world > 1:
         # the round exchange: per-peer slot, runs per peer a round moves now

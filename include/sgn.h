@@ -165,8 +165,11 @@ typedef struct sgn_sim_config {
   uint64_t runahead_ns;         /* experimental.runahead; 0 = None (runahead.rs:55) */
   int32_t use_dynamic_runahead; /* experimental.use_dynamic_runahead (runahead.rs:61-67) */
   uint32_t out_fifo_cap;        /* synthetic socket send-queue entries per host (>= 1) */
-  uint32_t codel_cap;           /* device CoDel ring slots per host (reference: unlimited;
-                                   exceeding it is SGN_EOVERFLOW, never a silent drop) */
+  uint32_t codel_cap;           /* device CoDel run slots per host ON AVERAGE (reference:
+                                   unlimited): the queues are chains of 16-run pages from one
+                                   pool of max(hosts + 64, hosts * codel_cap / 16) pages, so any
+                                   host may hold far more; exhausting the pool is
+                                   SGN_EOVERFLOW, never a silent drop */
   uint32_t hosts_per_wave;      /* hosts served by one 64-lane execute wave: a power of two
                                    in [1, 64]; 0 = default (64). Performance only. */
   uint64_t event_capacity;      /* in-flight packet-event slots per shard (0 = auto) */
@@ -421,6 +424,13 @@ typedef struct sgn_engine_info {
   uint64_t exchange_hwm_runs;
   uint64_t exchange_spills;
   uint64_t exchange_bytes;
+  /* CoDel queues: pages of 16 runs in the shared pool (codel_cap slots per host on average,
+   * at least one page per host), and pages taken from its free ring so far */
+  uint64_t codel_pages;
+  uint64_t codel_page_allocs;
+  uint64_t codel_pages_free;     /* pages in the free ring now */
+  uint64_t codel_pages_chained;  /* pages in the hosts' queue chains now (read from the host
+                                    records: free + chained == codel_pages, no page lost) */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

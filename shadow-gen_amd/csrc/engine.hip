@@ -163,6 +163,29 @@ __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
   st_dev(q + 3, (uint64_t)r.pc | ((uint64_t)r.tag << 32));
 }
 
+// CoDel pool entries: a page serves other hosts (other workgroups, other XCDs) after it is
+// freed, so its entries are written through and read from memory like other cross-workgroup
+// data (a dirty L2 line of the previous owner must never overwrite the new owner's runs)
+__device__ __forceinline__ CodelEnt ld_dev_cq(SGN_GLB const CodelEnt* p) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  CodelEnt e;
+  e.enqueue_ts = ld_dev(q);
+  e.eid = ld_dev(q + 1);
+  const uint64_t a = ld_dev(q + 2), b = ld_dev(q + 3);
+  e.src = (uint32_t)a;
+  e.payload = (uint32_t)(a >> 32);
+  e.tag = (uint32_t)b;
+  e.count = (uint32_t)(b >> 32);
+  return e;
+}
+__device__ __forceinline__ void st_dev_cq(SGN_GLB CodelEnt* p, const CodelEnt& e) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  st_dev(q, e.enqueue_ts);
+  st_dev(q + 1, e.eid);
+  st_dev(q + 2, (uint64_t)e.src | ((uint64_t)e.payload << 32));
+  st_dev(q + 3, (uint64_t)e.tag | ((uint64_t)e.count << 32));
+}
+
 // device-scope atomic min whose result is not used: the wave does not wait for it here (a
 // returning one costs a round trip per call); the arrival's s_waitcnt vmcnt(0) completes it
 // before the round edge reads the minima
@@ -259,6 +282,8 @@ struct Outbox {
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
   uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
   SGN_GLB uint64_t* keepmin;  // minimum of this round's new runs for the window's last bucket
+  uint64_t pg_avail;          // CoDel page pool: free-ring entries allocations may use this round
+  SGN_GLB uint64_t* pg_freed; // ... and the round's freed-page counter
 };
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
@@ -281,7 +306,7 @@ struct LaneLDS {
   uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
   uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
   uint32_t rc_sid;   // ... whose slot id is this
-  uint32_t pad;
+  uint32_t cq_tp;    // CoDel chain's tail page
 };
 
 // kTrace: the per-packet trace can be on (k_execute). The persistent k_rounds is built
@@ -304,7 +329,7 @@ struct HostExec {
   uint32_t ri_src, ri_pay, ri_tag;
   uint64_t ri_eid;
   uint64_t tbb0, tbl0, tbb1, tbl1;  // balances / last refills (capacity, increment: memory)
-  uint32_t cq_head, cq_nr, cq_len;  // head run slot, runs in the ring, packets queued
+  uint32_t cq_head, cq_nr, cq_len;  // head run's pool index (page * CQ_PAGE + offset), runs, packets queued
   uint64_t cq_bytes;  // (CoDel drop state: the lane's LDS slot)
   uint32_t fq_head, fq_len;
   // per-round counter increments (a host cannot see 2^32 events in one window)
@@ -359,6 +384,7 @@ struct HostExec {
     tbb1 = r.tb_bal[1];
     tbl1 = r.tb_last[1];
     cq_head = r.cq_head;
+    L->cq_tp = r.cq_tp;
     cq_nr = r.cq_nr;
     cq_len = r.cq_len;
     cq_bytes = r.cq_bytes;
@@ -385,7 +411,7 @@ struct HostExec {
     c_maxcodel = r.max_codel;
     hd_valid = tl_open = false;
     if (cq_nr > 0) {
-      L->hd = *cq_slot(0);
+      L->hd = ld_dev_cq(cq_head_slot());
       hd_valid = true;
     }
     L->fh_idx = NO_HOST;
@@ -433,6 +459,7 @@ struct HostExec {
     r.ri_pay = ri_pay;
     r.ri_tag = ri_tag;
     r.cq_head = cq_head;
+    r.cq_tp = L->cq_tp;
     r.cq_nr = cq_nr;
     r.cq_len = cq_len;
     r.fq_head = fq_head;
@@ -449,8 +476,8 @@ struct HostExec {
     r.cq_prev = L->cq[3];
     r.app_k = L->app_k;
     S.nextloc[h] = next_local_time();
-    if (hd_valid) *cq_slot(0) = L->hd;
-    if (tl_open) *cq_slot(cq_nr - 1) = L->tl;
+    if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
+    if (tl_open) st_dev_cq(cq_tail_slot(), L->tl);
   }
 
   // rare counters go straight to memory (registers are kept for the per-packet ones)
@@ -607,11 +634,40 @@ struct HostExec {
     return true;
   }
 
-  // ---- CoDel (router/codel_queue.rs) on a per-host ring ----
-  __device__ __forceinline__ CodelEnt* cq_slot(uint32_t i) {
-    uint32_t idx = cq_head + i;
-    if (idx >= S.codel_cap) idx -= S.codel_cap;
-    return S.codel + (size_t)h * S.codel_cap + idx;
+  // ---- CoDel (router/codel_queue.rs) on a chain of pool pages ----
+  // The queue's runs in order fill the head page from cq_head's offset, whole pages, and the
+  // tail page (L->cq_tp) up to run cq_nr - 1; only the head and tail runs are ever touched.
+  __device__ __forceinline__ SGN_GLB CodelEnt* cq_head_slot() { return S.codel + cq_head; }
+  __device__ __forceinline__ SGN_GLB CodelEnt* cq_tail_slot() {
+    return S.codel + ((size_t)L->cq_tp * CQ_PAGE + ((cq_head + cq_nr - 1) & (CQ_PAGE - 1)));
+  }
+  // a page from the pool: the free ring's next entry, if it was freed before this round
+  // (the entries of the current round are still being written by other waves)
+  __device__ __forceinline__ uint32_t cq_alloc_page() {
+    const uint64_t i = __hip_atomic_fetch_add(&C->pg_alloc, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i >= ob->pg_avail) return NO_HOST;
+    return ld_dev(&S.cq_free[i % S.cq_pages]);
+  }
+  __device__ __forceinline__ void cq_free_page(uint32_t pg) {
+    const uint64_t j = __hip_atomic_fetch_add(&C->pg_tail, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_dev(&S.cq_free[j % S.cq_pages], pg);
+    cnt_add(ob->pg_freed, 1);
+  }
+  // the head run left the queue: next run, next page (the old one back to the pool), or an
+  // empty queue that keeps its page from the start
+  __device__ __forceinline__ void cq_pop_head() {
+    cq_nr--;
+    if (cq_nr == 0) {
+      cq_head &= ~(CQ_PAGE - 1);
+      L->cq_tp = cq_head / CQ_PAGE;
+    } else if (((cq_head + 1) & (CQ_PAGE - 1)) != 0) {
+      cq_head++;
+    } else {
+      const uint32_t pg = cq_head / CQ_PAGE;
+      const uint32_t nx = ld_dev(&S.cq_next[pg]);  // (neighbouring links belong to other hosts)
+      cq_free_page(pg);
+      cq_head = nx * CQ_PAGE;
+    }
   }
   // Router::route_incoming_packet (router/mod.rs:55-57) -> CoDelQueue::push (:303-317) for a
   // run of n packets arriving at `now`: extends the open tail run when it continues it.
@@ -627,12 +683,18 @@ struct HostExec {
       L->hd.count += n;
     } else {
       if (tl_open) {
-        *cq_slot(cq_nr - 1) = L->tl;
+        st_dev_cq(cq_tail_slot(), L->tl);
         tl_open = false;
       }
-      if (cq_nr >= S.codel_cap) {
-        overflow(OVF_CODEL);
-        return;
+      if (cq_nr > 0 && ((cq_head + cq_nr) & (CQ_PAGE - 1)) == 0) {
+        // the tail page is full: link a page from the pool
+        const uint32_t np = cq_alloc_page();
+        if (np == NO_HOST) {
+          overflow(OVF_CODEL);
+          return;
+        }
+        st_dev(&S.cq_next[L->cq_tp], np);
+        L->cq_tp = np;
       }
       L->tl.enqueue_ts = now;
       L->tl.eid = eid0;
@@ -667,7 +729,7 @@ struct HostExec {
     } else {
       DG(DG_HDLOAD);
       DGT_BEGIN(th);
-      L->hd = *cq_slot(0);
+      L->hd = ld_dev_cq(cq_head_slot());
       DGT_WAIT();
       DGT_END(DGT_HDLD, th);
     }
@@ -684,8 +746,7 @@ struct HostExec {
     L->hd.eid++;
     if (--L->hd.count == 0) {
       hd_valid = false;
-      cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
-      cq_nr--;
+      cq_pop_head();
     }
     cq_len--;
     cq_bytes = sat_sub(cq_bytes, (uint64_t)e.payload + sgn_header_bytes(e.tag));
@@ -912,8 +973,7 @@ struct HostExec {
             }  // else drop mode before drop_next: unchanged
             if (L->hd.count == 0) {
               hd_valid = false;
-              cq_head = cq_head + 1 == S.codel_cap ? 0 : cq_head + 1;
-              cq_nr--;
+              cq_pop_head();
             }
             if (m) deliver_run(r.src, r.eid, m, r.payload, r.tag);
             if (blocked) {
@@ -1499,6 +1559,9 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     st_dev(&C->keep_slab, slab_b1);
     const uint64_t nb1 = km < kk ? km : kk;
     st_dev(&S.bucket_min[b1], nb1);
+    // CoDel page pool: the pages freed this round become allocatable in the next
+    const uint64_t fr = __hip_atomic_exchange(&C->pg_freed, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fr) st_dev(&C->pg_avail, ld_dev(&C->pg_avail) + fr);
     m = nb1 < m ? nb1 : m;
     m = wn < m ? wn : m;
     if (local) {
@@ -1896,7 +1959,11 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   const uint32_t ks = C->keep_slab;
   if (S.NB <= LDS_BSLAB)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)S.bucket_slab[i];
-  if (threadIdx.x == 0) X.ob->keepmin = &C->keep_min;
+  if (threadIdx.x == 0) {
+    X.ob->keepmin = &C->keep_min;
+    X.ob->pg_avail = C->pg_avail;
+    X.ob->pg_freed = &C->pg_freed;
+  }
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
@@ -2044,11 +2111,12 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   // bookkeeping that workgroup 0 does during the next round. The bucket -> slab table
   // changes by one swap per round, applied by every workgroup to its own LDS copy.
   struct RoundLDS {
-    uint64_t ws, we, pend_ws, pend_we, pend_nb1;
+    uint64_t ws, we, pend_ws, pend_we, pend_nb1, pg_avail;
     uint32_t active, ks, pend_new, pend;
   };
   __shared__ RoundLDS rs;
   if (threadIdx.x == 0) {
+    rs.pg_avail = ld_dev(&C->pg_avail);
     rs.ws = ld_dev(&C->ws);
     rs.we = ld_dev(&C->we);
     rs.active = ld_dev(&C->active);
@@ -2076,7 +2144,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       const uint32_t q = (r + 1) % 3;
       for (uint32_t i = threadIdx.x; i < RB_CH * 2; i += 64) st_dev(&S.rb_min[(size_t)q * RB_CH * 2 + i], (uint64_t)INVALID);
       for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64) st_dev(&S.rb_cnt[(size_t)q * (RB_CH + 1) + i], 0u);
-      if (threadIdx.x == 0) st_dev(&S.rb_keep[q], (uint64_t)INVALID);
+      if (threadIdx.x == 0) {
+        st_dev(&S.rb_keep[q], (uint64_t)INVALID);
+        st_dev(&S.rb_free[q], (uint64_t)0);
+      }
     }
     // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
     // round edge known} on the 100 MHz clock
@@ -2084,7 +2155,11 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     if (rd && threadIdx.x == 0)
       __hip_atomic_fetch_min(rd, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) X.ob->keepmin = &S.rb_keep[p];
+    if (threadIdx.x == 0) {
+      X.ob->keepmin = &S.rb_keep[p];
+      X.ob->pg_avail = rs.pg_avail;
+      X.ob->pg_freed = &S.rb_free[p];
+    }
     uint64_t kall = INVALID, mall = INVALID;
     bool arrived = false;
     for (uint32_t g = w; g < S.G; g += P) {
@@ -2136,6 +2211,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       rs.ws = e.ws;
       rs.we = e.we;
       rs.active = e.active;
+      rs.pg_avail += ld_dev(&S.rb_free[p]);  // this round's freed pages (all written: barrier)
       if (w == 0) {
         st_dev(&C->last_min_next, e.min_next);
         st_dev(&C->prev_we, we);
@@ -2152,6 +2228,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       st_dev(&C->we, rs.we);
       st_dev(&C->active, rs.active);
       st_dev(&C->rounds, rounds0 + r);
+      st_dev(&C->pg_avail, rs.pg_avail);
     }
   }
 }
@@ -2428,7 +2505,7 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow == 0) return 0;
   std::string what;
   if (c.overflow & OVF_BUCKET) what += " calendar bucket (raise sgn_sim_config.event_capacity)";
-  if (c.overflow & OVF_CODEL) what += " CoDel ring (raise sgn_sim_config.codel_cap)";
+  if (c.overflow & OVF_CODEL) what += " CoDel page pool (raise sgn_sim_config.codel_cap)";
   if (c.overflow & OVF_SEG) what += " due-event segment buffer";
   if (c.overflow & OVF_EXCHANGE) what += " exchange slot (raise exchange_slot_events)";
   if (c.overflow & OVF_TRACE) what += " trace buffer";
@@ -2620,7 +2697,13 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.fifo_cap = cfg->out_fifo_cap;
   if (cfg->interface_qdisc > SGN_QDISC_ROUND_ROBIN) return set_error(ctx, SGN_EINVAL, "unknown interface_qdisc");
   S.qdisc_rr = cfg->interface_qdisc == SGN_QDISC_ROUND_ROBIN ? 1u : 0u;
-  S.codel_cap = cfg->codel_cap;
+  // CoDel page pool: codel_cap run slots per host on average, at least one page per host
+  // (its first) plus 64 to share
+  {
+    const uint64_t pages = std::max<uint64_t>((uint64_t)nH + 64, ((uint64_t)nH * cfg->codel_cap + CQ_PAGE - 1) / CQ_PAGE);
+    if (pages >= (1ULL << 28)) return set_error(ctx, SGN_EINVAL, "codel_cap: CoDel page pool above 2^28 pages");
+    S.cq_pages = (uint32_t)pages;
+  }
   S.trace_on = ctx->trace_cap > 0;
   S.tkind = tr->kind;
   S.payload_len = tr->payload_len;
@@ -2713,6 +2796,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     }
     for (int i = 0; i < 3; i++) r.dig[i] = SGN_DIGEST_SEED;
     r.rc_dst = NO_HOST;  // empty route cache
+    r.cq_head = h * CQ_PAGE;  // CoDel chain: page h
+    r.cq_tp = h;
     r.ip = ctx->ip[g];
     r.unode = ctx->unode[g];
     if (is_server[g]) r.flags |= F_SERVER;
@@ -2743,14 +2828,21 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   int rc = 0;
   if ((rc = up32(ctx->sid_of, &S.sid_of)) || (rc = up32(ctx->host_of, &S.host_of))) return rc;
   S.hrec = (decltype(S.hrec))dalloc<HostRec>(ctx, nH);
-  S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)nH * cfg->codel_cap);
+  S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)S.cq_pages * CQ_PAGE);
+  S.cq_next = (decltype(S.cq_next))dalloc<uint32_t>(ctx, S.cq_pages);
+  {  // host slot h starts with page h; pages nH.. are the free ring's first entries
+    std::vector<uint32_t> fr(S.cq_pages, 0);
+    for (uint32_t i = 0; i + nH < S.cq_pages; i++) fr[i] = nH + i;
+    if ((rc = up32(fr, &S.cq_free))) return rc;
+  }
+  S.rb_free = (decltype(S.rb_free))dalloc<uint64_t>(ctx, 3);
   S.fifo = (decltype(S.fifo))dalloc<FifoEnt>(ctx, (size_t)nH * cfg->out_fifo_cap);
   S.fifo_addr = nullptr;
   if (ctx->trace_cap) {
     S.fifo_addr = (decltype(S.fifo_addr))dalloc<uint32_t>(ctx, (size_t)nH * cfg->out_fifo_cap);
     if (!S.fifo_addr) return set_error(ctx, SGN_ENOMEM, "device allocation failed (trace)");
   }
-  if (!S.hrec || !S.codel || !S.fifo)
+  if (!S.hrec || !S.codel || !S.fifo || !S.cq_next || !S.rb_free)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
   if ((rc = up64(nextloc, &S.nextloc))) return rc;
@@ -2847,6 +2939,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   c.keep_min = INVALID;
   c.last_min_next = INVALID;
   c.prev_we = SIM_START;
+  c.pg_tail = c.pg_avail = S.cq_pages - nH;  // the free ring holds the pages beyond the hosts' first
   // multi-shard exchange size: RCCL rounds start at min(slot, kXszInit) runs per peer and
   // grow with the high-water mark; a local shard group copies counts, so it uses the slot
   ctx->xsz_cur = ctx->nranks > 1 ? (ctx->comm_local ? (uint32_t)ctx->xslot
@@ -2963,6 +3056,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
       SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * 2 + 4) * 8, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, 3 * (RB_CH + 1) * 4, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_free, 0, 3 * 8, ctx->stream));
       time_begin(ctx, K_EXECUTE);
       launch_k_rounds(ctx, n);
       time_end(ctx);
@@ -3191,6 +3285,19 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   out->exchange_hwm_runs = ctx->h_ctrl ? ctx->h_ctrl->xhwm : 0;
   out->exchange_spills = ctx->x_spills;
   out->exchange_bytes = ctx->x_bytes;
+  out->codel_pages = ctx->S.cq_pages;
+  // the control block as is (an overflow is reported by the calls that run rounds, not here)
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SGN_HIP(ctx, hipMemcpy(ctx->h_ctrl, (const void*)ctx->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+  const Ctrl& c = *ctx->h_ctrl;
+  out->codel_page_allocs = c.pg_alloc;
+  out->codel_pages_free = c.pg_tail >= c.pg_alloc ? c.pg_tail - c.pg_alloc : 0;
+  std::vector<HostRec> recs;
+  if (int e = read_recs(ctx, 0, ctx->S.nH, &recs)) return e;
+  uint64_t chained = 0;
+  for (const HostRec& r : recs)
+    chained += r.cq_nr == 0 ? 1 : ((r.cq_head & (CQ_PAGE - 1)) + r.cq_nr + CQ_PAGE - 1) / CQ_PAGE;
+  out->codel_pages_chained = chained;
   return 0;
 }
 

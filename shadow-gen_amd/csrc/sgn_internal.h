@@ -108,6 +108,11 @@ struct Ctrl {
   // and the largest per-peer run count any shard produced in a round so far
   uint32_t xsz, xspill;
   uint64_t xhwm;
+  // CoDel page pool: allocations so far (index into the free ring), free-ring entries
+  // written so far, entries allocations may use this round (the ring as of the last round
+  // edge: a page freed in a round is reused from the next one), pages freed this round
+  // (per-round launches; the persistent kernel counts in DevSim::rb_free)
+  uint64_t pg_alloc, pg_tail, pg_avail, pg_freed;
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
@@ -129,6 +134,8 @@ enum : uint32_t {
 // A round touches only the hosts with something due (~1 in 8 at the bench workload), so a
 // record per host turns each executed host's state into 3 contiguous cache lines; the hot
 // part (bytes 0..335) is what Host::execute reads and writes every time it runs.
+constexpr uint32_t CQ_PAGE = 16;  // CoDel runs per pool page (cq_head = page * CQ_PAGE + offset)
+
 struct __attribute__((aligned(128))) HostRec {
   uint64_t rng[4];           // Xoshiro256++ state (host/host.rs:234)
   uint64_t eid;              // next event id (host.rs:259,662-666)
@@ -143,10 +150,11 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t rc_lat, rc_T;     // route cache: latency, integer loss threshold ...
   uint64_t dig[3];           // digests tx, rx, app
   uint32_t flags, ro_dst, ro_pay, ro_tag;    // flag bits; relay_inet_out cached packet
-  uint32_t ri_src, ri_pay, ri_tag, cq_head;  // relay_inet_in cached packet; CoDel ring head
+  uint32_t ri_src, ri_pay, ri_tag, cq_head;  // relay_inet_in cached packet; CoDel head run (pool index)
   uint32_t cq_nr, cq_len, fq_head, fq_len;   // CoDel runs / packets; send queue
   uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
   uint32_t gid, rc_sid;                      // this host's HostId; route cache peer's slot id
+  uint32_t cq_tp, cq_pad;                    // CoDel chain's tail page (cq_head: head run's pool index)
   uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
   uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
   uint64_t app_k;                            // synthetic app counter
@@ -154,7 +162,7 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t tseq;                            // trace sequence
   uint64_t rng_pos;                         // RNG draws so far (kept while tracing, and by sgn_rng_*)
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
-  uint64_t pad[15];
+  uint64_t pad[14];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
@@ -228,7 +236,8 @@ struct DevSim {
   uint64_t end_time, boot_end, runahead_cfg;
   uint64_t min_possible;
   int32_t dynamic;
-  uint32_t fifo_cap, codel_cap;
+  uint32_t fifo_cap;
+  uint32_t cq_pages;  // CoDel page pool: pages of CQ_PAGE runs (every host owns >= 1)
   uint32_t qdisc_rr;  // interface_qdisc == SGN_QDISC_ROUND_ROBIN
   uint32_t pad_q;
   uint32_t trace_on;
@@ -257,7 +266,14 @@ struct DevSim {
   // for all hosts at the start of a round: a dense array keeps that read coalesced)
   SGN_GLB HostRec* hrec;        // [nH]
   SGN_GLB uint64_t* nextloc;    // [nH]
-  SGN_GLB CodelEnt* codel;      // [nH * codel_cap] run ring per host
+  // CoDel queues (Router's inbound CoDelQueue, unbounded in the reference) as chains of
+  // pages from ONE pool sized by total occupancy, not per host: a host's queue is its runs
+  // in order over a chain head page -> ... -> tail page (cq_next links them). Pages leave
+  // the chain from the head and go back through the free ring.
+  SGN_GLB CodelEnt* codel;      // [cq_pages * CQ_PAGE] page pool
+  SGN_GLB uint32_t* cq_next;    // [cq_pages] next page of the chain
+  SGN_GLB uint32_t* cq_free;    // [cq_pages] free ring (Ctrl::pg_alloc / pg_tail index it mod cq_pages)
+  SGN_GLB uint64_t* rb_free;    // [3] persistent rounds: pages freed in the round (by round % 3)
   SGN_GLB FifoEnt* fifo;        // [nH * fifo_cap] send queue per host
   SGN_GLB uint32_t* fifo_addr;  // [nH * fifo_cap] traced runs: an unknown entry's address
   // calendar: NB time buckets of width BW; every bucket is a set of slabs, one per host

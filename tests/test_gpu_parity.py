@@ -290,6 +290,24 @@ def test_engine_tgen_trace_codel(ctxf, oracle):
     assert_same_run(o, c, args[2].n)
 
 
+@pytest.mark.parametrize("trace", [True, False])
+def test_engine_codel_page_pool(ctxf, oracle, trace):
+    # CoDel queues as chains of pool pages: 160 run slots per host on average (3000 pages of
+    # 16 runs for 300 hosts) while the slow hosts' standing queues need ~2.7k pages beyond
+    # their first at peak: pages leave the free ring, come back as queues drain and are
+    # taken again by other hosts in later rounds — traced (k_execute) and persistent rounds
+    bw = np.where(np.arange(300) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+    args = scenario(n=300, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=2_000_000_000, bw=bw, tor=True,
+                    tgen_think=200_000_000, codel=160)
+    o, c = run_both(ctxf, oracle, args, trace=trace)
+    st, info = c.stats(), c.engine_info()
+    assert st["codel_dropped"] > 0, st
+    assert info["codel_pages"] == 3000
+    assert info["codel_page_allocs"] > 3000 - 300, info  # more allocations than spare pages: reuse
+    assert info["codel_pages_free"] + info["codel_pages_chained"] == info["codel_pages"], info
+    assert_same_run(o, c, args[2].n, trace=trace)
+
+
 def test_engine_tgen_round_robin_qdisc(ctxf, oracle):
     # experimental.interface_qdisc: round_robin; short think times keep several response
     # trains (sockets) queued at a server, so the interface interleaves them packet by packet
