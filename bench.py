@@ -483,6 +483,19 @@ def main():
                 roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
                 roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
     info = ctx.engine_info()
+    if roof is not None:
+        # why the kernel sits far below the HBM roof: a latency chain on a partly filled chip.
+        # Workgroups are one wave; k_rounds keeps its grid resident (each workgroup serves
+        # groups g, g + grid, ...), k_execute launches one workgroup per group every round.
+        grid = info["persistent_grid"] if rk == "k_rounds" else info["host_groups"]
+        wave_rounds = info["host_groups"] * max(1, rounds)
+        roof["occupancy"] = {
+            "compute_units": info["compute_units"],
+            "resident_waves_per_cu": round(min(grid, 8 * info["compute_units"]) / max(1, info["compute_units"]), 2),
+            "lanes_per_wave": 64, "hosts_per_wave": info["hosts_per_wave"],
+            "busy_lanes_per_wave_round": round(host_exec / wave_rounds, 2),
+            "note": "a host runs in its own lane; busy lanes = hosts with an event due in the window, "
+                    "averaged over every (group, round); the slowest wave of a round sets its length"}
     out = {
         "metric": METRIC,
         "value": ev / el,

@@ -431,6 +431,7 @@ typedef struct sgn_engine_info {
   uint64_t codel_pages_free;     /* pages in the free ring now */
   uint64_t codel_pages_chained;  /* pages in the hosts' queue chains now (read from the host
                                     records: free + chained == codel_pages, no page lost) */
+  uint64_t compute_units;        /* of this context's GPU */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

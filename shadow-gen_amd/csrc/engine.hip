@@ -3298,6 +3298,9 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   for (const HostRec& r : recs)
     chained += r.cq_nr == 0 ? 1 : ((r.cq_head & (CQ_PAGE - 1)) + r.cq_nr + CQ_PAGE - 1) / CQ_PAGE;
   out->codel_pages_chained = chained;
+  int ncu = 0;
+  SGN_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  out->compute_units = (uint64_t)ncu;
   return 0;
 }
 

@@ -176,7 +176,8 @@ class EngineInfo(C.Structure):
         "calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity", "hosts_per_wave",
         "persistent_grid", "persistent_fallbacks", "device_bytes", "exchange_slot_runs",
         "exchange_send_runs", "exchange_hwm_runs", "exchange_spills", "exchange_bytes", "codel_pages",
-        "codel_page_allocs", "codel_pages_free", "codel_pages_chained")]
+        "codel_page_allocs", "codel_pages_free", "codel_pages_chained",
+        "compute_units")]
 
 
 class KernelTimes(C.Structure):
