@@ -432,6 +432,7 @@ typedef struct sgn_engine_info {
   uint64_t codel_pages_chained;  /* pages in the hosts' queue chains now (read from the host
                                     records: free + chained == codel_pages, no page lost) */
   uint64_t compute_units;        /* of this context's GPU */
+  uint64_t bucket_min_lds;       /* 1: round kernels fold bucket minima in LDS first */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

@@ -282,6 +282,7 @@ struct Outbox {
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
   uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
   SGN_GLB uint64_t* keepmin;  // minimum of this round's new runs for the window's last bucket
+  uint64_t* bmin;             // LDS minima per bucket (+ [NB]: the spare slab) or null (below)
   uint64_t pg_avail;          // CoDel page pool: free-ring entries allocations may use this round
   SGN_GLB uint64_t* pg_freed; // ... and the round's freed-page counter
 };
@@ -1163,7 +1164,12 @@ struct HostExec {
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dsid - S.lo) >> S.gsh);
-      min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
+      // the bucket's pending minimum: folded in the workgroup's LDS table when it has one
+      // (flush_bmin publishes it before the round's arrival), else one device atomic per run
+      if (ob->bmin)
+        atomicMin((unsigned long long*)&ob->bmin[b == b1 ? S.NB : b], (unsigned long long)deliver);
+      else
+        min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
       if (nrec == 1) {
         const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
         if (k < OBOX) {
@@ -1622,6 +1628,7 @@ struct ExecLDS {
   LaneLDS* lslot;     // the lanes' LDS slots
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   Outbox* ob;         // the wave's outbox
+  uint64_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
 };
 
 // One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
@@ -1908,13 +1915,36 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   ExecLDS X;                                                                         \
   X.lev = (EvRec*)lds_dyn;                                                           \
   X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \
-  X.lc = X.lb + S.CAP;                                                               \
+  X.lc = X.lb + ((S.CAP + 3) & ~3u);                                                 \
+  X.bmin = S.agg_bmin ? (uint64_t*)(X.lc + ((S.CAP + 3) & ~3u)) : nullptr;           \
   X.lcnt = lcnt_;                                                                    \
   X.lstart = lstart_;                                                                \
   X.lcur = lcur_;                                                                    \
   X.lslot = lslot_;                                                                  \
   X.lbs = lbs_;                                                                      \
-  X.ob = &ob_;
+  X.ob = &ob_;                                                                       \
+  if (threadIdx.x == 0) ob_.bmin = X.bmin;
+
+// The workgroup's LDS table of bucket minima (S.agg_bmin): its sends of the round fold their
+// delivery times there with LDS atomics; before the round's arrival every lane publishes a
+// share of the table with one device atomic per touched bucket and resets it. Config D (every
+// host sends to a random peer every round) otherwise puts ~1 M device atomics per round on
+// the ~50 bucket words of the next 50 ms — a few cache lines — and serialises on them.
+__device__ __forceinline__ void init_bmin(const DevSim& S, const ExecLDS& X) {
+  if (X.bmin)
+    for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) X.bmin[i] = INVALID;
+}
+__device__ __forceinline__ void flush_bmin(const DevSim& S, const ExecLDS& X) {
+  if (!X.bmin) return;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) {
+    const uint64_t v = X.bmin[i];
+    if (v != INVALID) {
+      min_nr(i == S.NB ? X.ob->keepmin : &S.bucket_min[i], v);
+      X.bmin[i] = INVALID;
+    }
+  }
+}
 
 // Arrival of one workgroup at the end of a round: its minima go into its chunk's slots with
 // returning device-scope atomics, then it counts itself in (64 workgroups per chunk counter,
@@ -1964,10 +1994,12 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     X.ob->pg_avail = C->pg_avail;
     X.ob->pg_freed = &C->pg_freed;
   }
+  init_bmin(S, X);
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
   exec_group<true, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+    flush_bmin(S, X);
     last = arrive(S, blockIdx.x, gridDim.x, k, n);
   });
   if (!last) return;
@@ -2127,6 +2159,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   const bool lds_tab = S.NB <= LDS_BSLAB;
   if (lds_tab)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
+  init_bmin(S, X);
   __syncthreads();
   auto uni64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -2172,6 +2205,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
           if (rd && threadIdx.x == 0)
             __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flush_bmin(S, X);
           rb_arrive(S, p, w, P, kall, mall);
           arrived = true;
         }
@@ -2431,7 +2465,11 @@ const char* kKernelNames[K_NUM] = {"k_execute", "k_import"};
 int launch_round(sgn_ctx* ctx);
 
 // dynamic LDS of k_execute / k_rounds: CAP event runs + two u16 index arrays
-inline size_t exec_lds_bytes(uint32_t cap) { return (size_t)cap * (sizeof(EvRec) + 4); }
+// (the u16 index arrays are padded to 8 bytes so the optional bucket-minimum table that
+// follows them is aligned)
+inline size_t exec_lds_bytes(uint32_t cap, uint32_t agg_nb = 0) {
+  return (size_t)cap * sizeof(EvRec) + 2 * (size_t)((cap + 3) & ~3u) * 2 + (agg_nb ? (size_t)(agg_nb + 1) * 8 : 0);
+}
 constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then a host sync)
 constexpr uint64_t kTimeEvery = 8;        // per-round launches: one timed in kTimeEvery
 
@@ -2454,7 +2492,7 @@ const void* rounds_fn(uint32_t kind) {
 void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
   const uint32_t k = ctx->S.tkind;
   const dim3 grid(ctx->S.G), block(64);
-  const size_t lds = exec_lds_bytes(ctx->S.CAP);
+  const size_t lds = exec_lds_bytes(ctx->S.CAP, ctx->S.agg_bmin ? ctx->S.NB : 0);
   const DevSim* d = (const DevSim*)ctx->d_S;
   if (k == SGN_TRAFFIC_TGEN)
     hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_TGEN>, grid, block, lds, st, d);
@@ -2466,7 +2504,7 @@ void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
 void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
   const uint32_t k = ctx->S.tkind;
   const dim3 grid(ctx->persist_grid), block(64);
-  const size_t lds = exec_lds_bytes(ctx->S.CAP);
+  const size_t lds = exec_lds_bytes(ctx->S.CAP, ctx->S.agg_bmin ? ctx->S.NB : 0);
   const DevSim* d = (const DevSim*)ctx->d_S;
   if (k == SGN_TRAFFIC_TGEN)
     hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_TGEN>, grid, block, lds, ctx->stream, d, n);
@@ -2963,19 +3001,37 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // persistent rounds keep the bucket -> slab table in LDS (each workgroup applies the round's
   // swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per round, and
   // so does a traced run (k_rounds is built without the per-packet trace)
-  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+  // Resident workgroups of a round kernel on this GPU (0: unknown): the occupancy query,
+  // capped by LDS per CU — LDS is allocated per workgroup in 512-byte granules (a 23184-byte
+  // workgroup fits 6 per CU, not 7: a grid sized for 7 was not resident and its barrier
+  // timed out)
+  auto resident = [&](const void* fn, size_t dyn) -> uint64_t {
     int occ = 0, ncu = 0;
-    const size_t dyn = exec_lds_bytes((uint32_t)CAP);
     hipFuncAttributes fa{};
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rounds_fn(S.tkind), 64, dyn) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
-        hipFuncGetAttributes(&fa, rounds_fn(S.tkind)) == hipSuccess && occ > 0 && ncu > 0) {
-      // LDS is allocated per workgroup in 512-byte granules (a 23184-byte workgroup fits 6
-      // per CU, not 7: a grid sized for 7 was not resident and its barrier timed out)
-      const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
-      const int lds_occ = (int)((160u * 1024u) / lds_wg);
-      occ = std::min(occ, lds_occ);
-      ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, (uint64_t)occ * (uint64_t)ncu);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64, dyn) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+        hipFuncGetAttributes(&fa, fn) != hipSuccess || occ <= 0 || ncu <= 0)
+      return 0;
+    const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
+    return (uint64_t)std::min<int>(occ, (int)((160u * 1024u) / lds_wg)) * (uint64_t)ncu;
+  };
+  // The LDS table of bucket minima ((NB + 1) x 8 bytes per workgroup, flush_bmin) is used
+  // when it costs no resident workgroups where they count: the round kernels' grids stay as
+  // large (config C has no LDS to spare: its 1563 groups need 7 workgroups per CU), or the
+  // grid exceeds the chip either way (config D). SGN_AGG_BMIN=0/1 overrides.
+  {
+    bool agg = true;
+    for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind)}) {
+      const uint64_t r0 = resident(fn, exec_lds_bytes((uint32_t)CAP)), r1 = resident(fn, exec_lds_bytes((uint32_t)CAP, NB));
+      if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
+    }
+    if (const char* e = getenv("SGN_AGG_BMIN")) agg = atoi(e) != 0;
+    S.agg_bmin = agg ? 1u : 0u;
+  }
+  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+    const uint64_t res = resident(rounds_fn(S.tkind), exec_lds_bytes((uint32_t)CAP, S.agg_bmin ? NB : 0));
+    if (res) {
+      ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, res);
       // test hook: a smaller grid makes every workgroup serve several groups per round
       if (const char* e = getenv("SGN_PERSIST_GRID"))
         ctx->persist_grid = std::max<uint32_t>(1, std::min<uint32_t>(ctx->persist_grid, (uint32_t)atoi(e)));
@@ -3301,6 +3357,7 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   int ncu = 0;
   SGN_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   out->compute_units = (uint64_t)ncu;
+  out->bucket_min_lds = ctx->S.agg_bmin;
   return 0;
 }
 

@@ -299,6 +299,7 @@ struct DevSim {
   SGN_GLB uint64_t* rb_keep;      // [3]
   SGN_GLB uint32_t* rb_cnt;       // [3][65]
   uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
+  uint32_t agg_bmin;      // the round kernels fold bucket minima in an LDS table (see engine.hip)
   uint32_t pad3;
   uint64_t BW;
   UDiv64 bw_div;          // division by BW

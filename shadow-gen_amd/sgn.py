@@ -177,7 +177,7 @@ class EngineInfo(C.Structure):
         "persistent_grid", "persistent_fallbacks", "device_bytes", "exchange_slot_runs",
         "exchange_send_runs", "exchange_hwm_runs", "exchange_spills", "exchange_bytes", "codel_pages",
         "codel_page_allocs", "codel_pages_free", "codel_pages_chained",
-        "compute_units")]
+        "compute_units", "bucket_min_lds")]
 
 
 class KernelTimes(C.Structure):
