@@ -282,7 +282,8 @@ struct Outbox {
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
   uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
   SGN_GLB uint64_t* keepmin;  // minimum of this round's new runs for the window's last bucket
-  uint64_t* bmin;             // LDS minima per bucket (+ [NB]: the spare slab) or null (below)
+  uint32_t* bmin;             // LDS minima per bucket (+ [NB]: the spare slab) or null (below),
+  uint64_t bbase;             // ... as offsets from this time (the round's window start)
   uint64_t pg_avail;          // CoDel page pool: free-ring entries allocations may use this round
   SGN_GLB uint64_t* pg_freed; // ... and the round's freed-page counter
 };
@@ -1167,7 +1168,7 @@ struct HostExec {
       // the bucket's pending minimum: folded in the workgroup's LDS table when it has one
       // (flush_bmin publishes it before the round's arrival), else one device atomic per run
       if (ob->bmin)
-        atomicMin((unsigned long long*)&ob->bmin[b == b1 ? S.NB : b], (unsigned long long)deliver);
+        atomicMin(&ob->bmin[b == b1 ? S.NB : b], (uint32_t)(deliver - ob->bbase));
       else
         min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
       if (nrec == 1) {
@@ -1628,7 +1629,7 @@ struct ExecLDS {
   LaneLDS* lslot;     // the lanes' LDS slots
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   Outbox* ob;         // the wave's outbox
-  uint64_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
+  uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
 };
 
 // One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
@@ -1916,7 +1917,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.lev = (EvRec*)lds_dyn;                                                           \
   X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \
   X.lc = X.lb + ((S.CAP + 3) & ~3u);                                                 \
-  X.bmin = S.agg_bmin ? (uint64_t*)(X.lc + ((S.CAP + 3) & ~3u)) : nullptr;           \
+  X.bmin = S.agg_bmin ? (uint32_t*)(X.lc + ((S.CAP + 3) & ~3u)) : nullptr;           \
   X.lcnt = lcnt_;                                                                    \
   X.lstart = lstart_;                                                                \
   X.lcur = lcur_;                                                                    \
@@ -1930,18 +1931,21 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 // share of the table with one device atomic per touched bucket and resets it. Config D (every
 // host sends to a random peer every round) otherwise puts ~1 M device atomics per round on
 // the ~50 bucket words of the next 50 ms — a few cache lines — and serialises on them.
+// Entries are u32 offsets from the round's window start (a delivery is below the calendar's
+// horizon, at most (NB + 1) bucket widths ahead; sim_init enables the table only when that
+// fits 32 bits).
 __device__ __forceinline__ void init_bmin(const DevSim& S, const ExecLDS& X) {
   if (X.bmin)
-    for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) X.bmin[i] = INVALID;
+    for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) X.bmin[i] = 0xFFFFFFFFu;
 }
 __device__ __forceinline__ void flush_bmin(const DevSim& S, const ExecLDS& X) {
   if (!X.bmin) return;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) {
-    const uint64_t v = X.bmin[i];
-    if (v != INVALID) {
-      min_nr(i == S.NB ? X.ob->keepmin : &S.bucket_min[i], v);
-      X.bmin[i] = INVALID;
+    const uint32_t v = X.bmin[i];
+    if (v != 0xFFFFFFFFu) {
+      min_nr(i == S.NB ? X.ob->keepmin : &S.bucket_min[i], X.ob->bbase + v);
+      X.bmin[i] = 0xFFFFFFFFu;
     }
   }
 }
@@ -1991,6 +1995,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)S.bucket_slab[i];
   if (threadIdx.x == 0) {
     X.ob->keepmin = &C->keep_min;
+    X.ob->bbase = C->ws;
     X.ob->pg_avail = C->pg_avail;
     X.ob->pg_freed = &C->pg_freed;
   }
@@ -2190,6 +2195,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) {
       X.ob->keepmin = &S.rb_keep[p];
+      X.ob->bbase = ws;
       X.ob->pg_avail = rs.pg_avail;
       X.ob->pg_freed = &S.rb_free[p];
     }
@@ -2468,7 +2474,7 @@ int launch_round(sgn_ctx* ctx);
 // (the u16 index arrays are padded to 8 bytes so the optional bucket-minimum table that
 // follows them is aligned)
 inline size_t exec_lds_bytes(uint32_t cap, uint32_t agg_nb = 0) {
-  return (size_t)cap * sizeof(EvRec) + 2 * (size_t)((cap + 3) & ~3u) * 2 + (agg_nb ? (size_t)(agg_nb + 1) * 8 : 0);
+  return (size_t)cap * sizeof(EvRec) + 2 * (size_t)((cap + 3) & ~3u) * 2 + (agg_nb ? (size_t)(agg_nb + 1) * 4 : 0);
 }
 constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then a host sync)
 constexpr uint64_t kTimeEvery = 8;        // per-round launches: one timed in kTimeEvery
@@ -3015,7 +3021,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
     return (uint64_t)std::min<int>(occ, (int)((160u * 1024u) / lds_wg)) * (uint64_t)ncu;
   };
-  // The LDS table of bucket minima ((NB + 1) x 8 bytes per workgroup, flush_bmin) is used
+  // The LDS table of bucket minima ((NB + 1) x 4 bytes per workgroup, flush_bmin) is used
   // when it costs no resident workgroups where they count: the round kernels' grids stay as
   // large (config C has no LDS to spare: its 1563 groups need 7 workgroups per CU), or the
   // grid exceeds the chip either way (config D). SGN_AGG_BMIN=0/1 overrides.
@@ -3026,6 +3032,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
     }
     if (const char* e = getenv("SGN_AGG_BMIN")) agg = atoi(e) != 0;
+    if ((NB + 1) * BW >= (1ULL << 32)) agg = false;  // offsets from the window start must fit u32
     S.agg_bmin = agg ? 1u : 0u;
   }
   if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
