@@ -335,6 +335,8 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
                     help="wall budget of the CPU mode samples after the parity run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--codel-cap", type=int, default=None,
+                    help="CoDel run slots per host on average (the shared page pool's size)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU machine: every rank on device 0, each "
                          "with its own NCCL_HOSTID, so RCCL accepts the ranks (as if on different hosts) "
@@ -371,6 +373,8 @@ def main():
         groups = -(-args.hosts // 64)
         cfg.event_capacity = 257 * groups * 128
 
+    if args.codel_cap:
+        cfg.codel_cap = args.codel_cap
     ctx = sgn.Context(device=local, shard_rank=rank, shard_count=world,
                       flags=2)  # SGN_CREATE_TIME_EXECUTE: HIP events around the round kernel
     if world > 1:

@@ -1167,7 +1167,9 @@ struct HostExec {
       const size_t idx = (size_t)slab * S.G + ((dsid - S.lo) >> S.gsh);
       // the bucket's pending minimum: folded in the workgroup's LDS table when it has one
       // (flush_bmin publishes it before the round's arrival), else one device atomic per run
-      if (ob->bmin)
+      // (compiled for PERIODIC traffic only — configs B and D, where every host sends every
+      // round; the TGEN kernel of config C keeps its per-run atomic, uncontended there)
+      if (kApp == SGN_TRAFFIC_PERIODIC && S.agg_bmin)
         atomicMin(&ob->bmin[b == b1 ? S.NB : b], (uint32_t)(deliver - ob->bbase));
       else
         min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
@@ -1934,12 +1936,14 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 // Entries are u32 offsets from the round's window start (a delivery is below the calendar's
 // horizon, at most (NB + 1) bucket widths ahead; sim_init enables the table only when that
 // fits 32 bits).
+template <uint32_t kApp>
 __device__ __forceinline__ void init_bmin(const DevSim& S, const ExecLDS& X) {
-  if (X.bmin)
+  if (kApp == SGN_TRAFFIC_PERIODIC && X.bmin)
     for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) X.bmin[i] = 0xFFFFFFFFu;
 }
+template <uint32_t kApp>
 __device__ __forceinline__ void flush_bmin(const DevSim& S, const ExecLDS& X) {
-  if (!X.bmin) return;
+  if (kApp != SGN_TRAFFIC_PERIODIC || !X.bmin) return;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) {
     const uint32_t v = X.bmin[i];
@@ -1999,12 +2003,12 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     X.ob->pg_avail = C->pg_avail;
     X.ob->pg_freed = &C->pg_freed;
   }
-  init_bmin(S, X);
+  init_bmin<kApp>(S, X);
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
   exec_group<true, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
-    flush_bmin(S, X);
+    flush_bmin<kApp>(S, X);
     last = arrive(S, blockIdx.x, gridDim.x, k, n);
   });
   if (!last) return;
@@ -2164,7 +2168,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   const bool lds_tab = S.NB <= LDS_BSLAB;
   if (lds_tab)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
-  init_bmin(S, X);
+  init_bmin<kApp>(S, X);
   __syncthreads();
   auto uni64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -2211,7 +2215,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
           if (rd && threadIdx.x == 0)
             __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          flush_bmin(S, X);
+          flush_bmin<kApp>(S, X);
           rb_arrive(S, p, w, P, kall, mall);
           arrived = true;
         }
@@ -3026,7 +3030,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // large (config C has no LDS to spare: its 1563 groups need 7 workgroups per CU), or the
   // grid exceeds the chip either way (config D). SGN_AGG_BMIN=0/1 overrides.
   {
-    bool agg = true;
+    bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic
     for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind)}) {
       const uint64_t r0 = resident(fn, exec_lds_bytes((uint32_t)CAP)), r1 = resident(fn, exec_lds_bytes((uint32_t)CAP, NB));
       if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
