@@ -559,12 +559,15 @@ def main():
         out["parity"] = par["ok"]
         out["parity_detail"] = par
         ok = ok and par["ok"]
-    if world > 1 and args.workload == "C" and not args.no_shard_check:
+    if world > 1 and not args.no_shard_check:
         def unsharded():
             c1 = sgn.Context(device=local)
             c1.routes_build(g, used)
             c1.hosts_set(hosts)
-            c1.sim_init(cfg, tr)
+            cfg1 = type(cfg).from_buffer_copy(cfg)
+            if cfg1.event_capacity:  # calendar sized per host group: N x the groups
+                cfg1.event_capacity *= world
+            c1.sim_init(cfg1, tr)
             return c1
 
         par = shard_check(ctx, dist, rank, world, hosts.n, int(st1["rounds"]), unsharded)

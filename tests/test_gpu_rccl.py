@@ -24,14 +24,18 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 # xsz: the exchange size the first rounds move per peer (SGN_XSZ_INIT); 16 runs make the
 # early rounds exceed it, so they are held and completed with the whole slot (spill path)
-@pytest.mark.parametrize("graph,xsz,port", [("1", "", 29541), ("0", "", 29542), ("1", "16", 29543)])
-def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port):
+# workload D: every host sends to a random peer every round (half of it to the other shard),
+# through the LDS bucket minima of the PERIODIC kernel and a spill to a larger exchange size
+@pytest.mark.parametrize("graph,xsz,port,workload", [("1", "", 29541, "C"), ("0", "", 29542, "C"),
+                                                     ("1", "16", 29543, "C"), ("0", "", 29544, "D")])
+def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload):
     env = dict(os.environ, SGN_GRAPH=graph, NCCL_DEBUG="WARN", TMPDIR="/tmp")
     if xsz:
         env["SGN_XSZ_INIT"] = xsz
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "20000", "--rounds-per-step", "70"]
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "20000", "--rounds-per-step", "70",
+           "--workload", workload]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
