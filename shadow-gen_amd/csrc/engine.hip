@@ -1693,26 +1693,9 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 #ifdef SGN_DIAG
   uint64_t w_load = 0, w_run = 0;
 #endif
-  for (uint32_t bi = 0; bi < nbk; bi++) {
-    const uint64_t c0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t b = (bs + bi) & (S.NB - 1);
-    const bool last = bi == nbk - 1;
-    const uint64_t sub_end = last ? we : SIM_START + (S.bw_div.div(ws - SIM_START) + bi + 1) * S.BW;
-    // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
-    //      runs at >= we, which join this round's new runs for it in the spare slab) ----
-    const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
-    // the slab's fill and its first GATHER_SPEC records in ONE round trip: the records are
-    // loaded before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
-    // appends to a bucket's slab while its window runs (new runs for the window's last
-    // bucket go to the spare slab set). Only GATHER_SPEC lanes load speculatively: a slab
-    // holds ~4 runs on average, and loading all 64 slots pulled 2 KB of cold HBM lines per
-    // slab (PMC fetch 58 -> 342 MB per launch); fuller slabs load the rest below.
-    SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
-    EvRec r0{};
-    if (lane < GATHER_SPEC) r0 = ld_dev_rec(pb + lane);
-    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
-    lcnt[lane] = 0;
-    uint32_t N = 0;
+  // Append the runs of one slab (fill n, its first GATHER_SPEC records already in r0) that
+  // are due to lev[N..]; in the window's last bucket the runs at >= we move to the spare slab.
+  auto gather_slab = [&](SGN_GLB const EvRec* pb, const EvRec& r0, uint32_t n, bool last, uint32_t& N) {
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
       const uint32_t j = j0 + lane;
       EvRec r = r0;
@@ -1743,10 +1726,56 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
         }
       }
     }
+  };
+  auto slab_done = [&](size_t ib, uint32_t n) {
     if (lane == 0) {
       st_dev(&S.slab_n[ib], 0u);  // consumed (or moved); nobody appends to it this round
       if (n) __hip_atomic_fetch_max(&S.w_cnt[W_MAXFILL * S.G + g], (uint64_t)n, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
+    }
+  };
+  for (uint32_t bi = 0; bi < nbk; bi++) {
+    const uint64_t c0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t b = (bs + bi) & (S.NB - 1);
+    bool last = bi == nbk - 1;
+    uint64_t sub_end = last ? we : SIM_START + (S.bw_div.div(ws - SIM_START) + bi + 1) * S.BW;
+    // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
+    //      runs at >= we, which join this round's new runs for it in the spare slab) ----
+    const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
+    // the slab's fill and its first GATHER_SPEC records in ONE round trip: the records are
+    // loaded before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
+    // appends to a bucket's slab while its window runs (new runs for the window's last
+    // bucket go to the spare slab set). Only GATHER_SPEC lanes load speculatively: a slab
+    // holds ~4 runs on average, and loading all 64 slots pulled 2 KB of cold HBM lines per
+    // slab (PMC fetch 58 -> 342 MB per launch); fuller slabs load the rest below.
+    // A window that straddles one bucket boundary (the common case) loads both slabs in
+    // that round trip and, when both fit in LDS, runs as one sub-window: one sort, one
+    // event-loop pass (the runs of the second bucket are all later than the first's).
+    const bool pair = bi == 0 && nbk == 2;
+    SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
+    EvRec r0{}, r1{};
+    size_t ib1 = 0;
+    SGN_GLB const EvRec* pb1 = nullptr;
+    if (pair) {
+      ib1 = (size_t)(S.NB <= LDS_BSLAB ? lbs[(b + 1) & (S.NB - 1)] : ld_dev(&S.bucket_slab[(b + 1) & (S.NB - 1)])) * S.G + g;
+      pb1 = S.pool + ib1 * S.CAP;
+    }
+    if (lane < GATHER_SPEC) {
+      r0 = ld_dev_rec(pb + lane);
+      if (pair) r1 = ld_dev_rec(pb1 + lane);
+    }
+    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
+    const uint32_t n1 = pair ? min(ld_dev(&S.slab_n[ib1]), S.CAP) : 0u;
+    lcnt[lane] = 0;
+    uint32_t N = 0;
+    gather_slab(pb, r0, n, last, N);
+    slab_done(ib, n);
+    if (pair && n + n1 <= S.CAP) {
+      gather_slab(pb1, r1, n1, true, N);
+      slab_done(ib1, n1);
+      bi = 1;  // the second bucket is done: this is the window's last sub-window
+      last = true;
+      sub_end = we;
     }
     N_all += N;
     __syncthreads();
