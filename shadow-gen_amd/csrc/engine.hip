@@ -1749,9 +1749,11 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     // holds ~4 runs on average, and loading all 64 slots pulled 2 KB of cold HBM lines per
     // slab (PMC fetch 58 -> 342 MB per launch); fuller slabs load the rest below.
     // A window that straddles one bucket boundary (the common case) loads both slabs in
-    // that round trip and, when both fit in LDS, runs as one sub-window: one sort, one
-    // event-loop pass (the runs of the second bucket are all later than the first's).
-    const bool pair = bi == 0 && nbk == 2;
+    // that round trip and, when both fit one 64-run pass, runs as one sub-window: one sort,
+    // one event-loop pass (the runs of the second bucket are all later than the first's).
+    // (compiled into the PERIODIC kernel only: same-box A/B, config B +25 %, while C's TGEN
+    // kernel — whose rounds are set by its servers' trains — measured 0.7 % slower with it)
+    const bool pair = kApp == SGN_TRAFFIC_PERIODIC && bi == 0 && nbk == 2;
     SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
     EvRec r0{}, r1{};
     size_t ib1 = 0;
@@ -1770,7 +1772,9 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     uint32_t N = 0;
     gather_slab(pb, r0, n, last, N);
     slab_done(ib, n);
-    if (pair && n + n1 <= S.CAP) {
+    // (merged only while the pair fits one 64-run pass: config D's slabs hold ~64 runs each,
+    // and merging them made its longer per-lane rank sorts cost more than the pass saved)
+    if (pair && n + n1 <= min(S.CAP, 64u)) {
       gather_slab(pb1, r1, n1, true, N);
       slab_done(ib1, n1);
       bi = 1;  // the second bucket is done: this is the window's last sub-window
