@@ -2345,7 +2345,9 @@ __device__ __forceinline__ void advance_window(const DevSim& S, Ctrl* C) {
   C->rounds++;
 }
 
-constexpr uint32_t kImportBlocks = 128;
+// few blocks: the round's received runs are a few thousand, and every block counts itself in
+// with a device atomic on one word
+constexpr uint32_t kImportBlocks = 16;
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
   // every block reads the same values: nothing changes them before all blocks count in
