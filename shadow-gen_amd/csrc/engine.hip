@@ -1124,9 +1124,29 @@ struct HostExec {
       run = n;
       eid += n;
     } else {
-      // x >> 11 >= T  <=>  x >= T << 11 (T < 2^53); four draws per test in the common case
+      // x >> 11 >= T  <=>  x >= T << 11 (T < 2^53); eight, then four draws per test
       const uint64_t Tx = T << 11;
       uint32_t sent = 0, j = 0;
+      // eight draws per test (same-box A/B on config C: +1.3 % over four, sixteen was slower;
+      // the loop's scalar control and test sit on the slowest waves' chain)
+      for (; j + 8 <= n; j += 8) {
+        const uint64_t x0 = rng_next(), x1 = rng_next(), x2 = rng_next(), x3 = rng_next();
+        const uint64_t x4 = rng_next(), x5 = rng_next(), x6 = rng_next(), x7 = rng_next();
+        if ((x0 >= Tx) | (x1 >= Tx) | (x2 >= Tx) | (x3 >= Tx) | (x4 >= Tx) | (x5 >= Tx) | (x6 >= Tx) |
+            (x7 >= Tx)) {
+          loss_step(x0 >= Tx, run, sent, dst, deliver);
+          loss_step(x1 >= Tx, run, sent, dst, deliver);
+          loss_step(x2 >= Tx, run, sent, dst, deliver);
+          loss_step(x3 >= Tx, run, sent, dst, deliver);
+          loss_step(x4 >= Tx, run, sent, dst, deliver);
+          loss_step(x5 >= Tx, run, sent, dst, deliver);
+          loss_step(x6 >= Tx, run, sent, dst, deliver);
+          loss_step(x7 >= Tx, run, sent, dst, deliver);
+        } else {
+          run += 8;
+          sent += 8;
+        }
+      }
       for (; j + 4 <= n; j += 4) {
         const uint64_t x0 = rng_next(), x1 = rng_next(), x2 = rng_next(), x3 = rng_next();
         if ((x0 >= Tx) | (x1 >= Tx) | (x2 >= Tx) | (x3 >= Tx)) {
