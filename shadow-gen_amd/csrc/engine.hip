@@ -1120,6 +1120,7 @@ struct HostExec {
     } else if (!can_drop || T >= (1ULL << 53)) {
       // nothing can drop (bootstrapping, empty payload, or a lossless path: chance < 1.0 =
       // reliability always); the draws still advance the stream (worker.rs:366 draws first)
+#pragma unroll 8
       for (uint32_t j = 0; j < n; j++) rng_skip();
       run = n;
       eid += n;
