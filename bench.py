@@ -391,28 +391,32 @@ def main():
         # D (every host sends every 1 ms, 7/8 of it to other shards): ~1e6 x 7/8 / 7 runs per
         # peer per round at 1M hosts per GPU, so its slot holds 2^18 runs (8 MB per peer)
         ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 18 if args.workload == "D" else 1 << 13))
-    # with the communicator set, the APSP build is sharded: each GPU computes its block of
-    # used sources and the blocks are exchanged over RCCL
+    # with the communicator set, large graphs (>= 2048 used nodes) build the APSP sharded: each
+    # GPU computes its block of used sources and the blocks are exchanged over RCCL
+    # (DESIGN.md §5); smaller ones build it whole on every GPU (~1 ms)
     ctx.routes_build(g, used)
     apsp_first = ctx.routes_timing()  # includes loading the APSP kernels' code object
     ctx.routes_build(g, used)         # steady state: the build time proper
     apsp = ctx.routes_timing()
     apsp_shard = None
     if world > 1:
-        # the sharded table against one built whole on this GPU (SGN_APSP_REPLICATED), bit for bit
-        lat_s, loss_s = ctx.routes_copy()
-        os.environ["SGN_APSP_REPLICATED"] = "1"
+        # the other form, timed the same way (second build), bit for bit against the first
+        lat_a, loss_a = ctx.routes_copy()
+        other = "SGN_APSP_REPLICATED" if apsp["shards"] > 1 else "SGN_APSP_SHARDED"
+        os.environ[other] = "1"
         ctx.routes_build(g, used)
-        whole = ctx.routes_timing()
-        lat_w, loss_w = ctx.routes_copy()
-        del os.environ["SGN_APSP_REPLICATED"]
-        same = bool(np.array_equal(lat_s, lat_w) and np.array_equal(loss_s.view(np.uint32), loss_w.view(np.uint32)))
+        ctx.routes_build(g, used)
+        alt = ctx.routes_timing()
+        lat_b, loss_b = ctx.routes_copy()
+        del os.environ[other]
+        same = bool(np.array_equal(lat_a, lat_b) and np.array_equal(loss_a.view(np.uint32), loss_b.view(np.uint32)))
         import torch
         f = torch.tensor([0 if same else 1], dtype=torch.int64)
         dist.all_reduce(f, op=dist.ReduceOp.SUM)
-        apsp_shard = {"shards": apsp["shards"], "equal_on_all_ranks": int(f.item()) == 0,
-                      "replicated_ms": round(whole["total_ms"], 3), "sharded_ms": round(apsp["total_ms"], 3)}
-        ctx.routes_build(g, used)  # the sharded table again for the run
+        sh, rep = (apsp, alt) if apsp["shards"] > 1 else (alt, apsp)
+        apsp_shard = {"shards": sh["shards"], "equal_on_all_ranks": int(f.item()) == 0,
+                      "default_form": "sharded" if apsp["shards"] > 1 else "replicated",
+                      "replicated_ms": round(rep["total_ms"], 3), "sharded_ms": round(sh["total_ms"], 3)}
     ctx.hosts_set(hosts)
     ctx.sim_init(cfg, tr)
 

@@ -807,12 +807,17 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     // form a block of row tiles per pass, exchanged after each pass — and the table's blocks are
     // exchanged at the end, so every shard holds the whole table; all shards must call
     // sgn_routes_build with the same graph. The u64 Floyd-Warshall (a chain of pivot steps)
-    // runs whole on every shard. SGN_APSP_REPLICATED=1: every shard builds the table alone.
+    // runs whole on every shard. The split is used from kApspShardMinU used nodes on: below it
+    // the whole build takes ~1 ms on one GPU and the per-pass and final exchanges cost more
+    // than the share of work they save (replicated is acceptable at V <= 2k);
+    // SGN_APSP_SHARDED=1 forces the split, SGN_APSP_REPLICATED=1 forbids it.
     // SGN_APSP_VSHARDS=n without a communicator (a test hook): one process runs the n blocks
     // in turn over one buffer, which checks the block arithmetic on one GPU.
     uint32_t nsh = 1, me = 0;
     bool rccl = false;
-    if (ctx->comm && ctx->nranks > 1 && !getenv("SGN_APSP_REPLICATED")) {
+    constexpr uint32_t kApspShardMinU = 2048;
+    if (ctx->comm && ctx->nranks > 1 && !getenv("SGN_APSP_REPLICATED") &&
+        (U >= kApspShardMinU || getenv("SGN_APSP_SHARDED"))) {
       nsh = ctx->nranks;
       me = ctx->rank;
       rccl = true;
