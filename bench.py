@@ -13,6 +13,9 @@ at its destination. value = all ranks' packet events / max-ra
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, hosts sharded, RCCL exchange inside libsgn).
+Scaling is STRONG by default: the workload's hosts (C: 100k) are sharded over the N GPUs,
+as BASELINE.json names config C ("100k synthetic hosts ... sharded over 8 GPUs");
+--weak gives every GPU --hosts hosts instead.
 """
 import argparse
 import json
@@ -329,7 +332,12 @@ def main():
     ap.add_argument("--workload", choices=("B", "C", "D"), default="C",
                     help="C: the headline 100k-host Tor-like tgen workload; B: 10k hosts, UDP every 10 ms "
                          "on a random graph; D: 1M hosts, dense all-to-all")
-    ap.add_argument("--hosts", type=int, default=None, help="hosts per GPU (B: 10k, C: 100k, D: 1M)")
+    ap.add_argument("--hosts", type=int, default=None,
+                    help="hosts in the simulation (B: 10k, C: 100k, D: 1M), sharded over the GPUs; "
+                         "with --weak: hosts per GPU")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: --hosts hosts on every GPU (the default is strong scaling: "
+                         "--hosts in total, sharded over the GPUs)")
     ap.add_argument("--nodes", type=int, default=1000)
     ap.add_argument("--rounds-per-step", type=int, default=100)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0,
@@ -360,7 +368,8 @@ def main():
         dist.init_process_group("gloo", init_method="env://")
     if args.hosts is None:
         args.hosts = {"B": 10_000, "C": 100_000, "D": 1_000_000}[args.workload]
-    n_total = args.hosts * world
+    n_total = args.hosts * world if args.weak else args.hosts
+    n_shard = -(-n_total // world)  # hosts per GPU (the last shard may hold fewer)
     if args.workload == "C":
         g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
     elif args.workload == "B":
@@ -370,8 +379,11 @@ def main():
         # calendar slabs of 128 runs per host group and bucket: ~64 due on average, 108 at most
         # measured (a 128-run slab keeps the round kernel at 6 workgroups per CU; overflow is
         # detected and reported, never silent)
-        groups = -(-args.hosts // 64)
+        groups = -(-n_shard // 64)
         cfg.event_capacity = 257 * groups * 128
+    if cfg.event_capacity and world > 1 and not args.weak and args.workload != "D":
+        # the calendar is sized per shard: the same slabs per host group as the one-GPU run
+        cfg.event_capacity = -(-cfg.event_capacity // world)
 
     if args.codel_cap:
         cfg.codel_cap = args.codel_cap
@@ -488,7 +500,7 @@ def main():
             t = json.loads(tf.read_text())
             wl = t.get("workload", {})
             if (wl.get("name"), wl.get("hosts_per_gpu"), wl.get("graph_nodes"), wl.get("rounds_per_launch"),
-                    wl.get("n_gpus"), t.get("kernel")) == (args.workload, args.hosts, args.nodes, round(rpl), world, rk):
+                    wl.get("n_gpus"), t.get("kernel")) == (args.workload, n_shard, args.nodes, round(rpl), world, rk):
                 roof["traffic"] = t["traffic_bytes_per_launch"]
                 roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
                 roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
@@ -515,7 +527,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
@@ -524,7 +536,7 @@ def main():
                          "B": "B: 1000-node random graph (20 % lossy edges), 1024 B UDP every 10 ms to random peers",
                          "D": "D: 1000-node random graph, every host sends 64 B to a uniform random peer every 1 ms",
                          }[args.workload],
-            "hosts_per_gpu": args.hosts, "hosts_total": n_total, "graph_nodes": args.nodes,
+            "hosts_per_gpu": n_shard, "hosts_total": n_total, "graph_nodes": args.nodes,
             "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
             "parallelism": f"host-shard x{world}" + (" (one-GPU rehearsal: all ranks on device 0, RCCL socket transport)" if args.one_gpu else ""),
         },

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 6
+#define SGN_ABI_VERSION 7
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -62,7 +62,7 @@ typedef struct sgn_create_opts {
   uint32_t flags;      /* SGN_CREATE_* */
 } sgn_create_opts;
 
-#define SGN_CREATE_TIME_KERNELS 1u /* record HIP events around every launch (sgn_kernel_times) */
+#define SGN_CREATE_TIME_KERNELS 1u /* HIP events around the engine's launches (a sample: sgn_kernel_times) */
 #define SGN_CREATE_TIME_EXECUTE 2u /* ... around the per-host execute kernel only */
 
 /* Creates a context bound to one GPU. Replaces WorkerShared construction
@@ -344,7 +344,9 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* batch);
  * the controller thread then submits every stage with one sgn_stage_flush between rounds.
  * A flush is exactly one sgn_submit of the stages' datagrams concatenated in stage-creation
  * order (each stage in push order); on failure nothing is queued and the stages keep their
- * datagrams. Create and destroy stages only while no flush runs. */
+ * datagrams. A push that runs while a flush runs is either part of that flush or stays
+ * staged for the next one (a flush clears only what it copied). Create and destroy stages
+ * only while no flush runs. */
 typedef struct sgn_stage sgn_stage;
 int sgn_stage_create(sgn_ctx* ctx, sgn_stage** out);
 void sgn_stage_destroy(sgn_stage* stage);
@@ -433,15 +435,31 @@ typedef struct sgn_engine_info {
                                     records: free + chained == codel_pages, no page lost) */
   uint64_t compute_units;        /* of this context's GPU */
   uint64_t bucket_min_lds;       /* 1: round kernels fold bucket minima in LDS first */
+  /* ABI 7: device pools grow instead of refusing a scenario (the reference's queues are
+   * unbounded, codel_queue.rs:33,303-317, event_queue.rs:57-66). A round that could need more
+   * than a pool holds is held at its start (nothing of it has run), the pool grows between
+   * launches, and the round runs. */
+  uint64_t lds_per_cu;           /* LDS bytes per CU the residency model used (device attribute) */
+  uint64_t codel_pool_grows;     /* CoDel page pool enlargements */
+  uint64_t calendar_grows;       /* calendar re-layouts with larger slabs */
+  uint64_t calendar_spill_runs;  /* runs that went to the calendar's spill area (then re-filed) */
+  uint64_t exchange_slot_grows;  /* multi-shard exchange slot enlargements */
+  uint64_t rounds_held;          /* rounds held at their start for a pool to grow */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 
-/* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS). */
+/* Device timing of the engine's kernels since sim_init (needs SGN_CREATE_TIME_KERNELS or
+ * SGN_CREATE_TIME_EXECUTE). Persistent launches (k_rounds, many rounds each) are all timed;
+ * per-round launches are timed one in eight (an event pair around every launch cost ~20 % of
+ * the rounds), so launches[k] / ms[k] cover that sample: the average duration is
+ * ms[k] / launches[k], and launches_total[k] counts every launch (timed or not) to scale
+ * it to the total. */
 typedef struct sgn_kernel_times {
-  uint64_t launches[16];
-  double ms[16];
+  uint64_t launches[16];         /* timed launches */
+  double ms[16];                 /* their summed duration */
   const char* name[16];
   uint32_t n_kernels;
+  uint64_t launches_total[16];   /* every launch since sim_init (ABI 7) */
 } sgn_kernel_times;
 int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out);
 

@@ -43,6 +43,17 @@ void* dev_alloc(sgn_ctx* ctx, size_t bytes, bool zero) {
   return p;
 }
 
+// frees one dev_alloc'ed buffer before free_sim (a pool replaced by a larger one)
+void dev_free(sgn_ctx* ctx, void* p, size_t bytes) {
+  if (!p) return;
+  auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), p);
+  if (it == ctx->allocs.end()) return;
+  ctx->allocs.erase(it);
+  hipFree(p);
+  if (bytes == 0) bytes = 16;
+  ctx->sim_bytes -= std::min<uint64_t>(ctx->sim_bytes, bytes);
+}
+
 }  // namespace sgn
 
 sgn_ctx::~sgn_ctx() {

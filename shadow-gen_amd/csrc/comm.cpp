@@ -74,9 +74,10 @@ int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES], uint64_t sl
 
 namespace sgn {
 int ctrl_sync(sgn_ctx* ctx);  // engine.hip: the control block to the host, overflow check
+int resolve_pools(sgn_ctx* ctx);  // engine.hip: a held round edge's pool growth
 
 uint64_t comm_round_bytes(const sgn_ctx* ctx) {
-  return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)(1 + ctx->xsz_cur) * sizeof(EvRec)) : 0;
+  return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)(XHDR + ctx->xsz_cur) * sizeof(EvRec)) : 0;
 }
 
 // ONE grouped send/recv: per peer one message of the 32-byte round-edge record and the first
@@ -86,8 +87,8 @@ static int exchange(sgn_ctx* ctx, uint32_t sz) {
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   hipStream_t st = ctx->stream;
   // a peer's block: the message (one 32-byte record), then the runs
-  const size_t bytes = (size_t)(1 + sz) * sizeof(EvRec);
-  const size_t blk = (size_t)S.xslot + 1;
+  const size_t bytes = (size_t)(XHDR + sz) * sizeof(EvRec);
+  const size_t blk = (size_t)S.xslot + XHDR;
   ncclResult_t r = ncclGroupStart();
   for (uint32_t p = 0; p < S.n_ranks && r == ncclSuccess; p++) {
     if (p == S.rank) continue;
@@ -125,7 +126,7 @@ int comm_complete_spill(sgn_ctx* ctx) {
   SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xsz, (int)S.xslot, 1, st));
   SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xspill, 0, 1, st));
   if (int rc = exchange(ctx, S.xslot)) return rc;
-  ctx->x_bytes += (uint64_t)(ctx->nranks - 1) * ((uint64_t)(1 + S.xslot) * sizeof(EvRec));
+  ctx->x_bytes += (uint64_t)(ctx->nranks - 1) * ((uint64_t)(XHDR + S.xslot) * sizeof(EvRec));
   launch_import(ctx);
   uint64_t want = std::max<uint64_t>(2 * ctx->h_ctrl->xhwm, kXszInit);
   uint64_t sz = kXszInit;
@@ -225,15 +226,15 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
     // message b (what comm_round_exchange's grouped send/recv does)
     for (uint32_t a = 0; a < n; a++) {
       sgn_ctx* A = ctxs[a];
-      const size_t blk = (size_t)A->S.xslot + 1;
+      const size_t blk = (size_t)A->S.xslot + XHDR;
       for (uint32_t b = 0; b < n; b++) {
         if (b == a) continue;
         sgn_ctx* B = ctxs[b];
-        uint64_t msg[4];
-        SGN_HIP(A, hipMemcpy(msg, (const void*)(A->S.xout + (size_t)b * blk), 32, hipMemcpyDeviceToHost));
+        uint64_t msg[4 * XHDR];
+        SGN_HIP(A, hipMemcpy(msg, (const void*)(A->S.xout + (size_t)b * blk), sizeof(msg), hipMemcpyDeviceToHost));
         const uint64_t k = std::min<uint64_t>(msg[0], A->xslot);
         SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * blk), (const void*)(A->S.xout + (size_t)b * blk),
-                             (size_t)(1 + k) * sizeof(EvRec), hipMemcpyDefault));
+                             (size_t)(XHDR + k) * sizeof(EvRec), hipMemcpyDefault));
       }
     }
     for (uint32_t i = 0; i < n; i++) {
@@ -241,6 +242,12 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       SGN_HIP(c, hipSetDevice(c->device));
       launch_import(c);
       SGN_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    // a held round edge (the same on every shard) or a spill: the pools grow before the next
+    for (uint32_t i = 0; i < n; i++) {
+      int rc = ctrl_sync(ctxs[i]);
+      if (!rc) rc = resolve_pools(ctxs[i]);
+      if (rc) return rc;
     }
   }
   if (rounds_done) *rounds_done = done;

@@ -286,7 +286,24 @@ struct Outbox {
   uint64_t bbase;             // ... as offsets from this time (the round's window start)
   uint64_t pg_avail;          // CoDel page pool: free-ring entries allocations may use this round
   SGN_GLB uint64_t* pg_freed; // ... and the round's freed-page counter
+  SGN_GLB uint64_t* pg_allocd;// ... and allocated-page counter (the round edge's guard)
+  SGN_GLB uint64_t* spilled;  // runs this round put in the calendar's spill area
 };
+
+// A run whose calendar slab is full goes to the spill area with its slab index (lossless; the
+// round edge holds and the host re-lays the calendar out before the run can be due). Only a
+// full spill area is an overflow.
+__device__ __forceinline__ void spill_run(const DevSim& S, Outbox* ob, uint32_t idx, const EvRec& r) {
+  SGN_GLB Ctrl* C = S.ctrl;
+  const uint64_t i = __hip_atomic_fetch_add(&C->spill_n, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ob) cnt_add(ob->spilled, 1);
+  if (i < S.spill_cap) {
+    st_dev_rec(S.spill + i, r);
+    st_dev(&S.spill_idx[i], idx);
+  } else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0) {
+    C->overflow_info = r.dst;
+  }
+}
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
 // pad every lane's slot to a multiple of 16 B and cost a workgroup per CU)
@@ -336,6 +353,7 @@ struct HostExec {
   uint32_t fq_head, fq_len;
   // per-round counter increments (a host cannot see 2^32 events in one window)
   uint32_t c_sent, c_loss, c_popped, c_deliv, c_localev, c_maxcodel;
+  uint32_t c_runs;  // event runs this host appended to this shard's calendar (occupancy)
   uint64_t c_bytes;
   // CoDel run cache: the head run being consumed and the tail run being extended live in
   // registers; their ring slots are stale until store() (or until the tail is closed).
@@ -410,6 +428,7 @@ struct HostExec {
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
+    c_runs = 0;
     c_maxcodel = r.max_codel;
     hd_valid = tl_open = false;
     if (cq_nr > 0) {
@@ -647,6 +666,7 @@ struct HostExec {
   // (the entries of the current round are still being written by other waves)
   __device__ __forceinline__ uint32_t cq_alloc_page() {
     const uint64_t i = __hip_atomic_fetch_add(&C->pg_alloc, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cnt_add(ob->pg_allocd, 1);
     if (i >= ob->pg_avail) return NO_HOST;
     return ld_dev(&S.cq_free[i % S.cq_pages]);
   }
@@ -1177,12 +1197,14 @@ struct HostExec {
     SGN_GLB EvRec* dstp;
     uint32_t cap;
     uint32_t pos;
+    uint32_t sidx = 0;  // owned: the slab index (its spill tag)
     const bool owned = dst - S.lo < S.nH;
     if (owned) {
       if (deliver >= ob->hz) {  // past the calendar's horizon (sim_init sizes NB so it cannot be)
         overflow(OVF_HORIZON);
         return;
       }
+      c_runs += nrec;
       const uint32_t b = bucket_of(S, deliver);
       const uint32_t slab = b == b1 ? keep_slab : (S.NB <= LDS_BSLAB ? bslab[b] : ld_dev(&S.bucket_slab[b]));
       const size_t idx = (size_t)slab * S.G + ((dsid - S.lo) >> S.gsh);
@@ -1214,6 +1236,7 @@ struct HostExec {
       DGT_END(DGT_SLAB, tsl);
       dstp = S.pool + idx * S.CAP;
       cap = S.CAP;
+      sidx = (uint32_t)idx;
     } else {
       uint32_t lo = 0, hi = S.n_ranks;
       while (hi - lo > 1) {
@@ -1222,11 +1245,11 @@ struct HostExec {
       }
       atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
       pos = atomicAdd(&S.xout_n[lo], nrec);
-      dstp = S.xout + (size_t)lo * (S.xslot + 1) + 1;  // record 0 of a peer's block: the message
+      dstp = S.xout + (size_t)lo * (S.xslot + XHDR) + XHDR;  // (a peer's block starts with the message)
       cap = S.xslot;
     }
-    if (pos + nrec > cap) {
-      overflow(owned ? OVF_BUCKET : OVF_EXCHANGE);
+    if (!owned && pos + nrec > cap) {
+      overflow(OVF_EXCHANGE);
       return;
     }
     for (uint32_t m = 0; m < nrec; m++) {
@@ -1238,7 +1261,10 @@ struct HostExec {
       r.dst = dsid;
       r.pc = payload | (k << 16);
       r.tag = tag;
-      st_dev_rec(dstp + pos + m, r);
+      if (pos + m < cap)
+        st_dev_rec(dstp + pos + m, r);
+      else  // (owned: the slab is full)
+        spill_run(S, ob, sidx, r);
     }
   }
 
@@ -1541,6 +1567,25 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return (uint32_t)__popcll(lane ? (m & ((~0ULL) >> (64 - lane))) : 0ULL);
 }
 
+// The CoDel pages a round over [ws, we) may take. A page is taken only when a CoDel push
+// opens a new run on a full tail page (codel_push_run), and every push is one due event run:
+// a host receiving k runs takes at most ceil(k / 16) pages, so the round takes at most
+// (D + 15 min(D, hosts)) / 16 for D due runs — at most the calendar's runs (occupancy) and at
+// most the slabs of the buckets the window overlaps. A round edge whose free pages fall below
+// this holds before the round (Ctrl::hold) and the host grows the pool: a CoDel queue never
+// refuses a packet (codel_queue.rs:33,303-317 has no limit).
+__host__ __device__ __forceinline__ uint64_t codel_pages_bound(uint64_t due, uint64_t hosts) {
+  return (due + 15 * (due < hosts ? due : hosts) + 15) / 16;
+}
+__device__ __forceinline__ uint64_t codel_round_bound(const DevSim& S, uint64_t occ, uint64_t ws, uint64_t we) {
+  const uint32_t nbk = ((bucket_of(S, we - 1) - bucket_of(S, ws)) & (S.NB - 1)) + 1;
+  const uint64_t capb = (uint64_t)nbk * S.G * S.CAP;
+  return codel_pages_bound(occ < capb ? occ : capb, S.nH);
+}
+__device__ __forceinline__ uint64_t pages_free(uint64_t avail, uint64_t alloc) {
+  return avail > alloc ? avail - alloc : 0;
+}
+
 // finalize_round for the fused single-shard path, run by the last wave of k_execute: the
 // waves' minima come from the chunk slots; every value another wave changed during this
 // launch is read with a device-scope atomic (plain loads could hit a stale L2 line).
@@ -1554,12 +1599,13 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
   // one round trip: every value to read (chunk minima, spare-slab minimum, bucket minima,
   // lowest used latency) is fetched at once; the buckets [b0, b1) are consumed and b1 is
   // replaced, so neither is read
-  uint64_t kk = INVALID, wn = INVALID, m = INVALID;
+  uint64_t kk = INVALID, wn = INVALID, m = INVALID, od = 0;
   for (uint32_t i = lane; i < nch; i += 64) {
     const uint64_t a = __hip_atomic_exchange(&S.fin_keep[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t b = __hip_atomic_exchange(&S.fin_next[i], (unsigned long long)INVALID,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    od += __hip_atomic_exchange(&S.fin_occ[i], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     kk = a < kk ? a : kk;
     wn = b < wn ? b : wn;
   }
@@ -1579,6 +1625,8 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
   kk = wave_min_u64(kk);
   wn = wave_min_u64(wn);
   m = wave_min_u64(m);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) od += shfl_xor64(od, off);
   // then the writes (the caller drains them before publishing the round edge)
   for (uint32_t i = lane; i <= nch; i += 64) st_dev(&S.fin_cnt[i], 0u);
   if (lane == 0) {
@@ -1591,26 +1639,39 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     st_dev(&S.bucket_min[b1], nb1);
     // CoDel page pool: the pages freed this round become allocatable in the next
     const uint64_t fr = __hip_atomic_exchange(&C->pg_freed, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (fr) st_dev(&C->pg_avail, ld_dev(&C->pg_avail) + fr);
+    const uint64_t avail = ld_dev(&C->pg_avail) + fr;
+    if (fr) st_dev(&C->pg_avail, avail);
+    const uint64_t occ = ld_dev(&C->cal_occ) + od;  // (wraps back from a negative sum)
+    st_dev(&C->cal_occ, occ);
+    const uint64_t pfree = pages_free(avail, ld_dev(&C->pg_alloc));
+    const bool spilled = ld_dev(&C->spill_n) != 0;
     m = nb1 < m ? nb1 : m;
     m = wn < m ? wn : m;
     if (local) {
       // word 3: this shard's largest per-peer run count this round (every shard compares the
-      // maxima of all shards with the exchange size: the same decision everywhere)
-      uint64_t xmax = 0;
+      // maxima of all shards with the exchange size: the same decision everywhere), with the
+      // spill flag in its high half; words 4-7 let every shard evaluate every shard's CoDel
+      // guard for the next window alike (k_import): free pages, calendar occupancy, runs
+      // exported this round (a bound on what any shard receives), slab runs per bucket
+      uint64_t xmax = 0, xsum = 0;
       for (uint32_t p = 0; p < S.n_ranks; p++) {
         const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
         xmax = cnt > xmax ? cnt : xmax;
+        xsum += cnt;
       }
       for (uint32_t p = 0; p < S.n_ranks; p++) {
         const uint64_t cnt = p == S.rank ? 0 : ld_dev(&S.xout_n[p]);
-        // record 0 of the peer's outgoing block (travels with the runs); this shard's own in
-        // its incoming block, where k_import reads every shard's message
-        SGN_GLB uint64_t* o = (SGN_GLB uint64_t*)((p == S.rank ? S.xin : S.xout) + (size_t)p * (S.xslot + 1));
+        // the message records of the peer's outgoing block (travel with the runs); this
+        // shard's own in its incoming block, where k_import reads every shard's message
+        SGN_GLB uint64_t* o = (SGN_GLB uint64_t*)((p == S.rank ? S.xin : S.xout) + (size_t)p * (S.xslot + XHDR));
         st_dev(o, cnt);
         st_dev(o + 1, m);
         st_dev(o + 2, mu);
-        st_dev(o + 3, xmax);
+        st_dev(o + 3, (uint64_t)(xmax | ((spilled ? 1ULL : 0ULL) << 32)));
+        st_dev(o + 4, pfree);
+        st_dev(o + 5, occ);
+        st_dev(o + 6, xsum);
+        st_dev(o + 7, (uint64_t)S.G * S.CAP);
       }
       return;
     }
@@ -1624,6 +1685,14 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
     if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
     ne = ne < S.end_time ? ne : S.end_time;
     st_dev(&C->active, min_next < ne ? 1u : 0u);
+    if (min_next < ne) {  // the next round's guards (hold before it runs)
+      const uint64_t need = codel_round_bound(S, occ, min_next, ne);
+      const uint32_t hold = (pfree < need ? HOLD_CODEL : 0u) | (spilled ? HOLD_SPILL : 0u);
+      if (hold) {
+        st_dev(&C->hold, hold);
+        st_dev(&C->hold_need, need);
+      }
+    }
     st_dev(&C->prev_we, we);
     st_dev(&C->ws, min_next);
     st_dev(&C->we, ne);
@@ -1647,8 +1716,7 @@ struct ExecLDS {
   uint16_t* lb;       // grouped by destination lane (unordered)
   uint16_t* lc;       // ... ordered inside each destination segment
   uint32_t* lcnt;
-  uint32_t* lstart;
-  uint32_t* lcur;
+  uint32_t* lcur;     // placement cursors (after placement: segment ends, start = end - count)
   LaneLDS* lslot;     // the lanes' LDS slots
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   Outbox* ob;         // the wave's outbox
@@ -1676,7 +1744,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint16_t* lb = X.lb;
   uint16_t* lc = X.lc;
   uint32_t* lcnt = X.lcnt;
-  uint32_t* lstart = X.lstart;
   uint32_t* lcur = X.lcur;
   LaneLDS* lslot = X.lslot;
   uint16_t* lbs = X.lbs;
@@ -1741,8 +1808,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
             const uint32_t base = atomicAdd(&S.slab_n[ik], 1u);
             if (base < S.CAP)
               st_dev_rec(pk + base, r);
-            else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-              C->overflow_info = r.dst;
+            else
+              spill_run(S, ob, (uint32_t)ik, r);
           }
         }
       }
@@ -1787,8 +1854,15 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       r0 = ld_dev_rec(pb + lane);
       if (pair) r1 = ld_dev_rec(pb1 + lane);
     }
-    const uint32_t n = min(ld_dev(&S.slab_n[ib]), S.CAP);
-    const uint32_t n1 = pair ? min(ld_dev(&S.slab_n[ib1]), S.CAP) : 0u;
+    const uint32_t nraw = ld_dev(&S.slab_n[ib]);
+    const uint32_t n1raw = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
+    const uint32_t n = min(nraw, S.CAP);
+    const uint32_t n1 = min(n1raw, S.CAP);
+    // a slab with runs in the spill area: the calendar was not re-laid out before the runs are
+    // due (single shard: impossible, the round edge holds first; multi-shard: a spill by
+    // k_import due within the batch) — reported, never silent
+    if (lane == 0 && (nraw > S.CAP || n1raw > S.CAP) && (atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
+      C->overflow_info = gbase;
     lcnt[lane] = 0;
     uint32_t N = 0;
     gather_slab(pb, r0, n, last, N);
@@ -1815,7 +1889,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       if ((int)lane >= off) incl += y;
     }
     const uint32_t start = incl - cnt;
-    lstart[lane] = start;
     lcur[lane] = start;
     __syncthreads();
     for (uint32_t j = lane; j < N; j += 64) {
@@ -1827,7 +1900,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       const uint32_t idx = lb[q];
       const EvRec& r = lev[idx];
       const uint32_t d = r.dst - gbase;
-      const uint32_t a = lstart[d], k = lcnt[d];
+      const uint32_t k = lcnt[d], a = lcur[d] - k;  // (placement left lcur at the segment's end)
       uint32_t rank = 0;
       for (uint32_t t = a; k > 1 && t < a + k; t++) {
         const EvRec& o = lev[lb[t]];
@@ -1881,8 +1954,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
       if (pos < S.CAP)
         st_dev_rec(S.pool + (size_t)idx * S.CAP + pos, ob->rec[i]);
-      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-        C->overflow_info = ob->rec[i].dst;
+      else
+        spill_run(S, ob, idx, ob->rec[i]);
     }
   }
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
@@ -1892,7 +1965,10 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   m = ob->xmin < m ? ob->xmin : m;  // runs exported to other shards are pending events too
   *kmin_out = kmin;
   *next_out = m;
-  at_end(kmin, m);
+  // the calendar's occupancy change: runs this group appended minus the due runs it took out
+  // (the last bucket's later runs moved to the spare slab set count out and in)
+  const uint64_t occd = (uint64_t)wave_sum_u32(loaded ? ex.c_runs : 0u) - (uint64_t)N_all;
+  at_end(kmin, m, occd);
   uint32_t n_ev = 0;
 #ifdef SGN_DIAG
   const uint64_t td = __builtin_amdgcn_s_memtime();
@@ -1965,7 +2041,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 
 #define SGN_EXEC_LDS(X)                                                              \
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];                     \
-  __shared__ uint32_t lcnt_[64], lstart_[64], lcur_[64];                             \
+  __shared__ uint32_t lcnt_[64], lcur_[64];                                         \
   __shared__ LaneLDS lslot_[64];                                                     \
   __shared__ uint16_t lbs_[LDS_BSLAB];                                               \
   __shared__ Outbox ob_;                                                             \
@@ -1975,7 +2051,6 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.lc = X.lb + ((S.CAP + 3) & ~3u);                                                 \
   X.bmin = S.agg_bmin ? (uint32_t*)(X.lc + ((S.CAP + 3) & ~3u)) : nullptr;           \
   X.lcnt = lcnt_;                                                                    \
-  X.lstart = lstart_;                                                                \
   X.lcur = lcur_;                                                                    \
   X.lslot = lslot_;                                                                  \
   X.lbs = lbs_;                                                                      \
@@ -2012,12 +2087,13 @@ __device__ __forceinline__ void flush_bmin(const DevSim& S, const ExecLDS& X) {
 // returning device-scope atomics, then it counts itself in (64 workgroups per chunk counter,
 // then chunks). Only atomics cross between workgroups (no fences: an agent-scope release
 // writes the whole L2 back on gfx950). Returns true (all lanes) for the last arrival.
-__device__ bool arrive(const DevSim& S, uint32_t w, uint32_t nw, uint64_t kmin, uint64_t m) {
+__device__ bool arrive(const DevSim& S, uint32_t w, uint32_t nw, uint64_t kmin, uint64_t m, uint64_t occd) {
   uint32_t last = 0;
   if (threadIdx.x == 0) {
     const uint32_t ch = w >> 6;
     const uint32_t csz = min(64u, nw - (ch << 6));
     const uint32_t nch = (nw + 63) >> 6;
+    if (occd) cnt_add(&S.fin_occ[ch], occd);
     if (kmin != INVALID)
       __hip_atomic_fetch_min(&S.fin_keep[ch], (unsigned long long)kmin, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -2039,13 +2115,15 @@ __device__ bool arrive(const DevSim& S, uint32_t w, uint32_t nw, uint64_t kmin, 
 
 // One round per launch: one workgroup (one wave) per group; single shard: the last arrival
 // runs the round edge (finalize_fused), multi-shard: comm.cpp's exchange follows.
-template <uint32_t kApp>
+// kTrace: the per-packet trace compiled in (traced runs); untraced per-round launches — the
+// multi-shard rounds, sgn_round, the persistent kernel's fallback — use the lean twin.
+template <bool kTrace, uint32_t kApp>
 __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg) {
   // the simulation constants are read from device memory where they are used (a by-value
   // kernel argument would pin ~90 scalar registers for the whole kernel)
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
-  if (!C->active || C->xspill) return;  // multi-shard: a held round waits for the host
+  if (!C->active || C->xspill || C->hold) return;  // a held round waits for the host
   SGN_EXEC_LDS(X)
   const uint64_t ws = C->ws, we = C->we;
   const uint32_t ks = C->keep_slab;
@@ -2056,14 +2134,16 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     X.ob->bbase = C->ws;
     X.ob->pg_avail = C->pg_avail;
     X.ob->pg_freed = &C->pg_freed;
+    X.ob->pg_allocd = &C->rnd_alloc;
+    X.ob->spilled = &C->rnd_spill;
   }
   init_bmin<kApp>(S, X);
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
-  exec_group<true, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+  exec_group<kTrace, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
     flush_bmin<kApp>(S, X);
-    last = arrive(S, blockIdx.x, gridDim.x, k, n);
+    last = arrive(S, blockIdx.x, gridDim.x, k, n, od);
   });
   if (!last) return;
   const uint32_t b1 = bucket_of(S, we - 1);
@@ -2086,13 +2166,14 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
 constexpr uint32_t RB_CH = 64;  // chunk slots per buffer (persistent grids up to 4096 workgroups)
 
 __device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
-                                          uint64_t m) {
+                                          uint64_t m, uint64_t occd) {
   if (threadIdx.x != 0) return;
   const uint32_t ch = w >> 6;
   const uint32_t csz = min(64u, nw - (ch << 6));
   SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * 2;
   if (kmin != INVALID) min_nr(mn, kmin);
   if (m != INVALID) min_nr(mn + 1, m);
+  if (occd) cnt_add(&S.rb_occ[(size_t)p * RB_CH + ch], occd);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
   SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * (RB_CH + 1);
   const uint32_t c = __hip_atomic_fetch_add(&cnt[ch], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2102,16 +2183,20 @@ __device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t 
 // The next window from buffer p after the barrier (every workgroup, identical results).
 struct RbEdge {
   uint64_t ws, we, min_next, nb1;
+  uint64_t occd, nalloc, nfree, nspill;  // the round's calendar occupancy change, CoDel pages
+                                         // allocated / freed, runs spilled (buffer p: stable)
   uint32_t active;
 };
 __device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t nch, uint64_t ws, uint64_t we) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
   uint64_t kk = INVALID, wn = INVALID, m = INVALID, km = INVALID, mu = INVALID;
+  uint64_t od = 0, na = 0, nf = 0, ns = 0;
   if (lane < nch) {
     SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + lane) * 2;
     kk = ld_dev(mn);
     wn = ld_dev(mn + 1);
+    od = ld_dev(&S.rb_occ[(size_t)p * RB_CH + lane]);
   }
   for (uint32_t b = lane; b < S.NB; b += 64) {
     const bool consumed = ((b - b0) & (S.NB - 1)) < ((b1 - b0) & (S.NB - 1)) || b == b1;
@@ -2123,13 +2208,22 @@ __device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t 
   if (lane == 0) {
     km = ld_dev(&S.rb_keep[p]);
     mu = ld_dev(&S.ctrl->min_used);
+    na = ld_dev(&S.rb_occ[3 * RB_CH + p]);
+    ns = ld_dev(&S.rb_occ[3 * RB_CH + 3 + p]);
+    nf = ld_dev(&S.rb_free[p]);
   }
   kk = wave_min_u64(kk);
   wn = wave_min_u64(wn);
   m = wave_min_u64(m);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) od += shfl_xor64(od, off);
   km = shfl64(km, 0);
   mu = shfl64(mu, 0);
   RbEdge e;
+  e.occd = od;
+  e.nalloc = shfl64(na, 0);
+  e.nfree = shfl64(nf, 0);
+  e.nspill = shfl64(ns, 0);
   e.nb1 = km < kk ? km : kk;  // the spare slab set becomes bucket b1
   m = e.nb1 < m ? e.nb1 : m;
   m = wn < m ? wn : m;
@@ -2207,7 +2301,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   // changes by one swap per round, applied by every workgroup to its own LDS copy.
   struct RoundLDS {
     uint64_t ws, we, pend_ws, pend_we, pend_nb1, pg_avail;
-    uint32_t active, ks, pend_new, pend;
+    uint64_t pg_alloc, occ, nspill, hold_need;  // CoDel pages taken, calendar runs, runs spilled
+    uint32_t active, ks, pend_new, pend, ngap, hold;
   };
   __shared__ RoundLDS rs;
   if (threadIdx.x == 0) {
@@ -2217,6 +2312,12 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     rs.active = ld_dev(&C->active);
     rs.ks = ld_dev(&C->keep_slab);
     rs.pend = 0;
+    rs.ngap = 0;
+    rs.pg_alloc = ld_dev(&C->pg_alloc);
+    rs.occ = ld_dev(&C->cal_occ);
+    rs.nspill = ld_dev(&C->spill_n);
+    rs.hold = 0;
+    rs.hold_need = 0;
   }
   const uint64_t rounds0 = ld_dev(&C->rounds);
   const bool lds_tab = S.NB <= LDS_BSLAB;
@@ -2230,7 +2331,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   };
   uint32_t r = 0;
   for (; r < max_rounds; r++) {
-    if (!__builtin_amdgcn_readfirstlane((int)rs.active)) break;
+    // (a held round: the host grows a pool between launches, then the round runs)
+    if (!__builtin_amdgcn_readfirstlane((int)rs.active) || __builtin_amdgcn_readfirstlane((int)rs.hold)) break;
     const uint64_t ws = uni64(rs.ws), we = uni64(rs.we);
     const uint32_t ks = (uint32_t)__builtin_amdgcn_readfirstlane((int)rs.ks);
     const uint32_t p = r % 3;
@@ -2240,9 +2342,12 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       const uint32_t q = (r + 1) % 3;
       for (uint32_t i = threadIdx.x; i < RB_CH * 2; i += 64) st_dev(&S.rb_min[(size_t)q * RB_CH * 2 + i], (uint64_t)INVALID);
       for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64) st_dev(&S.rb_cnt[(size_t)q * (RB_CH + 1) + i], 0u);
+      for (uint32_t i = threadIdx.x; i < RB_CH; i += 64) st_dev(&S.rb_occ[(size_t)q * RB_CH + i], (uint64_t)0);
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH + q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH + 3 + q], (uint64_t)0);
       }
     }
     // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
@@ -2256,27 +2361,30 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       X.ob->bbase = ws;
       X.ob->pg_avail = rs.pg_avail;
       X.ob->pg_freed = &S.rb_free[p];
+      X.ob->pg_allocd = &S.rb_occ[3 * RB_CH + p];
+      X.ob->spilled = &S.rb_occ[3 * RB_CH + 3 + p];
     }
-    uint64_t kall = INVALID, mall = INVALID;
+    uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
       const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
-      exec_group<false, kApp>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n) {
+      exec_group<false, kApp>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
+        oall += od;
         if (lastg) {
           if (rd && threadIdx.x == 0)
             __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           flush_bmin<kApp>(S, X);
-          rb_arrive(S, p, w, P, kall, mall);
+          rb_arrive(S, p, w, P, kall, mall, oall);
           arrived = true;
         }
       });
       __syncthreads();
     }
-    if (!arrived) rb_arrive(S, p, w, P, INVALID, INVALID);  // a workgroup without groups
+    if (!arrived) rb_arrive(S, p, w, P, INVALID, INVALID, 0);  // a workgroup without groups
     // grid barrier: every chunk complete, bounded
     uint32_t spins = 0;
     bool ok = true;
@@ -2294,13 +2402,35 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     asm volatile("" ::: "memory");
     const RbEdge e = rb_edge(S, p, nch, ws, we);
     if (rd && w == 0 && threadIdx.x == 0) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
+    // This round's bucket bookkeeping (consumed minima -> INVALID, bucket b1 -> nb1) is done by
+    // workgroup 0 during the next round, with plain stores: safe while the next round's sends
+    // cannot reach this round's buckets. They can after an idle gap: a send at t maps to this
+    // round's bucket indices again once t >= bucketstart(ws) + NB * BW, and t < we' + max_lat.
+    // Then (every workgroup decides alike) workgroup 0 does it now and a second grid barrier
+    // keeps every send of the next round behind it (a lost bucket minimum).
+    const uint64_t span = (uint64_t)S.NB * S.BW;
+    const uint64_t bstart = SIM_START + S.bw_div.div(ws - SIM_START) * S.BW;
+    const bool gap = e.active && (e.we + S.max_lat >= bstart + span || e.we + S.max_lat < e.we);
+    if (gap) {
+      if (w == 0) rb_bookkeep(S, ws, we, e.nb1, ks);  // (the previous round's: done at this round's start)
+      if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // workgroup 0's stores are done
+        SGN_GLB uint32_t* gc = S.rb_cnt + 3 * (RB_CH + 1);
+        const uint32_t target = (rs.ngap + 1) * P;
+        __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t sp = 0;
+        while (ld_dev(gc) < target && ++sp < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+        if (sp >= (1u << 24)) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+        rs.ngap++;
+      }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
       const uint32_t b1 = bucket_of(S, we - 1);
       const uint32_t slab_b1 = lds_tab ? X.lbs[b1] : ld_dev(&S.bucket_slab[b1]);
       if (lds_tab) X.lbs[b1] = (uint16_t)ks;
-      rs.pend = 1;
+      rs.pend = gap ? 0u : 1u;
       rs.pend_ws = ws;
       rs.pend_we = we;
       rs.pend_nb1 = e.nb1;
@@ -2309,7 +2439,15 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       rs.ws = e.ws;
       rs.we = e.we;
       rs.active = e.active;
-      rs.pg_avail += ld_dev(&S.rb_free[p]);  // this round's freed pages (all written: barrier)
+      rs.pg_avail += e.nfree;  // this round's freed pages (all written: barrier)
+      rs.pg_alloc += e.nalloc;
+      rs.occ += e.occd;
+      rs.nspill += e.nspill;
+      if (e.active) {  // the next round's guards: every workgroup decides alike (same values)
+        const uint64_t need = codel_round_bound(S, rs.occ, e.ws, e.we);
+        rs.hold = (pages_free(rs.pg_avail, rs.pg_alloc) < need ? HOLD_CODEL : 0u) | (rs.nspill ? HOLD_SPILL : 0u);
+        rs.hold_need = need;
+      }
       if (w == 0) {
         st_dev(&C->last_min_next, e.min_next);
         st_dev(&C->prev_we, we);
@@ -2327,6 +2465,11 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       st_dev(&C->active, rs.active);
       st_dev(&C->rounds, rounds0 + r);
       st_dev(&C->pg_avail, rs.pg_avail);
+      st_dev(&C->cal_occ, rs.occ);
+      if (rs.hold) {
+        st_dev(&C->hold, rs.hold);
+        st_dev(&C->hold_need, rs.hold_need);
+      }
     }
   }
 }
@@ -2343,7 +2486,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 __device__ __forceinline__ void advance_window(const DevSim& S, Ctrl* C) {
   uint64_t m = INVALID, mu = INVALID;
   for (uint32_t p = 0; p < S.n_ranks; p++) {
-    const uint64_t* msg = (const uint64_t*)(S.xin + (size_t)p * (S.xslot + 1));
+    const uint64_t* msg = (const uint64_t*)(S.xin + (size_t)p * (S.xslot + XHDR));
     const uint64_t a = msg[1], b = msg[2];
     m = a < m ? a : m;
     mu = b < mu ? b : mu;
@@ -2372,7 +2515,7 @@ constexpr uint32_t kImportBlocks = 16;
 __global__ __launch_bounds__(256) void k_import(DevSim S) {
   Ctrl* C = S.ctrl;
   // every block reads the same values: nothing changes them before all blocks count in
-  if (!C->active || C->xspill) return;
+  if (!C->active || C->xspill || C->hold) return;
   // The send/recv moved the first C->xsz runs of each slot. If any shard had more for some
   // peer (the messages carry every shard's maximum), the round is held on every shard alike:
   // nothing is imported, the window stays, and the host completes the round with a
@@ -2380,20 +2523,21 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   // itself are an overflow the sender already reported.
   uint64_t gm = 0;
   for (uint32_t r = 0; r < S.n_ranks; r++) {
-    const uint64_t x = ((const uint64_t*)(S.xin + (size_t)r * (S.xslot + 1)))[3];
+    const uint64_t x = ((const uint64_t*)(S.xin + (size_t)r * (S.xslot + XHDR)))[3] & 0xFFFFFFFFull;
     gm = x > gm ? x : gm;
   }
   const uint32_t sz = C->xsz;
   const bool hold = gm > sz && sz < S.xslot;
   // the window that just ran (still C->ws): the same horizon as sends
   const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
+  uint32_t filed = 0;
   for (uint32_t r = 0; r < S.n_ranks && !hold; r++) {
     if (r == S.rank) continue;
-    const EvRec* blk = S.xin + (size_t)r * (S.xslot + 1);  // message, then the runs
+    const EvRec* blk = S.xin + (size_t)r * (S.xslot + XHDR);  // message, then the runs
     const uint32_t n = (uint32_t)min(((const uint64_t*)blk)[0], (uint64_t)S.xslot);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += gridDim.x * blockDim.x) {
-      const EvRec e = blk[1 + i];
+      const EvRec e = blk[XHDR + i];
       if (e.time >= hz) {
         if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = e.dst;
         continue;
@@ -2404,13 +2548,20 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
       atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)e.time);
       if (pos < S.CAP)
         S.pool[idx * S.CAP + pos] = e;
-      else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-        C->overflow_info = e.dst;
+      else
+        spill_run(S, nullptr, (uint32_t)idx, e);  // re-laid out at the batch's host sync
+      filed++;
     }
   }
-  __shared__ uint32_t last;
+  __shared__ uint32_t last, bfiled;
+  if (threadIdx.x == 0) bfiled = 0;
+  __syncthreads();
+  if (filed) atomicAdd(&bfiled, filed);
   __syncthreads();  // this block's reads of C->ws are done
-  if (threadIdx.x == 0) last = atomicAdd(&C->imp_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  if (threadIdx.x == 0) {
+    if (bfiled) (void)atomicAdd((unsigned long long*)&C->cal_occ, (unsigned long long)bfiled);  // (completes first)
+    last = atomicAdd(&C->imp_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
   __syncthreads();
   if (!last || threadIdx.x != 0) return;
   C->imp_done = 0;
@@ -2420,6 +2571,28 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
     return;
   }
   advance_window(S, C);
+  if (!C->active) return;
+  // the next round's guards, evaluated for EVERY shard from the messages alike (so all shards
+  // hold the same round, or none): a shard's CoDel pages may not cover the next window's due
+  // runs — its occupancy plus everything exported this round (a bound on what it received)
+  // and at most its slabs of the window's buckets — or some shard spilled runs
+  uint64_t xs = 0;
+  for (uint32_t q = 0; q < S.n_ranks; q++) xs += ((const uint64_t*)(S.xin + (size_t)q * (S.xslot + XHDR)))[6];
+  const uint32_t nbk = ((bucket_of(S, C->we - 1) - bucket_of(S, C->ws)) & (S.NB - 1)) + 1;
+  uint32_t hflags = 0;
+  uint64_t own = 0;
+  for (uint32_t q = 0; q < S.n_ranks; q++) {
+    const uint64_t* msg = (const uint64_t*)(S.xin + (size_t)q * (S.xslot + XHDR));
+    const uint64_t occ = msg[5] + xs, capb = (uint64_t)nbk * msg[7];
+    const uint64_t need = codel_pages_bound(occ < capb ? occ : capb, S.rank_lo[q + 1] - S.rank_lo[q]);
+    if (msg[4] < need) hflags |= HOLD_CODEL;
+    if ((msg[3] >> 32) & 1) hflags |= HOLD_SPILL;
+    if (q == S.rank) own = need;
+  }
+  if (hflags) {
+    C->hold = hflags;
+    C->hold_need = own;
+  }
 }
 
 // CoDel control-law self test (f64 sqrt/div/round on the device vs the host).
@@ -2440,12 +2613,34 @@ __global__ void k_inject(const DevSim* Sp, const EvRec* recs, uint32_t n) {
   const uint32_t b = bucket_of(S, r.time);
   const size_t idx = (size_t)S.bucket_slab[b] * S.G + g;
   const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
-  if (pos >= S.CAP) {
-    if ((atomicOr(&S.ctrl->overflow, OVF_BUCKET) & OVF_BUCKET) == 0) S.ctrl->overflow_info = r.dst;
-    return;
-  }
-  S.pool[idx * S.CAP + pos] = r;
   atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)r.time);
+  (void)atomicAdd((unsigned long long*)&S.ctrl->cal_occ, 1ULL);
+  if (pos < S.CAP)
+    S.pool[idx * S.CAP + pos] = r;
+  else
+    spill_run(S, nullptr, (uint32_t)idx, r);  // sgn_submit re-lays the calendar out right after
+}
+
+// Calendar re-layout (a held round edge after a spill): every slab's runs into a pool of
+// larger slabs, then the spilled runs after them. Order inside a slab is free (the gather
+// sorts by Shadow's key); slab_n already counts every run of a slab, spilled ones included.
+__global__ void k_relayout(const EvRec* __restrict__ old_pool, uint32_t old_cap, EvRec* __restrict__ pool,
+                           uint32_t cap, const uint32_t* __restrict__ slab_n, uint32_t* cursor, uint64_t n_slabs) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t idx = t / old_cap;
+  const uint32_t j = (uint32_t)(t % old_cap);
+  if (idx >= n_slabs) return;
+  const uint32_t n = min(slab_n[idx], old_cap);
+  if (j < n) pool[idx * cap + j] = old_pool[idx * old_cap + j];
+  if (j == 0) cursor[idx] = n;
+}
+__global__ void k_respill(const EvRec* __restrict__ spill, const uint32_t* __restrict__ spill_idx, uint64_t n,
+                          EvRec* __restrict__ pool, uint32_t cap, uint32_t* cursor) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t idx = spill_idx[i];
+  const uint32_t pos = atomicAdd(&cursor[idx], 1u);
+  if (pos < cap) pool[(size_t)idx * cap + pos] = spill[i];
 }
 
 // sgn_rng_*: draws of host Xoshiro256++ streams (the state stays on the device). One thread
@@ -2544,28 +2739,39 @@ constexpr uint64_t kTimeEvery = 8;        // per-round launches: one timed in kT
 
 namespace {
 
-// the round kernels of the simulation's traffic kind
-const void* execute_fn(uint32_t kind) {
-  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_execute<SGN_TRAFFIC_TGEN>;
-  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_execute<SGN_TRAFFIC_EXTERNAL>;
-  return (const void*)k_execute<SGN_TRAFFIC_PERIODIC>;
+// the round kernels of the simulation's traffic kind (k_execute: traced or lean)
+template <bool kTrace>
+const void* execute_fn_t(uint32_t kind) {
+  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_execute<kTrace, SGN_TRAFFIC_TGEN>;
+  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_execute<kTrace, SGN_TRAFFIC_EXTERNAL>;
+  return (const void*)k_execute<kTrace, SGN_TRAFFIC_PERIODIC>;
+}
+const void* execute_fn(uint32_t kind, bool trace) {
+  return trace ? execute_fn_t<true>(kind) : execute_fn_t<false>(kind);
 }
 const void* rounds_fn(uint32_t kind) {
   if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_rounds<SGN_TRAFFIC_TGEN>;
   if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_rounds<SGN_TRAFFIC_EXTERNAL>;
   return (const void*)k_rounds<SGN_TRAFFIC_PERIODIC>;
 }
-void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
+template <bool kTrace>
+void launch_k_execute_t(sgn_ctx* ctx, hipStream_t st) {
   const uint32_t k = ctx->S.tkind;
   const dim3 grid(ctx->S.G), block(64);
   const size_t lds = exec_lds_bytes(ctx->S.CAP, ctx->S.agg_bmin ? ctx->S.NB : 0);
   const DevSim* d = (const DevSim*)ctx->d_S;
   if (k == SGN_TRAFFIC_TGEN)
-    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_TGEN>, grid, block, lds, st, d);
+    hipLaunchKernelGGL((k_execute<kTrace, SGN_TRAFFIC_TGEN>), grid, block, lds, st, d);
   else if (k == SGN_TRAFFIC_EXTERNAL)
-    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_EXTERNAL>, grid, block, lds, st, d);
+    hipLaunchKernelGGL((k_execute<kTrace, SGN_TRAFFIC_EXTERNAL>), grid, block, lds, st, d);
   else
-    hipLaunchKernelGGL(k_execute<SGN_TRAFFIC_PERIODIC>, grid, block, lds, st, d);
+    hipLaunchKernelGGL((k_execute<kTrace, SGN_TRAFFIC_PERIODIC>), grid, block, lds, st, d);
+}
+void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
+  if (ctx->S.trace_on)
+    launch_k_execute_t<true>(ctx, st);
+  else
+    launch_k_execute_t<false>(ctx, st);
 }
 void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
   const uint32_t k = ctx->S.tkind;
@@ -2592,6 +2798,7 @@ int launch_round(sgn_ctx* ctx) {
   if (timed) time_begin(ctx, K_EXECUTE);
   launch_k_execute(ctx, st);
   if (timed) time_end(ctx);
+  if (!ctx->capturing) ctx->kt[K_EXECUTE].total++;
   if (ctx->nranks > 1) {
     // exchange + import + local finalize + all-reduce(min) + advance (comm.cpp)
     int rc = comm_round_exchange(ctx);
@@ -2602,6 +2809,74 @@ int launch_round(sgn_ctx* ctx) {
   SGN_HIP(ctx, hipGetLastError());
   ctx->rounds_enqueued++;
   return 0;
+}
+
+// Resident workgroups of a round kernel on this GPU (0: unknown): the occupancy query,
+// capped by LDS per CU (the device attribute: 160 KiB on gfx950) — LDS is allocated per
+// workgroup in 512-byte granules (a 23184-byte workgroup fits 6 per CU, not 7: a grid sized
+// for 7 was not resident and its barrier timed out)
+uint64_t resident_wg(sgn_ctx* ctx, const void* fn, size_t dyn) {
+  int occ = 0, ncu = 0, lds_cu = 0;
+  hipFuncAttributes fa{};
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64, dyn) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+      hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, ctx->device) != hipSuccess ||
+      hipFuncGetAttributes(&fa, fn) != hipSuccess || occ <= 0 || ncu <= 0 || lds_cu <= 0)
+    return 0;
+  const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
+  ctx->lds_per_cu = (uint32_t)lds_cu;
+  return (uint64_t)std::min<int>(occ, (int)((size_t)lds_cu / lds_wg)) * (uint64_t)ncu;
+}
+
+// The largest slab capacity whose round-kernel LDS fits one workgroup (calendar re-layout).
+uint32_t max_slab_capacity(sgn_ctx* ctx, const DevSim& S) {
+  int per_block = 0;
+  if (hipDeviceGetAttribute(&per_block, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess ||
+      per_block <= 0)
+    per_block = 64 * 1024;
+  size_t st = 0;
+  for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind, S.trace_on)}) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, fn) == hipSuccess) st = std::max<size_t>(st, fa.sharedSizeBytes);
+  }
+  uint32_t cap = CAP_MIN;
+  while (cap < (1u << 15) && st + exec_lds_bytes(cap * 2, S.NB) <= (size_t)per_block) cap *= 2;
+  return cap;
+}
+
+// The round kernels' shapes for the calendar as it is now (sim_init, and after a re-layout):
+// the LDS table of bucket minima ((NB + 1) x 4 bytes per workgroup, flush_bmin) is used when
+// it costs no resident workgroups where they count — the round kernels' grids stay as large
+// (config C has no LDS to spare: its 1563 groups need 7 workgroups per CU), or the grid
+// exceeds the chip either way (config D); SGN_AGG_BMIN=0/1 overrides — and the persistent
+// grid (single shard): entirely resident, with workgroups looping over groups when G exceeds
+// it. Persistent rounds keep the bucket -> slab table in LDS (each workgroup applies the
+// round's swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per
+// round, and so does a traced run (k_rounds is built without the per-packet trace).
+void size_round_kernels(sgn_ctx* ctx, DevSim& S) {
+  const uint64_t G = S.G, NB = S.NB;
+  bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic
+  for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind, S.trace_on)}) {
+    const uint64_t r0 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP)), r1 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP, S.NB));
+    if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
+  }
+  if (const char* e = getenv("SGN_AGG_BMIN")) agg = atoi(e) != 0;
+  if ((NB + 1) * S.BW >= (1ULL << 32)) agg = false;  // offsets from the window start must fit u32
+  S.agg_bmin = agg ? 1u : 0u;
+  ctx->persist_grid = 0;
+  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !ctx->persist_off &&
+      !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
+    const uint64_t res = resident_wg(ctx, rounds_fn(S.tkind), exec_lds_bytes(S.CAP, S.agg_bmin ? S.NB : 0));
+    if (res) {
+      ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, res);
+      // test hook: a smaller grid makes every workgroup serve several groups per round
+      if (const char* e = getenv("SGN_PERSIST_GRID"))
+        ctx->persist_grid = std::max<uint32_t>(1, std::min<uint32_t>(ctx->persist_grid, (uint32_t)atoi(e)));
+      // test hook: an oversized grid (not resident) exercises the residency census fallback
+      if (const char* e = getenv("SGN_PERSIST_GRID_FORCE")) ctx->persist_grid = (uint32_t)atoi(e);
+    }
+  }
+  if (ctx->persist_grid > 64 * RB_CH) ctx->persist_grid = 64 * RB_CH;
 }
 
 int check_overflow(sgn_ctx* ctx) {
@@ -2629,6 +2904,130 @@ int sync_ctrl(sgn_ctx* ctx) {
   return check_overflow(ctx);
 }
 
+// ---- pools that grow (the reference's queues are unbounded): run at a held round edge ----
+int upload_sim(sgn_ctx* ctx) {
+  SGN_HIP(ctx, hipMemcpy(ctx->d_S, &ctx->S, sizeof(DevSim), hipMemcpyHostToDevice));
+  drop_graph(ctx);  // captured batches hold k_import's by-value DevSim
+  return 0;
+}
+
+// The calendar with larger slabs: the fullest slab (spilled runs counted) plus a quarter,
+// within what one workgroup's LDS holds; the spill area is emptied into it.
+int relayout_calendar(sgn_ctx* ctx) {
+  DevSim& S = ctx->S;
+  const uint64_t n_slabs = (uint64_t)(S.NB + 1) * S.G;
+  const uint64_t nsp = std::min<uint64_t>(ctx->h_ctrl->spill_n, S.spill_cap);
+  if (ctx->h_ctrl->spill_n > S.spill_cap)
+    return set_error(ctx, SGN_EOVERFLOW, "calendar spill area exhausted within one round (" +
+                                             std::to_string(ctx->h_ctrl->spill_n) + " runs)");
+  std::vector<uint32_t> fill(n_slabs);
+  SGN_HIP(ctx, hipMemcpy(fill.data(), (const void*)S.slab_n, n_slabs * 4, hipMemcpyDeviceToHost));
+  const uint32_t mx = *std::max_element(fill.begin(), fill.end());
+  const uint32_t lim = max_slab_capacity(ctx, S);
+  uint32_t cap = S.CAP;
+  while (cap < mx + mx / 4 && cap < lim) cap *= 2;
+  cap = std::min(cap, lim);
+  if (cap < mx)
+    return set_error(ctx, SGN_EOVERFLOW, "calendar slab needs " + std::to_string(mx) +
+                                             " runs; one workgroup's LDS holds " + std::to_string(lim) +
+                                             " (raise the bucket width: runahead)");
+  if (cap > S.CAP) {
+    EvRec* np = (EvRec*)dev_alloc(ctx, n_slabs * cap * sizeof(EvRec), false);
+    uint32_t* cur = (uint32_t*)dev_alloc(ctx, n_slabs * 4, false);
+    if (!np || !cur) return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar re-layout)");
+    const uint64_t nt = n_slabs * S.CAP;
+    hipLaunchKernelGGL(k_relayout, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, ctx->stream,
+                       (const EvRec*)S.pool, S.CAP, np, cap, (const uint32_t*)S.slab_n, cur, n_slabs);
+    if (nsp)
+      hipLaunchKernelGGL(k_respill, dim3((uint32_t)((nsp + 255) / 256)), dim3(256), 0, ctx->stream,
+                         (const EvRec*)S.spill, (const uint32_t*)S.spill_idx, nsp, np, cap, cur);
+    SGN_HIP(ctx, hipGetLastError());
+    SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    dev_free(ctx, (void*)S.pool, n_slabs * S.CAP * sizeof(EvRec));
+    dev_free(ctx, cur, n_slabs * 4);
+    S.pool = (decltype(S.pool))np;
+    S.CAP = cap;
+    size_round_kernels(ctx, S);
+    ctx->cal_grows++;
+  }
+  ctx->cal_spill_runs += nsp;
+  const uint64_t zero = 0;
+  SGN_HIP(ctx, hipMemcpy((char*)S.ctrl + offsetof(Ctrl, spill_n), &zero, 8, hipMemcpyHostToDevice));
+  ctx->h_ctrl->spill_n = 0;
+  return upload_sim(ctx);
+}
+
+// the CoDel pages the round of the current window may take (codel_round_bound, host form)
+uint64_t codel_need_host(const sgn_ctx* ctx) {
+  const DevSim& S = ctx->S;
+  const Ctrl& c = *ctx->h_ctrl;
+  if (!c.active || c.we <= c.ws) return 0;
+  auto bk = [&](uint64_t t) { return (uint32_t)((t - SIM_START) / S.BW) & (S.NB - 1); };
+  const uint64_t nbk = ((bk(c.we - 1) - bk(c.ws)) & (S.NB - 1)) + 1;
+  return codel_pages_bound(std::min<uint64_t>(c.cal_occ, nbk * S.G * S.CAP), S.nH);
+}
+
+// A CoDel page pool with at least `extra` more free pages (and at least double the size): the
+// pages keep their indices (host records and chains stay valid), the free ring is rebuilt as
+// its current entries followed by the new pages.
+int grow_codel(sgn_ctx* ctx, uint64_t extra) {
+  DevSim& S = ctx->S;
+  Ctrl& c = *ctx->h_ctrl;
+  if (c.pg_avail != c.pg_tail)
+    return set_error(ctx, SGN_ESTATE, "CoDel pool growth outside a round edge");
+  const uint64_t P = S.cq_pages;
+  const uint64_t P2 = std::max<uint64_t>(2 * P, P + extra + extra / 2 + 64);
+  if (P2 >= (1ULL << 28)) return set_error(ctx, SGN_EOVERFLOW, "CoDel page pool above 2^28 pages");
+  CodelEnt* ne = (CodelEnt*)dev_alloc(ctx, P2 * CQ_PAGE * sizeof(CodelEnt), false);
+  uint32_t* nn = (uint32_t*)dev_alloc(ctx, P2 * 4, true);
+  uint32_t* nf = (uint32_t*)dev_alloc(ctx, P2 * 4, false);
+  if (!ne || !nn || !nf) return set_error(ctx, SGN_ENOMEM, "device allocation failed (CoDel pool growth)");
+  SGN_HIP(ctx, hipMemcpy(ne, (const void*)S.codel, P * CQ_PAGE * sizeof(CodelEnt), hipMemcpyDeviceToDevice));
+  SGN_HIP(ctx, hipMemcpy(nn, (const void*)S.cq_next, P * 4, hipMemcpyDeviceToDevice));
+  std::vector<uint32_t> ring(P), fr;
+  SGN_HIP(ctx, hipMemcpy(ring.data(), (const void*)S.cq_free, P * 4, hipMemcpyDeviceToHost));
+  fr.reserve(P2);
+  for (uint64_t i = c.pg_alloc; i < c.pg_tail; i++) fr.push_back(ring[i % P]);
+  for (uint64_t pg = P; pg < P2; pg++) fr.push_back((uint32_t)pg);
+  const uint64_t nfree = fr.size();
+  fr.resize(P2, 0);
+  SGN_HIP(ctx, hipMemcpy(nf, fr.data(), P2 * 4, hipMemcpyHostToDevice));
+  dev_free(ctx, (void*)S.codel, P * CQ_PAGE * sizeof(CodelEnt));
+  dev_free(ctx, (void*)S.cq_next, P * 4);
+  dev_free(ctx, (void*)S.cq_free, P * 4);
+  S.codel = (decltype(S.codel))ne;
+  S.cq_next = (decltype(S.cq_next))nn;
+  S.cq_free = (decltype(S.cq_free))nf;
+  S.cq_pages = (uint32_t)P2;
+  ctx->codel_allocs_before += c.pg_alloc;
+  c.pg_alloc = 0;
+  c.pg_tail = c.pg_avail = nfree;
+  SGN_HIP(ctx, hipMemcpy((char*)S.ctrl + offsetof(Ctrl, pg_alloc), &c.pg_alloc, 3 * 8, hipMemcpyHostToDevice));
+  ctx->codel_grows++;
+  return upload_sim(ctx);
+}
+
+// A round edge held the rounds (Ctrl::hold; nothing of the next round has run): the calendar
+// is re-laid out after a spill, the CoDel pool grows until its free pages cover the next
+// round's bound, and the rounds are released. (Multi-shard: every shard holds the same round;
+// each grows what it needs.)
+int resolve_hold(sgn_ctx* ctx) {
+  Ctrl& c = *ctx->h_ctrl;
+  if (!c.hold) {
+    // (multi-shard: runs k_import spilled hold nothing; re-laid out at the batch's sync)
+    return c.spill_n ? relayout_calendar(ctx) : 0;
+  }
+  int rc = 0;
+  if (c.spill_n && (rc = relayout_calendar(ctx))) return rc;
+  const uint64_t free = c.pg_avail > c.pg_alloc ? c.pg_avail - c.pg_alloc : 0;
+  if (free < c.hold_need && (rc = grow_codel(ctx, c.hold_need - free))) return rc;
+  ctx->rounds_held++;
+  c.hold = 0;
+  c.hold_need = 0;
+  SGN_HIP(ctx, hipMemcpy((char*)ctx->S.ctrl + offsetof(Ctrl, hold), &c.hold, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
 // Event-record nodes around the timed kernel nodes of a captured batch (a captured
 // hipEventRecord yields no timing on ROCm 7.2; explicit record nodes do).
 int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
@@ -2636,7 +3035,7 @@ int add_timing_nodes(sgn_ctx* ctx, hipGraph_t g) {
   const bool exec = ctx->flags & SGN_CREATE_TIME_EXECUTE;
   ctx->graph_timed.clear();
   if (!all && !exec) return 0;
-  const void* fn[K_NUM] = {execute_fn(ctx->S.tkind), (const void*)k_import};
+  const void* fn[K_NUM] = {execute_fn(ctx->S.tkind, ctx->S.trace_on), (const void*)k_import};
   size_t n = 0;
   SGN_HIP(ctx, hipGraphGetNodes(g, nullptr, &n));
   std::vector<hipGraphNode_t> nodes(n);
@@ -2731,6 +3130,7 @@ void time_collect(sgn_ctx* ctx) {
 }
 
 int ctrl_sync(sgn_ctx* ctx) { return sync_ctrl(ctx); }
+int resolve_pools(sgn_ctx* ctx) { return resolve_hold(ctx); }
 
 void drop_graph(sgn_ctx* ctx) {
   if (ctx->gexec) hipGraphExecDestroy(ctx->gexec);
@@ -2790,6 +3190,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   DevSim S{};
   const uint32_t nH = ctx->hi - ctx->lo;
   const uint32_t N = ctx->n_all;
+  ctx->persist_off = false;
+  ctx->codel_grows = ctx->cal_grows = ctx->cal_spill_runs = ctx->xslot_grows = ctx->rounds_held = 0;
+  ctx->codel_allocs_before = 0;
   S.n_all = N;
   S.lo = ctx->lo;
   S.nH = nH;
@@ -2821,6 +3224,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
 
   const uint64_t min_possible = ctx->lat_min, max_lat = ctx->lat_max;
   S.min_possible = min_possible;
+  S.max_lat = max_lat;
   if (min_possible == 0) return set_error(ctx, SGN_EINVAL, "route latency 0 (Runahead::new asserts)");
 
   // routing (device copies made by sgn_routes_build)
@@ -2977,6 +3381,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   uint64_t cap = cfg->event_capacity ? cfg->event_capacity : (1ULL << 22);
   uint64_t CAP = cap / ((NB + 1) * G);
   CAP = std::max<uint64_t>(CAP_MIN, std::min<uint64_t>(CAP_MAX, CAP));
+  // test hook: small slabs, so that rounds spill runs and the calendar is re-laid out
+  if (const char* e = getenv("SGN_SLAB_CAP")) CAP = std::max<uint64_t>(16, std::min<uint64_t>(CAP_MAX, atoll(e)));
   S.NB = (uint32_t)NB;
   S.G = (uint32_t)G;
   S.CAP = (uint32_t)CAP;
@@ -3027,8 +3433,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       return set_error(ctx, SGN_ESTATE, "multi-shard context needs sgn_comm_init (or sgn_comm_init_local) before sgn_sim_init");
     S.xslot = (uint32_t)ctx->xslot;
     // per peer a block of 1 + xslot records: the 32-byte round-edge message, then the runs
-    S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + 1));
-    S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + 1));
+    S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
+    S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
     S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
@@ -3061,58 +3467,22 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
-  // persistent rounds (single shard): a grid that is entirely resident — the occupancy
-  // query, capped by LDS per CU — with workgroups looping over groups when G exceeds it
-  ctx->persist_grid = 0;
-  // persistent rounds keep the bucket -> slab table in LDS (each workgroup applies the round's
-  // swap itself), so they need NB <= LDS_BSLAB; longer calendars run one launch per round, and
-  // so does a traced run (k_rounds is built without the per-packet trace)
-  // Resident workgroups of a round kernel on this GPU (0: unknown): the occupancy query,
-  // capped by LDS per CU — LDS is allocated per workgroup in 512-byte granules (a 23184-byte
-  // workgroup fits 6 per CU, not 7: a grid sized for 7 was not resident and its barrier
-  // timed out)
-  auto resident = [&](const void* fn, size_t dyn) -> uint64_t {
-    int occ = 0, ncu = 0;
-    hipFuncAttributes fa{};
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64, dyn) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
-        hipFuncGetAttributes(&fa, fn) != hipSuccess || occ <= 0 || ncu <= 0)
-      return 0;
-    const size_t lds_wg = (fa.sharedSizeBytes + dyn + 511) / 512 * 512;
-    return (uint64_t)std::min<int>(occ, (int)((160u * 1024u) / lds_wg)) * (uint64_t)ncu;
-  };
-  // The LDS table of bucket minima ((NB + 1) x 4 bytes per workgroup, flush_bmin) is used
-  // when it costs no resident workgroups where they count: the round kernels' grids stay as
-  // large (config C has no LDS to spare: its 1563 groups need 7 workgroups per CU), or the
-  // grid exceeds the chip either way (config D). SGN_AGG_BMIN=0/1 overrides.
-  {
-    bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic
-    for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind)}) {
-      const uint64_t r0 = resident(fn, exec_lds_bytes((uint32_t)CAP)), r1 = resident(fn, exec_lds_bytes((uint32_t)CAP, NB));
-      if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
-    }
-    if (const char* e = getenv("SGN_AGG_BMIN")) agg = atoi(e) != 0;
-    if ((NB + 1) * BW >= (1ULL << 32)) agg = false;  // offsets from the window start must fit u32
-    S.agg_bmin = agg ? 1u : 0u;
-  }
-  if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
-    const uint64_t res = resident(rounds_fn(S.tkind), exec_lds_bytes((uint32_t)CAP, S.agg_bmin ? NB : 0));
-    if (res) {
-      ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, res);
-      // test hook: a smaller grid makes every workgroup serve several groups per round
-      if (const char* e = getenv("SGN_PERSIST_GRID"))
-        ctx->persist_grid = std::max<uint32_t>(1, std::min<uint32_t>(ctx->persist_grid, (uint32_t)atoi(e)));
-      // test hook: an oversized grid (not resident) exercises the residency census fallback
-      if (const char* e = getenv("SGN_PERSIST_GRID_FORCE")) ctx->persist_grid = (uint32_t)atoi(e);
-    }
-  }
+  size_round_kernels(ctx, S);
   // persistent-round buffers (three, by round % 3): chunk minima + keep minima, counters
   S.rb_min = (decltype(S.rb_min))dalloc<uint64_t>(ctx, 3 * RB_CH * 2 + 4);
   S.rb_keep = S.rb_min + 3 * RB_CH * 2;
-  S.rb_cnt = (decltype(S.rb_cnt))dalloc<uint32_t>(ctx, 3 * (RB_CH + 1));
-  if (!S.rb_min || !S.rb_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
-  if (ctx->persist_grid > 64 * RB_CH) ctx->persist_grid = 64 * RB_CH;
+  S.rb_cnt = (decltype(S.rb_cnt))dalloc<uint32_t>(ctx, 3 * (RB_CH + 1) + 1);
+  S.rb_occ = (decltype(S.rb_occ))dalloc<uint64_t>(ctx, 3 * RB_CH + 6);
+  if (!S.rb_min || !S.rb_cnt || !S.rb_occ) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
+  S.fin_occ = (decltype(S.fin_occ))dalloc<uint64_t>(ctx, (G + 63) / 64);
+  if (!S.fin_occ) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
+  // the calendar's spill area: runs whose slab is full until the next re-layout (a round edge
+  // holds right after a spill); sized for an eighth of the slabs, at least 2^16 runs
+  S.spill_cap = std::max<uint64_t>(1u << 16, std::min<uint64_t>(1u << 24, (NB + 1) * G * CAP / 8));
+  S.spill = (decltype(S.spill))dev_alloc(ctx, S.spill_cap * sizeof(EvRec), false);
+  S.spill_idx = (decltype(S.spill_idx))dev_alloc(ctx, S.spill_cap * 4, false);
+  if (!S.spill || !S.spill_idx) return set_error(ctx, SGN_ENOMEM, "device allocation failed (spill area)");
   {
     std::vector<uint64_t> inv((G + 63) / 64, INVALID);
     if ((rc = up64(inv, &S.fin_keep)) || (rc = up64(inv, &S.fin_next))) return rc;
@@ -3125,7 +3495,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   ctx->S = S;
   ctx->sim_ready = true;
   ctx->rounds_enqueued = 0;
-  for (int i = 0; i < K_NUM; i++) ctx->kt[i] = {kKernelNames[i], 0, 0.0};
+  for (int i = 0; i < K_NUM; i++) ctx->kt[i] = {kKernelNames[i], 0, 0.0, 0};
   return 0;
 }
 
@@ -3148,6 +3518,7 @@ int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
   if ((rc = launch_round(ctx))) return rc;
   rc = sync_ctrl(ctx);
   if (!rc && ctx->h_ctrl->xspill) rc = comm_complete_spill(ctx);
+  if (!rc) rc = resolve_hold(ctx);
   if (min_next) *min_next = ctx->h_ctrl->last_min_next;
   return rc;
 }
@@ -3173,16 +3544,19 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   const bool graph = ctx->use_graph && (ctx->nranks == 1 || ctx->comm) &&
                      getenv("SGN_GRAPH") && atoi(getenv("SGN_GRAPH")) == 1;
   if (ctx->nranks == 1 && ctx->persist_grid) {
-    // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside)
+    // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside);
+    // a launch ends early at a held round edge (a pool grows here, then the rounds go on)
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
       SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * 2 + 4) * 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, 3 * (RB_CH + 1) * 4, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, (3 * (RB_CH + 1) + 1) * 4, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_free, 0, 3 * 8, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_occ, 0, (3 * RB_CH + 6) * 8, ctx->stream));
       time_begin(ctx, K_EXECUTE);
       launch_k_rounds(ctx, n);
       time_end(ctx);
+      ctx->kt[K_EXECUTE].total++;
       SGN_HIP(ctx, hipGetLastError());
       if ((rc = sync_ctrl(ctx))) return rc;
       if (ctx->h_ctrl->res_verdict != 1) {
@@ -3190,9 +3564,11 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
         // part of the GPU): nothing ran; continue with one launch per round
         ctx->persist_grid = 0;
         ctx->persist_fallbacks++;
+        ctx->persist_off = true;
         break;
       }
-      enq += n;
+      if ((rc = resolve_hold(ctx))) return rc;
+      enq = ctx->h_ctrl->rounds - r_start;
     }
     if (!ctx->persist_grid) {
       uint64_t more = 0;
@@ -3234,6 +3610,8 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
         ctx->gsz = ctx->xsz_cur;
       }
       SGN_HIP(ctx, hipGraphLaunch(ctx->gexec, ctx->stream));
+      ctx->kt[K_EXECUTE].total += n;
+      if (ctx->nranks > 1) ctx->kt[K_IMPORT].total += n;
       ctx->graph_pending = !ctx->graph_timed.empty();
       ctx->x_bytes += n * comm_round_bytes(ctx);
     } else {
@@ -3246,6 +3624,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
               (unsigned long long)(ctx->h_ctrl->rounds - r_start), ctx->h_ctrl->xspill,
               (unsigned long long)ctx->h_ctrl->xhwm);
     if (ctx->h_ctrl->xspill && (rc = comm_complete_spill(ctx))) return rc;
+    if ((rc = resolve_hold(ctx))) return rc;
     if (dbg && ctx->h_ctrl->xspill == 0) fprintf(stderr, "[sgn r%u] after: rounds=%llu\n", ctx->rank,
                                                  (unsigned long long)(ctx->h_ctrl->rounds - r_start));
     done = ctx->h_ctrl->rounds - r_start;
@@ -3413,7 +3792,7 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
   SGN_HIP(ctx, hipMemcpy(ctx->h_ctrl, (const void*)ctx->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
   const Ctrl& c = *ctx->h_ctrl;
-  out->codel_page_allocs = c.pg_alloc;
+  out->codel_page_allocs = ctx->codel_allocs_before + c.pg_alloc;
   out->codel_pages_free = c.pg_tail >= c.pg_alloc ? c.pg_tail - c.pg_alloc : 0;
   std::vector<HostRec> recs;
   if (int e = read_recs(ctx, 0, ctx->S.nH, &recs)) return e;
@@ -3425,6 +3804,12 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   SGN_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   out->compute_units = (uint64_t)ncu;
   out->bucket_min_lds = ctx->S.agg_bmin;
+  out->lds_per_cu = ctx->lds_per_cu;
+  out->codel_pool_grows = ctx->codel_grows;
+  out->calendar_grows = ctx->cal_grows;
+  out->calendar_spill_runs = ctx->cal_spill_runs;
+  out->exchange_slot_grows = ctx->xslot_grows;
+  out->rounds_held = ctx->rounds_held;
   return 0;
 }
 
@@ -3438,6 +3823,7 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
   out->n_kernels = K_NUM;
   for (int i = 0; i < K_NUM; i++) {
     out->launches[i] = ctx->kt[i].launches;
+    out->launches_total[i] = ctx->kt[i].total;
     out->ms[i] = ctx->kt[i].ms;
     out->name[i] = kKernelNames[i];
   }
@@ -3542,6 +3928,7 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
                      (const DevSim*)ctx->d_S, (const EvRec*)ctx->d_stage, (uint32_t)b->n);
   SGN_HIP(ctx, hipGetLastError());
   if ((rc = sync_ctrl(ctx))) return rc;
+  if (ctx->h_ctrl->spill_n && (rc = relayout_calendar(ctx))) return rc;
   for (uint64_t i = 0; i < b->n; i++) ctx->handles.push_back(b->handle ? b->handle[i] : 0);
   ctx->submit_seq.swap(seq);
   return 0;
@@ -3580,6 +3967,7 @@ int sgn_stage_push(sgn_stage* st, const sgn_pkt_soa* b) {
         return SGN_EINVAL;
     }
   }
+  std::lock_guard<std::mutex> g(st->mu);  // (uncontended except against a concurrent flush)
   st->src.insert(st->src.end(), b->src_host, b->src_host + b->n);
   st->dst.insert(st->dst.end(), b->dst_ip, b->dst_ip + b->n);
   st->pay.insert(st->pay.end(), b->payload_len, b->payload_len + b->n);
@@ -3589,15 +3977,24 @@ int sgn_stage_push(sgn_stage* st, const sgn_pkt_soa* b) {
   return 0;
 }
 
-uint64_t sgn_stage_pending(const sgn_stage* st) { return st ? st->src.size() : 0; }
+uint64_t sgn_stage_pending(const sgn_stage* st) {
+  if (!st) return 0;
+  std::lock_guard<std::mutex> g(st->mu);
+  return st->src.size();
+}
 
 int sgn_stage_flush(sgn_ctx* ctx) {
   if (!ctx) return SGN_EINVAL;
   std::vector<uint32_t> src, dst, pay, wire;
   std::vector<uint64_t> time, handle;
+  // each stage's size at copy time: only that prefix is cleared after the submit, so a push
+  // that lands while the flush runs stays staged for the next flush
+  std::vector<std::pair<sgn_stage*, size_t>> taken;
   {
     std::lock_guard<std::mutex> g(ctx->stage_mu);
     for (sgn_stage* st : ctx->stages) {
+      std::lock_guard<std::mutex> sg(st->mu);
+      taken.push_back({st, st->src.size()});
       wire.insert(wire.end(), st->wire.begin(), st->wire.end());
       src.insert(src.end(), st->src.begin(), st->src.end());
       dst.insert(dst.end(), st->dst.begin(), st->dst.end());
@@ -3610,13 +4007,17 @@ int sgn_stage_flush(sgn_ctx* ctx) {
   sgn_pkt_soa b{src.size(), src.data(), dst.data(), pay.data(), wire.data(), time.data(), handle.data()};
   if (int rc = sgn_submit(ctx, &b)) return rc;
   std::lock_guard<std::mutex> g(ctx->stage_mu);
-  for (sgn_stage* st : ctx->stages) {
-    st->src.clear();
-    st->dst.clear();
-    st->pay.clear();
-    st->time.clear();
-    st->handle.clear();
-    st->wire.clear();
+  for (auto& t : taken) {
+    sgn_stage* st = t.first;
+    if (std::find(ctx->stages.begin(), ctx->stages.end(), st) == ctx->stages.end()) continue;  // destroyed meanwhile
+    std::lock_guard<std::mutex> sg(st->mu);
+    const size_t k = t.second;
+    st->src.erase(st->src.begin(), st->src.begin() + k);
+    st->dst.erase(st->dst.begin(), st->dst.begin() + k);
+    st->pay.erase(st->pay.begin(), st->pay.begin() + k);
+    st->time.erase(st->time.begin(), st->time.begin() + k);
+    st->handle.erase(st->handle.begin(), st->handle.begin() + k);
+    st->wire.erase(st->wire.begin(), st->wire.begin() + k);
   }
   return 0;
 }
@@ -3676,6 +4077,9 @@ int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end) {
   c.we = end;
   c.active = 1;
   SGN_HIP(ctx, hipMemcpy((void*)ctx->S.ctrl, &c, offsetof(Ctrl, overflow), hipMemcpyHostToDevice));
+  // the CoDel guard for the window as set (the last round edge evaluated the one it computed)
+  const uint64_t need = codel_need_host(ctx), have = c.pg_avail > c.pg_alloc ? c.pg_avail - c.pg_alloc : 0;
+  if (have < need) return grow_codel(ctx, need - have);
   return 0;
 }
 
@@ -3781,5 +4185,6 @@ void launch_execute(sgn_ctx* ctx) { launch_k_execute(ctx, ctx->stream); }
 // k_import files the received runs and its last block advances the window
 void launch_import(sgn_ctx* ctx) {
   hipLaunchKernelGGL(k_import, dim3(kImportBlocks), dim3(256), 0, ctx->stream, ctx->S);
+  if (!ctx->capturing) ctx->kt[K_IMPORT].total++;
 }
 }  // namespace sgn

@@ -542,39 +542,96 @@ __global__ __launch_bounds__(512) void loss_pass(const uint64_t* D, uint32_t Vp,
 
 // The U x U table straight into the engine's device buffers: latency from D, loss from the
 // loss rows, each used node's (n,n) entry replaced by its single self-loop edge
-// (graph/mod.rs:209-215); res = {first disconnected pair index, min latency, max latency}.
-// Rows [row0, row1) only (a shard's block of used sources; the whole table unsharded).
-__global__ void extract(const uint64_t* D, uint32_t Vp, const float* Lrows, const uint32_t* uidx,
-                        uint32_t U, const uint64_t* self_lat, const float* self_loss,
-                        uint64_t* lat, float* loss, unsigned long long* res, uint32_t row0, uint32_t row1) {
-  const uint64_t n = (uint64_t)U * row1;
-  uint64_t mn = ~0ULL, mx = 0, bad = ~0ULL;
-  for (uint64_t x = (uint64_t)U * row0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n;
-       x += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t i = (uint32_t)(x / U), j = (uint32_t)(x % U);
+// (graph/mod.rs:209-215). One workgroup per used source row of [row0, row1): the row's
+// {first disconnected column, min latency, max latency} go to rowres[3 i ..] with plain
+// stores (no same-address atomics across thousands of waves: that serialised the old form
+// at ~88 atomics/us on one word), and extract_fold reduces the rows into res.
+__global__ __launch_bounds__(256) void extract(const uint64_t* __restrict__ D, uint32_t Vp,
+                                               const float* __restrict__ Lrows, const uint32_t* __restrict__ uidx,
+                                               uint32_t U, const uint64_t* self_lat, const float* self_loss,
+                                               uint64_t* lat, float* loss, uint64_t* rowres, uint32_t row0) {
+  __shared__ uint64_t sh[3][4];
+  const uint32_t i = row0 + blockIdx.x;
+  const uint64_t base = (uint64_t)i * U;
+  const uint64_t* drow = D + (uint64_t)uidx[i] * Vp;
+  const float* lrow = Lrows + (uint64_t)i * Vp;
+  uint64_t mn = ~0ULL, mx = 0;
+  uint32_t bad = 0xFFFFFFFFu;
+  for (uint32_t j = threadIdx.x; j < U; j += blockDim.x) {
     uint64_t l;
     float p;
     if (i == j) {
       l = self_lat[i];
       p = self_loss[i];
     } else {
-      l = D[(uint64_t)uidx[i] * Vp + uidx[j]];
-      p = Lrows[(uint64_t)i * Vp + uidx[j]];
-      if (l >= FW_INF && x < bad) bad = x;
+      const uint32_t c = uidx[j];
+      l = drow[c];
+      p = lrow[c];
+      if (l >= FW_INF && j < bad) bad = j;
     }
-    lat[x] = l;
-    loss[x] = p;
+    lat[base + j] = l;
+    loss[base + j] = p;
     mn = l < mn ? l : mn;
     mx = l > mx ? l : mx;
   }
   for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64), c = __shfl_xor(bad, off, 64);
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    const uint32_t c = __shfl_xor(bad, off, 64);
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
     bad = c < bad ? c : bad;
   }
+  const uint32_t w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    if (bad != ~0ULL) atomicMin(&res[0], (unsigned long long)bad);
+    sh[0][w] = bad == 0xFFFFFFFFu ? ~0ULL : base + bad;
+    sh[1][w] = mn;
+    sh[2][w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b0 = sh[0][0], m0 = sh[1][0], x0 = sh[2][0];
+    for (uint32_t k = 1; k < (blockDim.x >> 6); k++) {
+      b0 = sh[0][k] < b0 ? sh[0][k] : b0;
+      m0 = sh[1][k] < m0 ? sh[1][k] : m0;
+      x0 = sh[2][k] > x0 ? sh[2][k] : x0;
+    }
+    rowres[3 * (uint64_t)i] = b0;
+    rowres[3 * (uint64_t)i + 1] = m0;
+    rowres[3 * (uint64_t)i + 2] = x0;
+  }
+}
+// rows [row0, row1) of rowres into res = {first disconnected pair index, min, max}: one
+// workgroup, three atomics (res also carries the other shard blocks' results)
+__global__ __launch_bounds__(256) void extract_fold(const uint64_t* rowres, uint32_t row0, uint32_t row1,
+                                                    unsigned long long* res) {
+  __shared__ uint64_t sh[3][4];
+  uint64_t b = ~0ULL, mn = ~0ULL, mx = 0;
+  for (uint32_t i = row0 + threadIdx.x; i < row1; i += blockDim.x) {
+    const uint64_t x = rowres[3 * (uint64_t)i], y = rowres[3 * (uint64_t)i + 1], z = rowres[3 * (uint64_t)i + 2];
+    b = x < b ? x : b;
+    mn = y < mn ? y : mn;
+    mx = z > mx ? z : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t x = __shfl_xor(b, off, 64), y = __shfl_xor(mn, off, 64), z = __shfl_xor(mx, off, 64);
+    b = x < b ? x : b;
+    mn = y < mn ? y : mn;
+    mx = z > mx ? z : mx;
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = b;
+    sh[1][w] = mn;
+    sh[2][w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < (blockDim.x >> 6); k++) {
+      b = sh[0][k] < b ? sh[0][k] : b;
+      mn = sh[1][k] < mn ? sh[1][k] : mn;
+      mx = sh[2][k] > mx ? sh[2][k] : mx;
+    }
+    if (b != ~0ULL) atomicMin(&res[0], (unsigned long long)b);
     atomicMin(&res[1], (unsigned long long)mn);
     atomicMax(&res[2], (unsigned long long)mx);
   }
@@ -730,7 +787,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     const uint32_t cap = (uint32_t)std::min<size_t>(std::max<size_t>(4096, 4 * (size_t)Vp),
                                                     (160 * 1024 - lds - 16) / 8);
     const size_t lds2 = lds + (size_t)cap * 8 + 16;
-    DevBuf dD, deu, dev, del, dauv, dal, dap, dus, dL, dit, dsl, dsp, dres;
+    DevBuf dD, deu, dev, del, dauv, dal, dap, dus, dL, dit, dsl, dsp, dres, drowres;
     int rc;
     if ((rc = upload(ctx, deu, es.data(), E)) || (rc = upload(ctx, dev, ed.data(), E)) ||
         (rc = upload(ctx, del, g->edge_latency_ns, E)) || (rc = upload(ctx, dauv, auv.data(), E2)) ||
@@ -743,6 +800,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     SGN_HIP(ctx, hipMalloc(&dD.p, (size_t)Vp * Vp * 8));
     SGN_HIP(ctx, hipMalloc(&dL.p, (size_t)U * Vp * 4));
     SGN_HIP(ctx, hipMalloc(&dit.p, (size_t)U * 4));
+    SGN_HIP(ctx, hipMalloc(&drowres.p, (size_t)U * 3 * 8));
     // the engine's table (replaces any previous one)
     if (ctx->d_lat) hipFree(ctx->d_lat);
     if (ctx->d_loss) hipFree(ctx->d_loss);
@@ -934,11 +992,13 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipEventRecord(e2, st));
     }
     for (uint32_t r = sh_first; r < sh_last; r++)
-      if (soff[r + 1] > soff[r])
-        hipLaunchKernelGGL(extract, dim3(1024), dim3(256), 0, st, D, Vp, (const float*)dL.p,
-                           (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p, (const float*)dsp.p,
-                           ctx->d_lat, ctx->d_loss, (unsigned long long*)dres.p, (uint32_t)soff[r],
-                           (uint32_t)soff[r + 1]);
+      if (soff[r + 1] > soff[r]) {
+        hipLaunchKernelGGL(extract, dim3((uint32_t)(soff[r + 1] - soff[r])), dim3(256), 0, st, D, Vp,
+                           (const float*)dL.p, (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p,
+                           (const float*)dsp.p, ctx->d_lat, ctx->d_loss, (uint64_t*)drowres.p, (uint32_t)soff[r]);
+        hipLaunchKernelGGL(extract_fold, dim3(1), dim3(256), 0, st, (const uint64_t*)drowres.p,
+                           (uint32_t)soff[r], (uint32_t)soff[r + 1], (unsigned long long*)dres.p);
+      }
     SGN_HIP(ctx, hipGetLastError());
     if (rccl) {  // the table's blocks to every shard; res = {min bad pair, min, max} over shards
       if ((rc = comm_bcast_blocks(ctx, ctx->d_lat, (size_t)U * 8, soff)) ||

@@ -113,10 +113,26 @@ struct Ctrl {
   // edge: a page freed in a round is reused from the next one), pages freed this round
   // (per-round launches; the persistent kernel counts in DevSim::rb_free)
   uint64_t pg_alloc, pg_tail, pg_avail, pg_freed;
+  // Pools that grow instead of refusing a scenario (the reference's queues are unbounded):
+  // runs in the event calendar (appended - gathered; the CoDel guard's bound), runs placed in
+  // the calendar's spill area this batch (their slab was full), and the hold flags (HOLD_*)
+  // that stop the rounds at a round edge — nothing of the next round has run — until the host
+  // has grown the pool; hold_need = the CoDel pages the held round may take
+  uint64_t cal_occ;
+  uint64_t spill_n;
+  uint32_t hold, pad_h;
+  uint64_t hold_need;
+  uint64_t rnd_alloc, rnd_spill;  // per-round launches: the Outbox counters' target (unread)
 };
 
 static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
               "comm.cpp all-reduces {round_min, min_used} as one u64[2]");
+
+// hold flags (Ctrl::hold): why the rounds stopped at a round edge
+enum : uint32_t {
+  HOLD_CODEL = 1u,  // the next round could take more CoDel pages than the pool has free
+  HOLD_SPILL = 2u,  // runs went to the calendar's spill area: the calendar is re-laid out
+};
 
 enum : uint32_t {
   OVF_BUCKET = 1u,
@@ -235,6 +251,7 @@ struct DevSim {
   uint32_t n_all, lo, nH, U;
   uint64_t end_time, boot_end, runahead_cfg;
   uint64_t min_possible;
+  uint64_t max_lat;   // largest route latency (the persistent kernel's calendar-alias check)
   int32_t dynamic;
   uint32_t fifo_cap;
   uint32_t cq_pages;  // CoDel page pool: pages of CQ_PAGE runs (every host owns >= 1)
@@ -284,6 +301,12 @@ struct DevSim {
   SGN_GLB uint32_t* slab_n;       // [(NB + 1) * G] fill of slab (s, g)
   SGN_GLB uint32_t* bucket_slab;  // [NB] slab id of bucket b
   SGN_GLB uint64_t* bucket_min;   // [NB] earliest event in bucket b (INVALID = empty)
+  // spill area: a run whose slab is full goes here with its slab index (lossless); the round
+  // edge then holds and the host re-lays the calendar out with larger slabs before any spilled
+  // run can be due (appends only ever target buckets after the running window)
+  SGN_GLB EvRec* spill;           // [spill_cap]
+  SGN_GLB uint32_t* spill_idx;    // [spill_cap] (slab set, group) index of each spilled run
+  uint64_t spill_cap;
   uint32_t NB, G;         // NB: a power of two (bucket index = (t / BW) & (NB - 1))
   uint32_t CAP;
   uint32_t gsh;           // log2(hosts per group); a group is served by one 64-lane wave
@@ -293,11 +316,14 @@ struct DevSim {
   SGN_GLB uint32_t* fin_cnt;      // [ceil(G / 64) + 1] arrival counters (chunks, then chunks done)
   SGN_GLB uint64_t* fin_keep;     // [ceil(G / 64)] per-chunk minima (atomicMin) of w_keep / w_next
   SGN_GLB uint64_t* fin_next;
+  SGN_GLB uint64_t* fin_occ;      // [ceil(G / 64)] per-chunk calendar occupancy change (two's complement sums)
   // persistent rounds (k_rounds): per round % 3, chunk minima {kept, next} and the minimum of
   // new runs for the window's last bucket, and the arrival counters (chunks, then chunks done)
   SGN_GLB uint64_t* rb_min;       // [3][64][2]
   SGN_GLB uint64_t* rb_keep;      // [3]
-  SGN_GLB uint32_t* rb_cnt;       // [3][65]
+  SGN_GLB uint32_t* rb_cnt;       // [3][65], then one monotone counter: the gap barrier (k_rounds)
+  SGN_GLB uint64_t* rb_occ;       // [3][64] per-chunk calendar occupancy change of the round,
+                                  // then rb_alloc [3] (pages allocated) and rb_spill [3] (runs spilled)
   uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
   uint32_t agg_bmin;      // the round kernels fold bucket minima in an LDS table (see engine.hip)
   uint32_t pad3;
@@ -327,6 +353,7 @@ struct DevSim {
   SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
 
+constexpr uint32_t XHDR = 2;  // multi-shard: message records (64 B) at the head of a peer's block
 constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute wave
 // event runs per (bucket, group) slab: one bucket's due runs of a group are ordered in LDS
 // (k_execute's dynamic LDS = CAP * 36 B), so CAP also sets k_execute's occupancy
@@ -340,6 +367,7 @@ struct sgn_ctx;
 // A CPU worker thread's staging buffer for sgn_submit (sgn_stage_*).
 struct sgn_stage {
   sgn_ctx* ctx = nullptr;
+  mutable std::mutex mu;  // the worker thread's pushes against a concurrent sgn_stage_flush
   std::vector<uint32_t> src, dst, pay, wire;
   std::vector<uint64_t> time, handle;
 };
@@ -405,8 +433,9 @@ struct sgn_ctx {
   // kernel timing
   struct KT {
     const char* name;
-    uint64_t launches = 0;
+    uint64_t launches = 0;   // timed (a sample of per-round launches)
     double ms = 0;
+    uint64_t total = 0;      // every launch
   };
   KT kt[16];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -424,6 +453,11 @@ struct sgn_ctx {
   bool use_graph = true;
   uint32_t persist_grid = 0;  // persistent-rounds grid size (0: per-round launches)
   uint32_t persist_fallbacks = 0;  // persistent launches refused by the residency census
+  bool persist_off = false;        // ... since sim_init: per-round launches from then on
+  uint32_t lds_per_cu = 0;         // LDS bytes per CU (device attribute; the residency model)
+  // pool growth (a held round, then a larger pool): counts for sgn_engine_info
+  uint64_t codel_grows = 0, cal_grows = 0, cal_spill_runs = 0, xslot_grows = 0, rounds_held = 0;
+  uint64_t codel_allocs_before = 0;  // page allocations before the last pool growth (its ring restarts)
   bool capturing = false;
 
   ~sgn_ctx();
@@ -433,6 +467,7 @@ namespace sgn {
 int set_error(sgn_ctx* ctx, int code, const std::string& msg);
 int hip_fail(sgn_ctx* ctx, hipError_t e, const char* what);
 void* dev_alloc(sgn_ctx* ctx, size_t bytes, bool zero = true);
+void dev_free(sgn_ctx* ctx, void* p, size_t bytes);
 void free_sim(sgn_ctx* ctx);
 void drop_graph(sgn_ctx* ctx);  // the captured batch of rounds, if any
 // multi-shard exchange (comm.cpp): runs per peer the first RCCL rounds move; bytes one

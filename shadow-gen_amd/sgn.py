@@ -177,12 +177,14 @@ class EngineInfo(C.Structure):
         "persistent_grid", "persistent_fallbacks", "device_bytes", "exchange_slot_runs",
         "exchange_send_runs", "exchange_hwm_runs", "exchange_spills", "exchange_bytes", "codel_pages",
         "codel_page_allocs", "codel_pages_free", "codel_pages_chained",
-        "compute_units", "bucket_min_lds")]
+        "compute_units", "bucket_min_lds", "lds_per_cu", "codel_pool_grows", "calendar_grows",
+        "calendar_spill_runs", "exchange_slot_grows", "rounds_held")]
 
 
 class KernelTimes(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 16), ("ms", C.c_double * 16),
-                ("name", C.c_char_p * 16), ("n_kernels", C.c_uint32)]
+                ("name", C.c_char_p * 16), ("n_kernels", C.c_uint32),
+                ("launches_total", C.c_uint64 * 16)]
 
 
 _lib = None
@@ -522,6 +524,12 @@ class Context:
         k = KernelTimes()
         self.check(self.L.sgn_kernel_times_get(self.h, C.byref(k)))
         return {k.name[i].decode(): (int(k.launches[i]), float(k.ms[i])) for i in range(k.n_kernels)}
+
+    def kernel_launches_total(self):
+        """Every launch of each engine kernel since sim_init (kernel_times() covers a sample)."""
+        k = KernelTimes()
+        self.check(self.L.sgn_kernel_times_get(self.h, C.byref(k)))
+        return {k.name[i].decode(): int(k.launches_total[i]) for i in range(k.n_kernels)}
 
 
 # ------------------------------------------------------------------------------------

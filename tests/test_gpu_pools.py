@@ -1,0 +1,108 @@
+"""Device pools that grow instead of refusing a scenario (-m gpu).
+
+The reference's queues are unbounded: the router's CoDelQueue has no limit
+(network/router/codel_queue.rs:33,303-317) and each host's EventQueue is a BinaryHeap
+(core/work/event_queue.rs:12,57-66). libsgn keeps them in device pools sized at sim_init; a
+round edge holds the rounds before a round that could outgrow a pool (nothing of that round
+has run), the host grows the pool, and the round runs:
+  * CoDel page pool: a round takes at most (D + 15 min(D, hosts)) / 16 pages for D due runs;
+  * calendar slabs: a run whose slab is full goes to a spill area, the round edge holds, and
+    the calendar is re-laid out with larger slabs before the run can be due.
+Every case is bit-exact against the oracle (which has unbounded std containers) and checks
+that the pools really grew and that no CoDel page was lost.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import sgn
+from test_gpu_parity import assert_same_run, ctxf, run_both, scenario  # noqa: F401 (ctxf: fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def _codel_args(n=300, codel=1):
+    # slow down-links make CoDel queues stand (thousands of runs at the slow hosts); codel=1:
+    # the pool starts at one page per host plus 64
+    bw = np.where(np.arange(n) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+    return scenario(n=n, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=2_000_000_000, bw=bw, tor=True,
+                    tgen_think=200_000_000, codel=codel)
+
+
+def _pages_ok(info):
+    assert info["codel_pages_free"] + info["codel_pages_chained"] == info["codel_pages"], info
+
+
+@pytest.mark.parametrize("persistent,trace", [("1", False), ("0", False), ("0", True)])
+def test_codel_pool_grows(ctxf, oracle, monkeypatch, persistent, trace):
+    monkeypatch.setenv("SGN_PERSISTENT", persistent)
+    args = _codel_args()
+    o, c = run_both(ctxf, oracle, args, trace=trace)
+    st, info = c.stats(), c.engine_info()
+    assert st["codel_dropped"] > 0 and st["max_codel_len"] > 1000, st
+    assert info["codel_pool_grows"] >= 1 and info["rounds_held"] >= 1, info
+    assert info["codel_pages"] > args[2].n + 64, info
+    assert (info["persistent_grid"] > 0) == (persistent == "1" and not trace), info
+    _pages_ok(info)
+    assert_same_run(o, c, args[2].n, trace=trace)
+
+
+@pytest.mark.parametrize("persistent,trace,hpw", [("1", False, "64"), ("0", False, "32"), ("0", True, "64")])
+def test_calendar_spill_relayout(ctxf, oracle, monkeypatch, persistent, trace, hpw):
+    # 16-run slabs and two datagrams per host per 1-ms bucket to random peers: ~128 runs per
+    # (bucket, host group) slab, so the first rounds spill and the calendar is re-laid out
+    monkeypatch.setenv("SGN_PERSISTENT", persistent)
+    monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    monkeypatch.setenv("SGN_HOSTS_PER_WAVE", hpw)
+    n = 2000
+    args = scenario(n=n, V=100, period_ns=500_000, stop_ns=150_000_000, bw=100_000_000)
+    o, c = run_both(ctxf, oracle, args, trace=trace)
+    info = c.engine_info()
+    assert info["calendar_grows"] >= 1 and info["calendar_spill_runs"] > 0, info
+    assert info["slab_capacity"] > 16 and info["rounds_held"] >= 1, info
+    assert c.stats()["packets_sent"] > 100_000
+    assert_same_run(o, c, n, trace=trace)
+
+
+def test_two_shards_grow_together(ctxf, oracle, monkeypatch):
+    """The multi-shard device path: every shard evaluates every shard's CoDel guard and spill
+    flag from the round-edge messages, so both hold the same round; each grows its own pools
+    (local shard-group transport on one GPU), identical to one unsharded shard."""
+    monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    n = 300
+    args = _codel_args(n=n)
+    g, used, hosts, cfg, tr = args
+    one = ctxf()
+    one.routes_build(g, used)
+    one.hosts_set(hosts)
+    one.sim_init(cfg, tr)
+    one.run()
+    shards = [ctxf(shard_rank=r, shard_count=2) for r in range(2)]
+    arr = (C.c_void_p * 2)(*[s.h.value for s in shards])
+    for s in shards:
+        s.routes_build(g, used)
+        s.hosts_set(hosts)
+    shards[0].check(shards[0].L.sgn_comm_init_local(arr, 2, 1 << 16))
+    for s in shards:
+        s.sim_init(cfg, tr)
+    done = C.c_uint64()
+    shards[0].check(shards[0].L.sgn_run_local_group(arr, 2, 1 << 40, C.byref(done)))
+    assert done.value == one.stats()["rounds"]
+    held = [s.engine_info()["rounds_held"] for s in shards]
+    assert held[0] == held[1] >= 1, held
+    assert max(s.engine_info()["codel_pool_grows"] for s in shards) >= 1
+    for r, s in enumerate(shards):
+        lo, hi = C.c_uint32(), C.c_uint32()
+        s.L.sgn_shard_range(n, r, 2, C.byref(lo), C.byref(hi))
+        d1, d2 = one.digests(lo.value, hi.value), s.digests(lo.value, hi.value)
+        for f in ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered",
+                  "n_codel_dropped"):
+            assert np.array_equal(d1[f], d2[f]), (r, f)
+        assert s.window() == one.window()
+        _pages_ok(s.engine_info())
+    # and the unsharded run against the oracle
+    lat, loss = oracle.routes(g, used)
+    o = oracle.Sim(used, lat, loss, hosts, cfg, tr)
+    o.run()
+    assert_same_run(o, one, n, trace=False)

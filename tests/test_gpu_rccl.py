@@ -34,7 +34,7 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload):
         env["SGN_XSZ_INIT"] = xsz
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "20000", "--rounds-per-step", "70",
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "100000", "--rounds-per-step", "70",
            "--workload", workload]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -42,7 +42,9 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload):
     assert line["n_gpus"] == 2
     assert line["apsp_sharded"]["equal_on_all_ranks"] is True
     assert line["parity"] is True, line.get("parity_detail")
-    assert line["parity_detail"]["hosts_compared"] == 40_000
+    # config C as BASELINE names it: 100k hosts in total, 2 x 50k (strong scaling)
+    assert line["parity_detail"]["hosts_compared"] == 100_000
+    assert line["config"]["hosts_total"] == 100_000 and line["scaling"] == "strong"
     assert line["rounds_timed"] == 140
     x = line["exchange"]
     assert x["hwm_runs"] > 0 and x["send_runs"] >= min(x["slot_runs"], x["hwm_runs"])

@@ -42,15 +42,19 @@ def _kernel_meta(so):
             continue
         notes = subprocess.run([str(llvm / "llvm-readelf"), "--notes", str(co)], capture_output=True,
                                text=True, check=True).stdout
-        cur = None
+        # one YAML map per kernel (it starts at "- .args"); its keys are sorted, so fields such
+        # as .group_segment_fixed_size come before .name
+        fields = {}
         for line in notes.splitlines():
+            if re.match(r"\s+- \.args:", line):
+                fields = {}
             m = re.match(r"\s+\.name:\s+(\S+)", line)
             if m:
-                cur = m.group(1)
-                out[cur] = {}
-            m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_count|vgpr_spill_count):\s+(\d+)", line)
-            if m and cur:
-                out[cur][m.group(1)] = int(m.group(2))
+                out[m.group(1)] = fields
+            m = re.match(r"\s+\.(private_segment_fixed_size|group_segment_fixed_size|vgpr_count|vgpr_spill_count):"
+                         r"\s+(\d+)", line)
+            if m:
+                fields[m.group(1)] = int(m.group(2))
     return out
 
 
@@ -60,10 +64,25 @@ def test_round_kernels_have_no_scratch():
     # the round kernels must keep every host's state in registers/LDS: a non-inlined helper
     # or a spill puts it in scratch memory and costs ~2x (seen when send_batch was outlined)
     meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
-    for k in ("k_rounds", "k_execute"):
+    # one instantiation per traffic kind; k_execute also per trace mode (traced / lean)
+    for k, count in (("k_rounds", 3), ("k_execute", 6)):
         names = [n for n in meta if k in n]
-        assert len(names) == 3, names  # one instantiation per traffic kind
+        assert len(names) == count, names
         for name in names:
             m = meta[name]
             assert m["private_segment_fixed_size"] == 0, (name, m)
             assert m["vgpr_spill_count"] == 0 and m["vgpr_count"] <= 256, (name, m)
+
+
+@pytest.mark.skipif(not pathlib.Path("/opt/rocm/lib/llvm/bin/clang-offload-bundler").exists(),
+                    reason="ROCm LLVM tools absent")
+def test_round_kernel_lds_budget():
+    # config C's persistent grid must stay entirely resident at one group per workgroup: its
+    # 1563 host groups need 7 workgroups per CU, i.e. static + dynamic LDS (64-run slabs:
+    # 64 x 36 B) within 45 granules of 512 B (7 x 23040 <= 160 KiB). A few dozen bytes more
+    # dropped the grid to 1536 and cost 14 % (round 3).
+    meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
+    for name, m in meta.items():
+        if "k_rounds" in name:
+            total = m["group_segment_fixed_size"] + 64 * 32 + 2 * 64 * 2
+            assert -(-total // 512) * 512 * 7 <= 160 * 1024, (name, m, total)
