@@ -350,6 +350,8 @@ def main():
                          "with its own NCCL_HOSTID, so RCCL accepts the ranks (as if on different hosts) "
                          "and moves the exchange over its socket transport; correctness only, not a "
                          "scaling measurement")
+    ap.add_argument("--exchange-slot", type=int, default=None,
+                    help="N > 1: per-peer exchange slot in runs (it grows when a round needs more)")
     ap.add_argument("--no-shard-check", action="store_true",
                     help="N > 1: skip the unsharded re-run on rank 0 that checks the sharded results")
     args = ap.parse_args()
@@ -402,7 +404,8 @@ def main():
         # peer at 100k hosts per GPU (overflow of the slot is detected and reported)
         # D (every host sends every 1 ms, 7/8 of it to other shards): ~1e6 x 7/8 / 7 runs per
         # peer per round at 1M hosts per GPU, so its slot holds 2^18 runs (8 MB per peer)
-        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, 1 << 18 if args.workload == "D" else 1 << 13))
+        slot = args.exchange_slot or (1 << 18 if args.workload == "D" else 1 << 13)
+        ctx.check(ctx.L.sgn_comm_init(ctx.h, idb, slot))
     # with the communicator set, large graphs (>= 2048 used nodes) build the APSP sharded: each
     # GPU computes its block of used sources and the blocks are exchanged over RCCL
     # (DESIGN.md §5); smaller ones build it whole on every GPU (~1 ms)

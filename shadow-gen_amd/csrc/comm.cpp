@@ -75,6 +75,7 @@ int sgn_comm_init(sgn_ctx* ctx, const uint8_t id[SGN_COMM_ID_BYTES], uint64_t sl
 namespace sgn {
 int ctrl_sync(sgn_ctx* ctx);  // engine.hip: the control block to the host, overflow check
 int resolve_pools(sgn_ctx* ctx);  // engine.hip: a held round edge's pool growth
+int grow_exchange_slot(sgn_ctx* ctx);  // engine.hip: larger exchange slots (runs past a slot)
 
 uint64_t comm_round_bytes(const sgn_ctx* ctx) {
   return ctx->nranks > 1 && ctx->comm ? (uint64_t)(ctx->nranks - 1) * ((uint64_t)(XHDR + ctx->xsz_cur) * sizeof(EvRec)) : 0;
@@ -121,6 +122,9 @@ int comm_round_exchange(sgn_ctx* ctx) {
 // batch moved the same slots again and their kernels returned at once. Complete it: the
 // whole slots, k_import again (which advances the window), and a larger exchange size.
 int comm_complete_spill(sgn_ctx* ctx) {
+  // some shard spilled runs past a slot: every shard grows its slots alike first
+  if (ctx->h_ctrl->xhwm > ctx->S.xslot)
+    if (int rc = grow_exchange_slot(ctx)) return rc;
   DevSim& S = ctx->S;
   hipStream_t st = ctx->stream;
   SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)&S.ctrl->xsz, (int)S.xslot, 1, st));
@@ -223,25 +227,45 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
     }
     for (uint32_t i = 0; i < n; i++) SGN_HIP(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
     // the all-to-all: shard b's receive slot and message a <- shard a's send slot and
-    // message b (what comm_round_exchange's grouped send/recv does)
-    for (uint32_t a = 0; a < n; a++) {
-      sgn_ctx* A = ctxs[a];
-      const size_t blk = (size_t)A->S.xslot + XHDR;
-      for (uint32_t b = 0; b < n; b++) {
-        if (b == a) continue;
-        sgn_ctx* B = ctxs[b];
-        uint64_t msg[4 * XHDR];
-        SGN_HIP(A, hipMemcpy(msg, (const void*)(A->S.xout + (size_t)b * blk), sizeof(msg), hipMemcpyDeviceToHost));
-        const uint64_t k = std::min<uint64_t>(msg[0], A->xslot);
-        SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * blk), (const void*)(A->S.xout + (size_t)b * blk),
-                             (size_t)(XHDR + k) * sizeof(EvRec), hipMemcpyDefault));
+    // message b (what comm_round_exchange's grouped send/recv does), then k_import everywhere
+    auto exchange_import = [&]() -> int {
+      for (uint32_t a = 0; a < n; a++) {
+        sgn_ctx* A = ctxs[a];
+        const size_t blk = (size_t)A->S.xslot + XHDR;
+        for (uint32_t b = 0; b < n; b++) {
+          if (b == a) continue;
+          sgn_ctx* B = ctxs[b];
+          uint64_t msg[4 * XHDR];
+          SGN_HIP(A, hipMemcpy(msg, (const void*)(A->S.xout + (size_t)b * blk), sizeof(msg), hipMemcpyDeviceToHost));
+          const uint64_t k = std::min<uint64_t>(msg[0], A->xslot);
+          SGN_HIP(B, hipMemcpy((void*)(B->S.xin + (size_t)a * blk), (const void*)(A->S.xout + (size_t)b * blk),
+                               (size_t)(XHDR + k) * sizeof(EvRec), hipMemcpyDefault));
+        }
       }
-    }
-    for (uint32_t i = 0; i < n; i++) {
-      sgn_ctx* c = ctxs[i];
-      SGN_HIP(c, hipSetDevice(c->device));
-      launch_import(c);
-      SGN_HIP(c, hipStreamSynchronize(c->stream));
+      for (uint32_t i = 0; i < n; i++) {
+        sgn_ctx* c = ctxs[i];
+        SGN_HIP(c, hipSetDevice(c->device));
+        launch_import(c);
+        SGN_HIP(c, hipStreamSynchronize(c->stream));
+      }
+      return 0;
+    };
+    if (int rc = exchange_import()) return rc;
+    // a round some shard spilled runs past a slot in was held by every shard alike: the slots
+    // grow (the same size everywhere) and the round is exchanged and imported again
+    if (int rc = ctrl_sync(ctxs[0])) return rc;
+    if (ctxs[0]->h_ctrl->xspill) {
+      for (uint32_t i = 0; i < n; i++) {
+        sgn_ctx* c = ctxs[i];
+        if (int rc = ctrl_sync(c)) return rc;
+        if (c->h_ctrl->xhwm > c->S.xslot)
+          if (int rc = grow_exchange_slot(c)) return rc;
+        SGN_HIP(c, hipMemsetD32Async((hipDeviceptr_t)&c->S.ctrl->xspill, 0, 1, c->stream));
+        SGN_HIP(c, hipMemsetD32Async((hipDeviceptr_t)&c->S.ctrl->xsz, (int)c->S.xslot, 1, c->stream));
+        c->xsz_cur = c->S.xslot;
+        SGN_HIP(c, hipStreamSynchronize(c->stream));
+      }
+      if (int rc = exchange_import()) return rc;
     }
     // a held round edge (the same on every shard) or a spill: the pools grow before the next
     for (uint32_t i = 0; i < n; i++) {

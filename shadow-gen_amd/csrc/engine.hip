@@ -1245,12 +1245,9 @@ struct HostExec {
       }
       atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
       pos = atomicAdd(&S.xout_n[lo], nrec);
+      sidx = SPILL_PEER | lo;  // (runs beyond the peer's slot: the slot grows at a held round)
       dstp = S.xout + (size_t)lo * (S.xslot + XHDR) + XHDR;  // (a peer's block starts with the message)
       cap = S.xslot;
-    }
-    if (!owned && pos + nrec > cap) {
-      overflow(OVF_EXCHANGE);
-      return;
     }
     for (uint32_t m = 0; m < nrec; m++) {
       const uint32_t k = min(RUN_MAX, nsent - m * RUN_MAX);
@@ -1263,7 +1260,7 @@ struct HostExec {
       r.tag = tag;
       if (pos + m < cap)
         st_dev_rec(dstp + pos + m, r);
-      else  // (owned: the slab is full)
+      else  // the slab (or the peer's exchange slot) is full
         spill_run(S, ob, sidx, r);
     }
   }
@@ -2527,7 +2524,8 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
     gm = x > gm ? x : gm;
   }
   const uint32_t sz = C->xsz;
-  const bool hold = gm > sz && sz < S.xslot;
+  // (gm > xslot: some shard spilled runs past a slot; the host grows the slots, then completes)
+  const bool hold = gm > sz && (sz < S.xslot || gm > S.xslot);
   // the window that just ran (still C->ws): the same horizon as sends
   const uint64_t hz = SIM_START + (S.bw_div.div(C->ws - SIM_START) + S.NB) * S.BW;
   uint32_t filed = 0;
@@ -2639,6 +2637,7 @@ __global__ void k_respill(const EvRec* __restrict__ spill, const uint32_t* __res
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t idx = spill_idx[i];
+  if (idx & SPILL_PEER) return;  // a run for another shard (grow_exchange_slot)
   const uint32_t pos = atomicAdd(&cursor[idx], 1u);
   if (pos < cap) pool[(size_t)idx * cap + pos] = spill[i];
 }
@@ -3007,6 +3006,49 @@ int grow_codel(sgn_ctx* ctx, uint64_t extra) {
   return upload_sim(ctx);
 }
 
+// Multi-shard: a round in which some shard had more runs for a peer than a slot holds (the
+// messages carry every shard's largest count, so every shard grows alike to twice that):
+// the slots grow, keeping each outgoing block's message and runs, and the runs that went to
+// the spill area (tagged SPILL_PEER | peer) follow them; comm_complete_spill then moves the
+// whole slots and completes the round.
+int grow_exchange_slot_impl(sgn_ctx* ctx) {
+  DevSim& S = ctx->S;
+  const uint64_t hwm = ctx->h_ctrl->xhwm;
+  uint64_t ns = S.xslot;
+  while (ns < 2 * hwm) ns *= 2;
+  if (ns > (1ULL << 26)) return set_error(ctx, SGN_EOVERFLOW, "exchange slot above 2^26 runs per peer");
+  const size_t ob = XHDR + (size_t)S.xslot, nb = XHDR + (size_t)ns, R = S.n_ranks;
+  EvRec* nxo = (EvRec*)dev_alloc(ctx, R * nb * sizeof(EvRec), true);
+  EvRec* nxi = (EvRec*)dev_alloc(ctx, R * nb * sizeof(EvRec), true);
+  if (!nxo || !nxi) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange slot growth)");
+  // (xin too: this shard's own message sits in its incoming block)
+  for (size_t p = 0; p < R; p++) {
+    SGN_HIP(ctx, hipMemcpy(nxo + p * nb, (const void*)(S.xout + p * ob), ob * sizeof(EvRec), hipMemcpyDeviceToDevice));
+    SGN_HIP(ctx, hipMemcpy(nxi + p * nb, (const void*)(S.xin + p * ob), ob * sizeof(EvRec), hipMemcpyDeviceToDevice));
+  }
+  const uint64_t n = std::min<uint64_t>(ctx->h_ctrl->spill_n, S.spill_cap);
+  if (n) {
+    std::vector<uint32_t> idx(n);
+    std::vector<EvRec> rec(n);
+    SGN_HIP(ctx, hipMemcpy(idx.data(), (const void*)S.spill_idx, n * 4, hipMemcpyDeviceToHost));
+    SGN_HIP(ctx, hipMemcpy(rec.data(), (const void*)S.spill, n * sizeof(EvRec), hipMemcpyDeviceToHost));
+    std::vector<std::vector<EvRec>> per(R);
+    for (uint64_t i = 0; i < n; i++)
+      if (idx[i] & SPILL_PEER) per[idx[i] & ~SPILL_PEER].push_back(rec[i]);
+    for (size_t p = 0; p < R; p++)
+      if (!per[p].empty())
+        SGN_HIP(ctx, hipMemcpy(nxo + p * nb + ob, per[p].data(), per[p].size() * sizeof(EvRec), hipMemcpyHostToDevice));
+  }
+  dev_free(ctx, (void*)S.xout, R * ob * sizeof(EvRec));
+  dev_free(ctx, (void*)S.xin, R * ob * sizeof(EvRec));
+  S.xout = (decltype(S.xout))nxo;
+  S.xin = (decltype(S.xin))nxi;
+  S.xslot = (uint32_t)ns;
+  ctx->xslot = ns;
+  ctx->xslot_grows++;
+  return upload_sim(ctx);
+}
+
 // A round edge held the rounds (Ctrl::hold; nothing of the next round has run): the calendar
 // is re-laid out after a spill, the CoDel pool grows until its free pages cover the next
 // round's bound, and the rounds are released. (Multi-shard: every shard holds the same round;
@@ -3130,6 +3172,7 @@ void time_collect(sgn_ctx* ctx) {
 }
 
 int ctrl_sync(sgn_ctx* ctx) { return sync_ctrl(ctx); }
+int grow_exchange_slot(sgn_ctx* ctx) { return grow_exchange_slot_impl(ctx); }
 int resolve_pools(sgn_ctx* ctx) { return resolve_hold(ctx); }
 
 void drop_graph(sgn_ctx* ctx) {

@@ -353,6 +353,7 @@ struct DevSim {
   SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
 };
 
+constexpr uint32_t SPILL_PEER = 0x80000000u;  // spill area tag: a run for that peer shard's exchange slot
 constexpr uint32_t XHDR = 2;  // multi-shard: message records (64 B) at the head of a peer's block
 constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute wave
 // event runs per (bucket, group) slab: one bucket's due runs of a group are ordered in LDS

@@ -65,10 +65,13 @@ def test_calendar_spill_relayout(ctxf, oracle, monkeypatch, persistent, trace, h
     assert_same_run(o, c, n, trace=trace)
 
 
-def test_two_shards_grow_together(ctxf, oracle, monkeypatch):
+@pytest.mark.parametrize("slot", [1 << 16, 16])
+def test_two_shards_grow_together(ctxf, oracle, monkeypatch, slot):
     """The multi-shard device path: every shard evaluates every shard's CoDel guard and spill
     flag from the round-edge messages, so both hold the same round; each grows its own pools
-    (local shard-group transport on one GPU), identical to one unsharded shard."""
+    (local shard-group transport on one GPU), identical to one unsharded shard. slot = 16:
+    runs past a peer's exchange slot spill, the round is held on both shards, the slots grow
+    alike and the round is exchanged again."""
     monkeypatch.setenv("SGN_SLAB_CAP", "16")
     n = 300
     args = _codel_args(n=n)
@@ -83,7 +86,7 @@ def test_two_shards_grow_together(ctxf, oracle, monkeypatch):
     for s in shards:
         s.routes_build(g, used)
         s.hosts_set(hosts)
-    shards[0].check(shards[0].L.sgn_comm_init_local(arr, 2, 1 << 16))
+    shards[0].check(shards[0].L.sgn_comm_init_local(arr, 2, slot))
     for s in shards:
         s.sim_init(cfg, tr)
     done = C.c_uint64()
@@ -92,6 +95,9 @@ def test_two_shards_grow_together(ctxf, oracle, monkeypatch):
     held = [s.engine_info()["rounds_held"] for s in shards]
     assert held[0] == held[1] >= 1, held
     assert max(s.engine_info()["codel_pool_grows"] for s in shards) >= 1
+    if slot == 16:
+        assert all(s.engine_info()["exchange_slot_grows"] >= 1 for s in shards)
+        assert shards[0].engine_info()["exchange_slot_runs"] == shards[1].engine_info()["exchange_slot_runs"] > 16
     for r, s in enumerate(shards):
         lo, hi = C.c_uint32(), C.c_uint32()
         s.L.sgn_shard_range(n, r, 2, C.byref(lo), C.byref(hi))

@@ -26,16 +26,24 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 # early rounds exceed it, so they are held and completed with the whole slot (spill path)
 # workload D: every host sends to a random peer every round (half of it to the other shard),
 # through the LDS bucket minima of the PERIODIC kernel and a spill to a larger exchange size
-@pytest.mark.parametrize("graph,xsz,port,workload", [("1", "", 29541, "C"), ("0", "", 29542, "C"),
-                                                     ("1", "16", 29543, "C"), ("0", "", 29544, "D")])
-def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload):
+# pools: a one-page-per-host CoDel pool, 16-run calendar slabs and a 64-run exchange slot, so
+# rounds are held on both ranks alike (guards evaluated from the round-edge messages) while the
+# pools and the slots grow over real RCCL
+@pytest.mark.parametrize("graph,xsz,port,workload,pools", [("1", "", 29541, "C", False), ("0", "", 29542, "C", False),
+                                                           ("1", "16", 29543, "C", False), ("0", "", 29544, "D", False),
+                                                           ("0", "", 29545, "C", True)])
+def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload, pools):
     env = dict(os.environ, SGN_GRAPH=graph, NCCL_DEBUG="WARN", TMPDIR="/tmp")
     if xsz:
         env["SGN_XSZ_INIT"] = xsz
+    extra = []
+    if pools:
+        env["SGN_SLAB_CAP"] = "16"
+        extra = ["--codel-cap", "1", "--exchange-slot", "64"]
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "100000", "--rounds-per-step", "70",
-           "--workload", workload]
+           "--workload", workload] + extra
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
@@ -50,3 +58,5 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload):
     assert x["hwm_runs"] > 0 and x["send_runs"] >= min(x["slot_runs"], x["hwm_runs"])
     if xsz:
         assert x["spills"] >= 1
+    if pools:
+        assert x["slot_runs"] > 64 and x["spills"] >= 1
