@@ -216,6 +216,8 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
   for (uint32_t i = 0; i < n; i++)
     if (!ctxs[i] || !ctxs[i]->sim_ready || !ctxs[i]->comm_local || ctxs[i]->group.size() != n)
       return ctxs[i] ? set_error(ctxs[i], SGN_ESTATE, "not a local shard group") : SGN_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    if (int rc = rng_release(ctxs[i])) return rc;
   uint64_t done = 0;
   for (; done < max_rounds; done++) {
     Ctrl h{};

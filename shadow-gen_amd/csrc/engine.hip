@@ -2669,6 +2669,20 @@ __global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* c
   R->rng_pos += count[i];
 }
 
+// CPU-held host RNG states back into the records (sgn_rng_* single draws): per entry
+// {slot, s0..s3, draws}; the stream position advances by the draws made on the CPU
+__global__ void k_rng_set(const DevSim* Sp, const uint64_t* st, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t* e = st + 6 * (size_t)i;
+  SGN_GLB HostRec* R = Sp->hrec + (uint32_t)e[0];
+  R->rng[0] = e[1];
+  R->rng[1] = e[2];
+  R->rng[2] = e[3];
+  R->rng[3] = e[4];
+  R->rng_pos += e[5];
+}
+
 // Host::next_event_time (host.rs:832-834) for the owned HostIds [lo, lo + n), between rounds:
 // the earliest local event (the host record's slots) ...
 __global__ void k_next_local(const DevSim* Sp, uint32_t lo, uint32_t n, uint64_t* out) {
@@ -3188,6 +3202,10 @@ void drop_graph(sgn_ctx* ctx) {
 
 void free_sim(sgn_ctx* ctx) {
   drop_graph(ctx);
+  ctx->rng_held.clear();
+  if (ctx->d_rng_stage) hipFree(ctx->d_rng_stage);
+  ctx->d_rng_stage = nullptr;
+  ctx->rng_stage_cap = 0;
   for (void* p : ctx->allocs) hipFree(p);
   ctx->allocs.clear();
   ctx->sim_bytes = 0;
@@ -3553,6 +3571,7 @@ int sgn_window(sgn_ctx* ctx, uint64_t* start, uint64_t* end, int32_t* active) {
 
 int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
   if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  if (int e = rng_release(ctx)) return e;
   if (ctx->comm_local)
     return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_round");
   int rc = sync_ctrl(ctx);
@@ -3568,6 +3587,7 @@ int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
 
 int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
+  if (int e = rng_release(ctx)) return e;
   if (ctx->comm_local)
     return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_run");
   int rc = sync_ctrl(ctx);
@@ -3734,6 +3754,7 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
   if (!ctx || !out) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   if (lo < ctx->lo || hi > ctx->hi || lo > hi) return set_error(ctx, SGN_EINVAL, "range outside the owned shard");
+  if (int e = rng_release(ctx)) return e;
   int rc = sync_ctrl(ctx);
   const uint32_t n = hi - lo;
   // the range's hosts sit in permuted slots: read the slots they span
@@ -4126,7 +4147,38 @@ int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end) {
   return 0;
 }
 
+
 namespace {
+// rand_xoshiro 0.7.0 Xoshiro256PlusPlus::next_u64 on the CPU (a CPU-held host state)
+inline uint64_t host_xoshiro_next(uint64_t* s) {
+  auto rotl = [](uint64_t x, int k) { return (x << k) | (x >> (64 - k)); };
+  const uint64_t r = rotl(s[0] + s[3], 23) + s[0], t = s[1] << 17;
+  s[2] ^= s[0];
+  s[3] ^= s[1];
+  s[1] ^= s[2];
+  s[0] ^= s[3];
+  s[2] ^= t;
+  s[3] = rotl(s[3], 45);
+  return r;
+}
+// n single draws of one owned host on the CPU: the first draw after a device operation reads
+// the state (one 32-byte copy); later ones are a few nanoseconds each
+int rng_cpu_draws(sgn_ctx* ctx, uint32_t host, uint64_t n, uint64_t* out) {
+  if (!ctx) return SGN_EINVAL;
+  if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
+  if (host < ctx->lo || host >= ctx->hi) return set_error(ctx, SGN_EINVAL, "host not owned by this shard");
+  const uint32_t slot = ctx->sid_of[host] - ctx->lo;
+  auto it = ctx->rng_held.find(slot);
+  if (it == ctx->rng_held.end()) {
+    sgn_ctx::RngHeld h{};
+    SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    SGN_HIP(ctx, hipMemcpy(h.s, (const void*)(ctx->S.hrec + slot), 32, hipMemcpyDeviceToHost));
+    it = ctx->rng_held.emplace(slot, h).first;
+  }
+  for (uint64_t i = 0; i < n; i++) out[i] = host_xoshiro_next(it->second.s);
+  it->second.draws += n;
+  return 0;
+}
 // counts[i] draws from each of n distinct owned hosts, concatenated in order into out
 int rng_draws(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint32_t n, uint64_t* out) {
   if (!ctx || (n && (!hosts || !counts))) return SGN_EINVAL;
@@ -4147,6 +4199,7 @@ int rng_draws(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint3
     return set_error(ctx, SGN_EINVAL, "sgn_rng_next_u64_batch: hosts must be distinct");
   if (total && !out) return SGN_EINVAL;
   if (n == 0) return 0;
+  if (int rc = rng_release(ctx)) return rc;
   SGN_HIP(ctx, hipSetDevice(ctx->device));
   char* d = nullptr;
   const size_t bytes = (size_t)n * (4 + 4 + 8) + total * 8 + 16;
@@ -4170,7 +4223,7 @@ int rng_draws(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint3
   return 0;
 }
 int rng_draw(sgn_ctx* ctx, uint32_t host, uint32_t n, uint64_t* out) {
-  return rng_draws(ctx, &host, &n, 1, out);
+  return rng_cpu_draws(ctx, host, n, out);
 }
 }  // namespace
 
@@ -4224,6 +4277,40 @@ int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
 
 // hooks used by comm.cpp
 namespace sgn {
+// The CPU-held states go back before anything on the device uses a host RNG (rounds, batch
+// draws, digests): one small upload and one kernel, stream-ordered (no host wait).
+int rng_release(sgn_ctx* ctx) {
+  if (ctx->rng_held.empty() || !ctx->sim_ready) {
+    ctx->rng_held.clear();
+    return 0;
+  }
+  std::vector<uint64_t> st;
+  st.reserve(ctx->rng_held.size() * 6);
+  for (auto& kv : ctx->rng_held) {
+    if (!kv.second.draws) continue;
+    st.push_back(kv.first);
+    for (int k = 0; k < 4; k++) st.push_back(kv.second.s[k]);
+    st.push_back(kv.second.draws);
+  }
+  ctx->rng_held.clear();
+  const uint32_t n = (uint32_t)(st.size() / 6);
+  if (!n) return 0;
+  SGN_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->rng_stage_cap < st.size()) {
+    if (ctx->d_rng_stage) hipFree(ctx->d_rng_stage);
+    ctx->d_rng_stage = nullptr;
+    ctx->rng_stage_cap = 0;
+    SGN_HIP(ctx, hipMalloc(&ctx->d_rng_stage, st.size() * 8));
+    ctx->rng_stage_cap = st.size();
+  }
+  SGN_HIP(ctx, hipMemcpyAsync(ctx->d_rng_stage, st.data(), st.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_rng_set, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, (const DevSim*)ctx->d_S,
+                     (const uint64_t*)ctx->d_rng_stage, n);
+  SGN_HIP(ctx, hipGetLastError());
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));  // (the staging vector goes out of scope)
+  return 0;
+}
+
 void launch_execute(sgn_ctx* ctx) { launch_k_execute(ctx, ctx->stream); }
 // k_import files the received runs and its last block advances the window
 void launch_import(sgn_ctx* ctx) {

@@ -16,6 +16,7 @@
 
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "sgn.h"
@@ -418,6 +419,16 @@ struct sgn_ctx {
   std::vector<sgn_drain_rec> drain_held;  // drained from the device, not yet returned
   void* d_stage = nullptr;                // sgn_submit staging (device)
   std::vector<sgn_stage*> stages;         // sgn_stage_create order
+  // CPU-side draws of host RNGs (sgn_rng_next_u64 / _double / _fill_bytes) between rounds: a
+  // host's state is read once, stepped on the CPU, and written back (with its stream position)
+  // before the next device operation that uses it (sgn::rng_release)
+  struct RngHeld {
+    uint64_t s[4];
+    uint64_t draws;  // since it was read
+  };
+  std::unordered_map<uint32_t, RngHeld> rng_held;  // by slot
+  void* d_rng_stage = nullptr;
+  uint64_t rng_stage_cap = 0;
   std::mutex stage_mu;
   uint64_t stage_cap = 0;
   uint64_t rounds_enqueued = 0;
@@ -477,6 +488,7 @@ constexpr uint32_t kXszInit = 512;
 uint64_t comm_round_bytes(const sgn_ctx* ctx);
 int comm_complete_spill(sgn_ctx* ctx);
 int ensure_host_routes(sgn_ctx* ctx);
+int rng_release(sgn_ctx* ctx);  // CPU-held host RNG states back to the device (stream-ordered)
 // timing helpers around a launch
 void time_begin(sgn_ctx* ctx, int kernel);
 void time_end(sgn_ctx* ctx);

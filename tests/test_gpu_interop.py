@@ -92,6 +92,38 @@ def test_rng_batch_is_the_host_stream(oracle):
         c.rng_next_u64_batch([3, 3], [1, 1])
 
 
+def test_rng_single_draws_cpu_held(oracle):
+    """sgn_rng_next_u64 / _double / _fill_bytes between rounds: the host's state is read once,
+    stepped on the CPU and written back (with the stream position) before the next device
+    operation — interleaved with batch draws, rounds and digests, draw for draw the host
+    stream; the per-call cost is reported (a device round trip only on a host's first draw
+    after a device operation)."""
+    import time
+    o, c, hosts, *_ = _pair(oracle, n=64, V=16, kind=sgn.TRAFFIC_PERIODIC)
+    for _ in range(10):
+        assert o.round() == c.round()
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        assert c.rng_double(9) == o.rng_double(9)
+    per_call_us = (time.perf_counter() - t0) / 2000 * 1e6
+    print(f"sgn_rng_double per call: {per_call_us:.2f} us (incl. the oracle's call)")
+    assert c.rng_next_u64(9) == o.rng_next_u64(9)
+    # a batch draw of the same host continues the CPU-held stream
+    got = c.rng_next_u64_batch(np.array([9, 4], np.uint32), np.array([5, 2], np.uint32))
+    want = [o.rng_next_u64(9) for _ in range(5)] + [o.rng_next_u64(4) for _ in range(2)]
+    assert got.tolist() == want
+    for _ in range(3):
+        assert c.rng_next_u64(4) == o.rng_next_u64(4)
+    assert c.rng_fill_bytes(4, 13) == o.rng_fill_bytes(4, 13)
+    d_o, d_c = o.digests(0, 64), c.digests(0, 64)  # digests see the CPU-held states
+    assert np.array_equal(d_o["rng"], d_c["rng"])
+    for _ in range(20):
+        assert o.round() == c.round()
+    d_o, d_c = o.digests(0, 64), c.digests(0, 64)
+    assert np.array_equal(d_o["rng"], d_c["rng"]) and np.array_equal(d_o["tx"], d_c["tx"])
+    assert per_call_us < 50
+
+
 class _Staged:
     """A CPU controller with three worker threads: each host's datagrams go through the
     stage of the thread that owns the host (host % 3), then one flush per round."""
