@@ -558,7 +558,8 @@ def main():
         "hbm_footprint_bytes": info["device_bytes"],
         "engine": {k: info[k] for k in ("calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity",
                                         "persistent_grid", "persistent_fallbacks", "codel_pages",
-                                        "codel_page_allocs", "bucket_min_lds")},
+                                        "codel_page_allocs", "bucket_min_lds", "codel_pool_grows",
+                                        "calendar_grows", "exchange_slot_grows", "rounds_held")},
     }
     if world > 1:
         # the round exchange: per-peer slot, runs per peer a round moves now

@@ -447,6 +447,29 @@ struct HostExec {
 #endif
   }
 
+  // PERIODIC traffic: the app's next datagram goes to a peer that is a hash of the app counter
+  // (sgn_periodic_dst), so its route can be in the route cache before the event loop needs it.
+  // prefetch_peer() issues the peer's load right after load(); prefetch_route() (after the
+  // gather's sort, so the load's latency hides behind it) fetches the route entry. A cache
+  // fill only: the entry is a pure function of (this host's node, the peer).
+  uint32_t pf_peer;
+  uint64_t pf_pi;
+  __device__ __forceinline__ void prefetch_peer() {
+    uint32_t peer = NO_HOST, uip = 0;
+    if (!sgn_periodic_dst(S.flow_seed, gid, L->app_k, S.n_all, S.unknown_permille, &peer, &uip) || peer == L->rc_dst)
+      peer = NO_HOST;
+    pf_peer = peer;
+    pf_pi = peer != NO_HOST ? S.peer[peer] : 0;
+  }
+  __device__ __forceinline__ void prefetch_route() {
+    if (pf_peer == NO_HOST) return;
+    const RouteEnt re = S.route[(size_t)my_unode * S.U + (uint32_t)(pf_pi >> 32)];
+    L->rc_dst = pf_peer;
+    L->rc_sid = (uint32_t)pf_pi;
+    L->rc_lat = re.lat;
+    L->rc_T = re.T;
+  }
+
   __device__ __forceinline__ void store() {
     HostRec& r = *R;
     r.rng[0] = r0;
@@ -1092,16 +1115,18 @@ struct HostExec {
     } else {
       DG(DG_RMISS);
       DGT_BEGIN(trt);
-      dsid = S.sid_of[dst];
-      const size_t ri = (size_t)my_unode * S.U + S.unode[dst];
-      const float rel32 = __fsub_rn(1.0f, S.rloss[ri]);
-      delay = S.rlat[ri];
+      // the peer's slot and used node (one load), then its route entry (one 16-byte load):
+      // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53;
+      // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an exact
+      // integer T (precomputed per route, sim_init) and the test is (x >> 11) >= T, bit for
+      // bit the same decision
+      const uint64_t pi = S.peer[dst];
+      dsid = (uint32_t)pi;
+      const RouteEnt re = S.route[(size_t)my_unode * S.U + (uint32_t)(pi >> 32)];
+      delay = re.lat;
+      T = re.T;
       DGT_WAIT();
       DGT_END(DGT_RTLD, trt);
-      // drop iff chance >= reliability (worker.rs:366-371) with chance = (x >> 11) * 2^-53:
-      // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an
-      // exact integer T and the test is (x >> 11) >= T, bit for bit the same decision
-      T = (uint64_t)((double)rel32 * 9007199254740992.0);
       L->rc_dst = dst;
       L->rc_sid = dsid;
       L->rc_lat = delay;
@@ -1853,6 +1878,15 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     }
     const uint32_t nraw = ld_dev(&S.slab_n[ib]);
     const uint32_t n1raw = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
+    // PERIODIC traffic (configs B and D: most executed hosts have their app timer due): the
+    // host record of a lane whose local event is due in the window loads in the same round trip
+    // as the gather, and the app's next route is prefetched behind the sort
+    const bool early = kApp == SGN_TRAFFIC_PERIODIC && bi == 0 && valid && lmin < we;
+    if (early) {
+      ex.load();
+      ex.prefetch_peer();
+      loaded = true;
+    }
     const uint32_t n = min(nraw, S.CAP);
     const uint32_t n1 = min(n1raw, S.CAP);
     // a slab with runs in the spill area: the calendar was not re-laid out before the runs are
@@ -1908,6 +1942,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       lc[a + rank] = (uint16_t)idx;
     }
     sorted += cnt > 1 ? 1u : 0u;
+    if (early) ex.prefetch_route();
     __syncthreads();
     // ---- 3. execute the sub-window [.., sub_end) ----
     const uint64_t c1 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -3396,6 +3431,24 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   };
   int rc = 0;
   if ((rc = up32(ctx->sid_of, &S.sid_of)) || (rc = up32(ctx->host_of, &S.host_of))) return rc;
+  {  // the packet path's peer and route forms (send_batch: two loads per route-cache miss)
+    std::vector<uint64_t> pe(N);
+    for (uint32_t i = 0; i < N; i++) pe[i] = (uint64_t)ctx->sid_of[i] | ((uint64_t)ctx->unode[i] << 32);
+    if ((rc = up64(pe, &S.peer))) return rc;
+    if ((rc = ensure_host_routes(ctx))) return rc;
+    const size_t UU = (size_t)ctx->U * ctx->U;
+    std::vector<RouteEnt> re(UU);
+    for (size_t i = 0; i < UU; i++) {
+      // reliability = (f64)(1.0f - loss) (worker.rs:363-371), exactly as the device would
+      volatile float rel32 = 1.0f - ctx->h_loss[i];
+      re[i].lat = ctx->h_lat[i];
+      re[i].T = (uint64_t)((double)rel32 * 9007199254740992.0);
+    }
+    RouteEnt* d = (RouteEnt*)dev_alloc(ctx, UU * sizeof(RouteEnt), false);
+    if (!d) return set_error(ctx, SGN_ENOMEM, "device allocation failed (route table)");
+    SGN_HIP(ctx, hipMemcpy(d, re.data(), UU * sizeof(RouteEnt), hipMemcpyHostToDevice));
+    S.route = (decltype(S.route))d;
+  }
   S.hrec = (decltype(S.hrec))dalloc<HostRec>(ctx, nH);
   S.codel = (decltype(S.codel))dalloc<CodelEnt>(ctx, (size_t)S.cq_pages * CQ_PAGE);
   S.cq_next = (decltype(S.cq_next))dalloc<uint32_t>(ctx, S.cq_pages);

@@ -80,6 +80,16 @@ struct __attribute__((aligned(16))) FifoEnt {
 };
 static_assert(sizeof(FifoEnt) == 16, "");
 
+// A route entry as the packet path reads it (WorkerShared::latency / reliability,
+// worker.rs:523-537): the latency and the integer loss threshold T = reliability * 2^53
+// (reliability = (f64)(1.0f - loss); the drop test is (x >> 11) >= T, see send_batch) — one
+// 16-byte load instead of a latency line and a loss line.
+struct __attribute__((aligned(16))) RouteEnt {
+  uint64_t lat;
+  uint64_t T;
+};
+static_assert(sizeof(RouteEnt) == 16, "");
+
 // Round control block, device resident. The window advances on the device.
 struct Ctrl {
   uint64_t ws, we;        // current window [ws, we)
@@ -275,6 +285,8 @@ struct DevSim {
   // same kind (server / client, bandwidth class) share waves (their event loops converge).
   // A slot id (sid) is lo + slot; event records carry the destination's sid.
   SGN_GLB const uint32_t* sid_of;   // [n_all] HostId -> sid (every shard's permutation)
+  SGN_GLB const uint64_t* peer;     // [n_all] HostId -> sid | used-node index << 32 (one load per peer)
+  SGN_GLB const RouteEnt* route;    // [U x U] {latency, loss threshold} (routing table, packet-path form)
   SGN_GLB const uint32_t* host_of;  // [nH] slot -> HostId of this shard
   SGN_GLB const uint32_t* dns_key;
   SGN_GLB const uint32_t* dns_val;

@@ -42,11 +42,11 @@ def _kernel_meta(so):
             continue
         notes = subprocess.run([str(llvm / "llvm-readelf"), "--notes", str(co)], capture_output=True,
                                text=True, check=True).stdout
-        # one YAML map per kernel (it starts at "- .args"); its keys are sorted, so fields such
-        # as .group_segment_fixed_size come before .name
+        # one YAML map per kernel (a list item at two spaces: "  - .agpr_count: ..."); its keys
+        # are sorted, so fields such as .group_segment_fixed_size come before .name
         fields = {}
         for line in notes.splitlines():
-            if re.match(r"\s+- \.args:", line):
+            if re.match(r"  - \.", line):
                 fields = {}
             m = re.match(r"\s+\.name:\s+(\S+)", line)
             if m:
