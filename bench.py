@@ -496,17 +496,19 @@ def main():
                             "ids force in-order work inside a host) with dependent memory round trips, "
                             "then a grid-wide barrier; HBM bytes are not what bounds it"}}
         # HBM bytes per launch measured by PMC (tools/pmc_traffic.sh: FETCH_SIZE x2 +
-        # WRITE_SIZE, separate passes) for this workload; per launch of the same number of
-        # rounds, so independent of --steps / --warmup
+        # WRITE_SIZE, separate passes) over the timed launches of THIS invocation: the entry
+        # keyed by workload, hosts, rounds per launch, GPUs, steps and warmup (null otherwise)
         tf = ROOT / "profiles" / "round_kernel_traffic.json"
         if tf.exists():
-            t = json.loads(tf.read_text())
-            wl = t.get("workload", {})
-            if (wl.get("name"), wl.get("hosts_per_gpu"), wl.get("graph_nodes"), wl.get("rounds_per_launch"),
-                    wl.get("n_gpus"), t.get("kernel")) == (args.workload, n_shard, args.nodes, round(rpl), world, rk):
-                roof["traffic"] = t["traffic_bytes_per_launch"]
-                roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
-                roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
+            want = {"name": args.workload, "hosts_per_gpu": n_shard, "graph_nodes": args.nodes,
+                    "rounds_per_launch": round(rpl), "n_gpus": world, "steps": args.steps, "warmup": args.warmup}
+            for t in json.loads(tf.read_text()).get("entries", []):
+                if t.get("workload") == want and t.get("kernel") == rk:
+                    roof["traffic"] = t["traffic_bytes_per_launch"]
+                    roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
+                    roof["traffic_provenance"] = t.get("bench_args")
+                    roof["traffic_uncorrected"] = t.get("traffic_bytes_per_launch_uncorrected")
+                    roof["traffic_GBps"] = round(t["traffic_bytes_per_launch"] / avg_s / 1e9, 2)
     info = ctx.engine_info()
     if roof is not None:
         # why the kernel sits far below the HBM roof: a latency chain on a partly filled chip.
