@@ -155,12 +155,26 @@ __device__ __forceinline__ EvRec ld_dev_rec(SGN_GLB const EvRec* p) {
   r.tag = (uint32_t)(pt >> 32);
   return r;
 }
+// A 16-byte write-through store (global_store_dwordx4 sc1: the agent-scope form of a store,
+// MI355X_MICROARCH.md's store table): a 32-byte record as two of them is two 32-B fabric
+// writes, where four 8-byte sc1 stores were four (tools/pmc_calib.sh: an 8-B sc1 store costs
+// a 32-B write). hipcc does not count an asm store in its waits: the round's arrival waits for
+// every store with its own s_waitcnt vmcnt(0); the s_nop keeps the data registers from being
+// overwritten under the store.
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_wt16(SGN_GLB void* p, uint64_t lo, uint64_t hi) {
+  u64x2 v;
+  v.x = lo;
+  v.y = hi;
+  // (no "memory" clobber: nothing in this wave reads the stored bytes before the round's
+  // arrival, whose own volatile asm s_waitcnt stays after this one; the clobber made hipcc
+  // keep a local aggregate in scratch)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"((uint64_t)p), "v"(v));
+}
 __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
-  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
-  st_dev(q, r.time);
-  st_dev(q + 1, r.eid);
-  st_dev(q + 2, (uint64_t)r.src | ((uint64_t)r.dst << 32));
-  st_dev(q + 3, (uint64_t)r.pc | ((uint64_t)r.tag << 32));
+  SGN_GLB char* q = (SGN_GLB char*)p;
+  st_wt16(q, r.time, r.eid);
+  st_wt16(q + 16, (uint64_t)r.src | ((uint64_t)r.dst << 32), (uint64_t)r.pc | ((uint64_t)r.tag << 32));
 }
 
 // CoDel pool entries: a page serves other hosts (other workgroups, other XCDs) after it is
@@ -179,11 +193,9 @@ __device__ __forceinline__ CodelEnt ld_dev_cq(SGN_GLB const CodelEnt* p) {
   return e;
 }
 __device__ __forceinline__ void st_dev_cq(SGN_GLB CodelEnt* p, const CodelEnt& e) {
-  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
-  st_dev(q, e.enqueue_ts);
-  st_dev(q + 1, e.eid);
-  st_dev(q + 2, (uint64_t)e.src | ((uint64_t)e.payload << 32));
-  st_dev(q + 3, (uint64_t)e.tag | ((uint64_t)e.count << 32));
+  SGN_GLB char* q = (SGN_GLB char*)p;
+  st_wt16(q, e.enqueue_ts, e.eid);
+  st_wt16(q + 16, (uint64_t)e.src | ((uint64_t)e.payload << 32), (uint64_t)e.tag | ((uint64_t)e.count << 32));
 }
 
 // device-scope atomic min whose result is not used: the wave does not wait for it here (a
