@@ -461,17 +461,21 @@ struct HostExec {
 
   // PERIODIC traffic: the app's next datagram goes to a peer that is a hash of the app counter
   // (sgn_periodic_dst), so its route can be in the route cache before the event loop needs it.
-  // prefetch_peer() issues the peer's load right after load(); prefetch_route() (after the
-  // gather's sort, so the load's latency hides behind it) fetches the route entry. A cache
-  // fill only: the entry is a pure function of (this host's node, the peer).
+  // store() leaves that peer in S.npeer; the next round's prefetch_peer(np) issues the peer's
+  // load beside the host record's (one round trip for both, not one after the other);
+  // prefetch_route() (after the gather's sort, so the load's latency hides behind it) fetches
+  // the route entry. A cache fill only: the entry is a pure function of (this host's node, the
+  // peer), so a hint that is not the next peer costs a miss, never a different result.
   uint32_t pf_peer;
   uint64_t pf_pi;
-  __device__ __forceinline__ void prefetch_peer() {
+  __device__ __forceinline__ void prefetch_peer(uint32_t np) {
+    pf_peer = np;
+    pf_pi = np != NO_HOST ? S.peer[np] : 0;
+  }
+  __device__ __forceinline__ uint32_t next_peer() const {
     uint32_t peer = NO_HOST, uip = 0;
-    if (!sgn_periodic_dst(S.flow_seed, gid, L->app_k, S.n_all, S.unknown_permille, &peer, &uip) || peer == L->rc_dst)
-      peer = NO_HOST;
-    pf_peer = peer;
-    pf_pi = peer != NO_HOST ? S.peer[peer] : 0;
+    if (!sgn_periodic_dst(S.flow_seed, gid, L->app_k, S.n_all, S.unknown_permille, &peer, &uip)) peer = NO_HOST;
+    return peer;
   }
   __device__ __forceinline__ void prefetch_route() {
     if (pf_peer == NO_HOST) return;
@@ -532,6 +536,7 @@ struct HostExec {
     r.cq_prev = L->cq[3];
     r.app_k = L->app_k;
     S.nextloc[h] = next_local_time();
+    if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
     if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
     if (tl_open) st_dev_cq(cq_tail_slot(), L->tl);
   }
@@ -1798,7 +1803,11 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   SGN_GLB EvRec* pk = S.pool + ik * S.CAP;
 
   uint64_t lmin = INVALID;
-  if (valid) lmin = S.nextloc[h];
+  uint32_t np = NO_HOST;  // PERIODIC: the next datagram's peer (store() of the host's last round)
+  if (valid) {
+    lmin = S.nextloc[h];
+    if (kApp == SGN_TRAFFIC_PERIODIC) np = S.npeer[h];
+  }
   Outbox* ob = X.ob;
   if (lane == 0) {
     ob->n = 0;
@@ -1896,7 +1905,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     const bool early = kApp == SGN_TRAFFIC_PERIODIC && bi == 0 && valid && lmin < we;
     if (early) {
       ex.load();
-      ex.prefetch_peer();
+      ex.prefetch_peer(np);
       loaded = true;
     }
     const uint32_t n = min(nraw, S.CAP);
@@ -3480,6 +3489,15 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
   if ((rc = up64(nextloc, &S.nextloc))) return rc;
+  S.npeer = nullptr;
+  if (tr->kind == SGN_TRAFFIC_PERIODIC) {  // every app counter starts at 0
+    std::vector<uint32_t> np(nH);
+    for (uint32_t h = 0; h < nH; h++) {
+      uint32_t peer = NO_HOST, uip = 0;
+      np[h] = sgn_periodic_dst(tr->flow_seed, ctx->host_of[h], 0, N, tr->unknown_dst_permille, &peer, &uip) ? peer : NO_HOST;
+    }
+    if ((rc = up32(np, &S.npeer))) return rc;
+  }
 
   // ---- calendar: bucket width >= any window length, horizon > max latency ----
   // The shortest possible window (Runahead::get, runahead.rs:44-57): a window spans at least

@@ -296,6 +296,10 @@ struct DevSim {
   // for all hosts at the start of a round: a dense array keeps that read coalesced)
   SGN_GLB HostRec* hrec;        // [nH]
   SGN_GLB uint64_t* nextloc;    // [nH]
+  // PERIODIC traffic: the peer (HostId, NO_HOST for an unknown address) of each host's next
+  // datagram, a hash of its app counter written when the host's record is stored, so the next
+  // round loads the peer's slot and node beside the host record instead of after it
+  SGN_GLB uint32_t* npeer;      // [nH] (null for other traffic kinds)
   // CoDel queues (Router's inbound CoDelQueue, unbounded in the reference) as chains of
   // pages from ONE pool sized by total occupancy, not per host: a host's queue is its runs
   // in order over a chain head page -> ... -> tail page (cq_next links them). Pages leave

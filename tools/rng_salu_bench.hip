@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 __device__ __forceinline__ uint64_t mk(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 template <int K>
@@ -78,11 +79,11 @@ __global__ void k(uint64_t* out, int n, int mode, int noise, uint64_t Tx, uint64
   if (threadIdx.x == 0) clk[0] = c1 - c0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   uint64_t *out, *clk;
   hipMalloc(&out, 64 * 8192 * 8);
   hipMalloc(&clk, 8);
-  const int n = 4096;
+  const int n = argc > 1 ? atoi(argv[1]) : 4096;  // draws per launch (88: one server's round)
   for (int mode = 0; mode < 2; mode++)
     for (int blocks : {1, 2048, 4096}) {
       for (int rep = 0; rep < 2; rep++) {
