@@ -2405,7 +2405,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     }
     // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
     // round edge known} on the 100 MHz clock
-    SGN_GLB uint64_t* rd = S.stamps ? S.rdbg + 3 * (size_t)(r & 127) : nullptr;
+    SGN_GLB uint64_t* rd = S.rdbg ? S.rdbg + 3 * (size_t)(r & 127) : nullptr;
     if (rd && threadIdx.x == 0)
       __hip_atomic_fetch_min(rd, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3542,9 +3542,11 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if ((rc = up32(bslab, &S.bucket_slab))) return rc;
   std::vector<uint64_t> bmin(NB, INVALID);
   if ((rc = up64(bmin, &S.bucket_min))) return rc;
-  if (getenv("SGN_STAMPS")) {
+  // SGN_STAMPS=1: per-group stamps; =2: also the persistent kernel's per-round timeline (one
+  // atomic min and max per workgroup and round on shared words: it slows the rounds it times)
+  if (const char* e = getenv("SGN_STAMPS")) {
     S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
-    S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 3 * 128);
+    if (atoi(e) >= 2) S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 3 * 128);
   }
   if (ctx->trace_cap) {
     S.trace = (decltype(S.trace))dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
@@ -3981,8 +3983,8 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
 
 // Diagnostics: per-wave {cycles, events, max lane events, busy lanes} of the last k_execute
 // (allocated when SGN_STAMPS=1 is set in the environment at sgn_sim_init).
-// Diagnostics of the last persistent launch: per round {earliest start, latest arrival,
-// round edge done} (100 MHz clock), 128 rounds; resets the buffer for the next launch.
+// Diagnostics of the last persistent launch (SGN_STAMPS=2): per round {earliest start, latest
+// arrival, round edge done} (100 MHz clock), 128 rounds; resets the buffer for the next launch.
 int sgn_debug_rounds(sgn_ctx* ctx, uint64_t* out) {
   if (!ctx || !ctx->sim_ready || !ctx->S.rdbg) return SGN_EINVAL;
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -3,7 +3,7 @@ span (earliest start -> latest arrival), round edge, and barrier wake-up to the 
 import os
 import sys
 
-os.environ["SGN_STAMPS"] = "1"
+os.environ["SGN_STAMPS"] = "2"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "shadow-gen_amd"))
