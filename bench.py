@@ -272,16 +272,20 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
     sample("faithful_all", True, cores, b / 4)
     sample("faithful_1", True, 1, b / 4)
     sample("optimised_1", False, 1, b / 4)
-    f = modes["faithful_all"]
+    # the headline is the stronger CPU baseline: the CPU-optimised restatement on every core of
+    # the box's share (the faithful mode keeps the reference's global packet-counter lock,
+    # which serialises it; it is reported in `modes`)
+    o, f = modes["optimised_all"], modes["faithful_all"]
     return {
-        "value": f["value"],
+        "value": o["value"],
         "unit": "packet events/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"reference-faithful C++ restatement (oracle/) of the round loop on {cores} worker threads, "
-                  f"{f['rounds']} rounds of the same {hosts.n}-host workload right after the GPU's timed rounds "
-                  f"({f['events']} packet events, {f['wall_s']} s); the CPU-optimised restatement over the GPU's "
-                  f"exact timed rounds reached {modes['optimised_all']['value'] / 1e6:.1f} M/s",
+        "sample": f"CPU-optimised C++ restatement (oracle/) of the round loop on {cores} worker threads over "
+                  f"exactly the GPU's {o['rounds']} timed rounds of the same {hosts.n}-host workload "
+                  f"({o['events']} packet events, {o['wall_s']} s); the reference-faithful restatement "
+                  f"(global packet-counter lock, hash-map lookups) reached {f['value'] / 1e6:.2f} M/s on "
+                  f"{f['rounds']} later rounds",
         "cpu_model": model, "cpus_visible": visible,
         "modes": {k: {kk: (round(vv, 1) if isinstance(vv, float) else vv) for kk, vv in m.items()}
                   for k, m in modes.items()},
