@@ -2442,7 +2442,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     uint32_t spins = 0;
     bool ok = true;
     while (ld_dev(&S.rb_cnt[(size_t)p * (RB_CH + 1) + RB_CH]) < nch) {
-      __builtin_amdgcn_s_sleep(1);
+      // (TGEN: 1563 workgroups poll one word; a longer sleep between polls leaves the memory
+      // side to the last arrivals' atomics: same-box A/B on C, 3639 -> 3586 us per 100-round
+      // launch; B, with 157 workgroups, was 0.3 % slower with it, D unchanged)
+      __builtin_amdgcn_s_sleep(kApp == SGN_TRAFFIC_TGEN ? 16 : 1);
       if (++spins > (1u << 22)) {
         ok = false;
         break;
