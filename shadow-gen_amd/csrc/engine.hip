@@ -2217,20 +2217,33 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
 // reset by workgroup 0 during round r (its last readers passed barrier r - 1). sim_init sizes
 // the calendar so no send of round r + 1 can reach a bucket consumed in round r.
 constexpr uint32_t RB_CH = 64;  // chunk slots per buffer (persistent grids up to 4096 workgroups)
+// Strides between chunks (u32 counters, u64 minimum pairs, u64 occupancy sums). TGEN rounds
+// (config C: 1563 workgroups in 25 chunks) give every chunk its own 128-B line for each, so
+// the ~4.7 k arrival atomics of a round do not queue on a few shared lines: same-box A/B on
+// C 3549 -> 3513 us per 100-round launch; the PERIODIC kernels keep them packed (D 0.2 %
+// slower padded, B unchanged). Buffers are allocated for the padded layout.
+template <uint32_t kApp> struct RbLayout {
+  static constexpr bool pad = kApp == SGN_TRAFFIC_TGEN;
+  static constexpr uint32_t CS = pad ? 32 : 1, MS = pad ? 16 : 2, OS = pad ? 16 : 1;
+  static constexpr uint32_t CB = (RB_CH + 1) * CS;  // u32 per buffer of counters (chunks, then the top)
+};
+constexpr uint32_t RB_CS_MAX = 32, RB_MS_MAX = 16, RB_OS_MAX = 16, RB_CB_MAX = (RB_CH + 1) * RB_CS_MAX;
 
+template <uint32_t kApp>
 __device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
                                           uint64_t m, uint64_t occd) {
   if (threadIdx.x != 0) return;
   const uint32_t ch = w >> 6;
   const uint32_t csz = min(64u, nw - (ch << 6));
-  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * 2;
+  using Y = RbLayout<kApp>;
+  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
   if (kmin != INVALID) min_nr(mn, kmin);
   if (m != INVALID) min_nr(mn + 1, m);
-  if (occd) cnt_add(&S.rb_occ[(size_t)p * RB_CH + ch], occd);
+  if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
-  SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * (RB_CH + 1);
-  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * Y::CB;
+  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The next window from buffer p after the barrier (every workgroup, identical results).
@@ -2240,16 +2253,18 @@ struct RbEdge {
                                          // allocated / freed, runs spilled (buffer p: stable)
   uint32_t active;
 };
+template <uint32_t kApp>
 __device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t nch, uint64_t ws, uint64_t we) {
+  using Y = RbLayout<kApp>;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
   uint64_t kk = INVALID, wn = INVALID, m = INVALID, km = INVALID, mu = INVALID;
   uint64_t od = 0, na = 0, nf = 0, ns = 0;
   if (lane < nch) {
-    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + lane) * 2;
+    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + lane) * Y::MS;
     kk = ld_dev(mn);
     wn = ld_dev(mn + 1);
-    od = ld_dev(&S.rb_occ[(size_t)p * RB_CH + lane]);
+    od = ld_dev(&S.rb_occ[((size_t)p * RB_CH + lane) * Y::OS]);
   }
   if (S.tkind != SGN_TRAFFIC_EXTERNAL) {
     // synthetic traffic: every pending event is a delivery, so it lies in [we, we + max_lat)
@@ -2275,8 +2290,8 @@ __device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t 
   if (lane == 0) {
     km = ld_dev(&S.rb_keep[p]);
     mu = ld_dev(&S.ctrl->min_used);
-    na = ld_dev(&S.rb_occ[3 * RB_CH + p]);
-    ns = ld_dev(&S.rb_occ[3 * RB_CH + 3 + p]);
+    na = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + p]);
+    ns = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p]);
     nf = ld_dev(&S.rb_free[p]);
   }
   kk = wave_min_u64(kk);
@@ -2407,14 +2422,18 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
       // reset buffer (r + 1) % 3 for the next round
       const uint32_t q = (r + 1) % 3;
-      for (uint32_t i = threadIdx.x; i < RB_CH * 2; i += 64) st_dev(&S.rb_min[(size_t)q * RB_CH * 2 + i], (uint64_t)INVALID);
-      for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64) st_dev(&S.rb_cnt[(size_t)q * (RB_CH + 1) + i], 0u);
-      for (uint32_t i = threadIdx.x; i < RB_CH; i += 64) st_dev(&S.rb_occ[(size_t)q * RB_CH + i], (uint64_t)0);
+      for (uint32_t i = threadIdx.x; i < RB_CH; i += 64) {
+        st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS], (uint64_t)INVALID);
+        st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS + 1], (uint64_t)INVALID);
+        st_dev(&S.rb_occ[((size_t)q * RB_CH + i) * RbLayout<kApp>::OS], (uint64_t)0);
+      }
+      for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64)
+        st_dev(&S.rb_cnt[(size_t)q * RbLayout<kApp>::CB + i * RbLayout<kApp>::CS], 0u);
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
-        st_dev(&S.rb_occ[3 * RB_CH + q], (uint64_t)0);
-        st_dev(&S.rb_occ[3 * RB_CH + 3 + q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + q], (uint64_t)0);
       }
     }
     // diagnostics (SGN_STAMPS): per round of this launch, {earliest start, latest arrival,
@@ -2428,8 +2447,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       X.ob->bbase = ws;
       X.ob->pg_avail = rs.pg_avail;
       X.ob->pg_freed = &S.rb_free[p];
-      X.ob->pg_allocd = &S.rb_occ[3 * RB_CH + p];
-      X.ob->spilled = &S.rb_occ[3 * RB_CH + 3 + p];
+      X.ob->pg_allocd = &S.rb_occ[3 * RB_CH * RB_OS_MAX + p];
+      X.ob->spilled = &S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p];
     }
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
@@ -2445,17 +2464,17 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
             __hip_atomic_fetch_max(rd + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           flush_bmin<kApp>(S, X);
-          rb_arrive(S, p, w, P, kall, mall, oall);
+          rb_arrive<kApp>(S, p, w, P, kall, mall, oall);
           arrived = true;
         }
       });
       __syncthreads();
     }
-    if (!arrived) rb_arrive(S, p, w, P, INVALID, INVALID, 0);  // a workgroup without groups
+    if (!arrived) rb_arrive<kApp>(S, p, w, P, INVALID, INVALID, 0);  // a workgroup without groups
     // grid barrier: every chunk complete, bounded
     uint32_t spins = 0;
     bool ok = true;
-    while (ld_dev(&S.rb_cnt[(size_t)p * (RB_CH + 1) + RB_CH]) < nch) {
+    while (ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
       // (TGEN: 1563 workgroups poll one word; a longer sleep between polls leaves the memory
       // side to the last arrivals' atomics: same-box A/B on C, 3639 -> 3586 us per 100-round
       // launch; B, with 157 workgroups, was 0.3 % slower with it, D unchanged)
@@ -2470,7 +2489,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       return;
     }
     asm volatile("" ::: "memory");
-    const RbEdge e = rb_edge(S, p, nch, ws, we);
+    const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);
     if (rd && w == 0 && threadIdx.x == 0) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
     // This round's bucket bookkeeping (consumed minima -> INVALID, bucket b1 -> nb1) is done by
     // workgroup 0 during the next round, with plain stores: safe while the next round's sends
@@ -2485,7 +2504,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       if (w == 0) rb_bookkeep(S, ws, we, e.nb1, ks);  // (the previous round's: done at this round's start)
       if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // workgroup 0's stores are done
-        SGN_GLB uint32_t* gc = S.rb_cnt + 3 * (RB_CH + 1);
+        SGN_GLB uint32_t* gc = S.rb_cnt + 3 * RB_CB_MAX;
         const uint32_t target = (rs.ngap + 1) * P;
         __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t sp = 0;
@@ -3632,10 +3651,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
   size_round_kernels(ctx, S);
   // persistent-round buffers (three, by round % 3): chunk minima + keep minima, counters
-  S.rb_min = (decltype(S.rb_min))dalloc<uint64_t>(ctx, 3 * RB_CH * 2 + 4);
-  S.rb_keep = S.rb_min + 3 * RB_CH * 2;
-  S.rb_cnt = (decltype(S.rb_cnt))dalloc<uint32_t>(ctx, 3 * (RB_CH + 1) + 1);
-  S.rb_occ = (decltype(S.rb_occ))dalloc<uint64_t>(ctx, 3 * RB_CH + 6);
+  S.rb_min = (decltype(S.rb_min))dalloc<uint64_t>(ctx, 3 * RB_CH * RB_MS_MAX + 4);
+  S.rb_keep = S.rb_min + 3 * RB_CH * RB_MS_MAX;
+  S.rb_cnt = (decltype(S.rb_cnt))dalloc<uint32_t>(ctx, 3 * RB_CB_MAX + 1);
+  S.rb_occ = (decltype(S.rb_occ))dalloc<uint64_t>(ctx, 3 * RB_CH * RB_OS_MAX + 6);
   if (!S.rb_min || !S.rb_cnt || !S.rb_occ) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   S.fin_cnt = (decltype(S.fin_cnt))dalloc<uint32_t>(ctx, (G + 63) / 64 + 1);
   S.fin_occ = (decltype(S.fin_occ))dalloc<uint64_t>(ctx, (G + 63) / 64);
@@ -3714,10 +3733,10 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
       SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * 2 + 4) * 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, (3 * (RB_CH + 1) + 1) * 4, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * RB_MS_MAX + 4) * 8, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, (3 * RB_CB_MAX + 1) * 4, ctx->stream));
       SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_free, 0, 3 * 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_occ, 0, (3 * RB_CH + 6) * 8, ctx->stream));
+      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_occ, 0, (3 * RB_CH * RB_OS_MAX + 6) * 8, ctx->stream));
       time_begin(ctx, K_EXECUTE);
       launch_k_rounds(ctx, n);
       time_end(ctx);
