@@ -2377,6 +2377,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     if (verdict != 1) return;
   }
   const uint32_t nch = (P + 63) >> 6;
+  // the workgroup that does the shared bookkeeping (the previous round's bucket minima and
+  // slab table, the next round buffer's reset, the control block): the last one, whose group
+  // is a client group (slots start with the TGEN servers, whose groups are the slowest)
+  const uint32_t wbk = P - 1;
   // The round state every workgroup keeps for itself, in LDS (registers are the scarce
   // resource of the round kernel): the window, the spare slab, and the previous round's
   // bookkeeping that workgroup 0 does during the next round. The bucket -> slab table
@@ -2418,17 +2422,17 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     const uint64_t ws = uni64(rs.ws), we = uni64(rs.we);
     const uint32_t ks = (uint32_t)__builtin_amdgcn_readfirstlane((int)rs.ks);
     const uint32_t p = r % 3;
-    if (w == 0) {
+    if (w == wbk) {
       if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
       // reset buffer (r + 1) % 3 for the next round
       const uint32_t q = (r + 1) % 3;
-      for (uint32_t i = threadIdx.x; i < RB_CH; i += 64) {
+      for (uint32_t i = threadIdx.x; i < nch; i += 64) {
         st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS], (uint64_t)INVALID);
         st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS + 1], (uint64_t)INVALID);
         st_dev(&S.rb_occ[((size_t)q * RB_CH + i) * RbLayout<kApp>::OS], (uint64_t)0);
       }
-      for (uint32_t i = threadIdx.x; i <= RB_CH; i += 64)
-        st_dev(&S.rb_cnt[(size_t)q * RbLayout<kApp>::CB + i * RbLayout<kApp>::CS], 0u);
+      for (uint32_t i = threadIdx.x; i <= nch; i += 64)  // the grid's chunks, then the top counter
+        st_dev(&S.rb_cnt[(size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS], 0u);
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
@@ -2490,7 +2494,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     }
     asm volatile("" ::: "memory");
     const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);
-    if (rd && w == 0 && threadIdx.x == 0) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
+    if (rd && w == wbk && threadIdx.x == 0) st_dev(rd + 2, (uint64_t)__builtin_amdgcn_s_memrealtime());
     // This round's bucket bookkeeping (consumed minima -> INVALID, bucket b1 -> nb1) is done by
     // workgroup 0 during the next round, with plain stores: safe while the next round's sends
     // cannot reach this round's buckets. They can after an idle gap: a send at t maps to this
@@ -2501,7 +2505,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     const uint64_t bstart = SIM_START + S.bw_div.div(ws - SIM_START) * S.BW;
     const bool gap = e.active && (e.we + S.max_lat >= bstart + span || e.we + S.max_lat < e.we);
     if (gap) {
-      if (w == 0) rb_bookkeep(S, ws, we, e.nb1, ks);  // (the previous round's: done at this round's start)
+      if (w == wbk) rb_bookkeep(S, ws, we, e.nb1, ks);  // (the previous round's: done at this round's start)
       if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // workgroup 0's stores are done
         SGN_GLB uint32_t* gc = S.rb_cnt + 3 * RB_CB_MAX;
@@ -2537,7 +2541,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
         rs.hold = (pages_free(rs.pg_avail, rs.pg_alloc) < need ? HOLD_CODEL : 0u) | (rs.nspill ? HOLD_SPILL : 0u);
         rs.hold_need = need;
       }
-      if (w == 0) {
+      if (w == wbk) {
         st_dev(&C->last_min_next, e.min_next);
         st_dev(&C->prev_we, we);
       }
@@ -2545,7 +2549,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     __syncthreads();
   }
   // the last round's bookkeeping and the host-visible control block
-  if (w == 0) {
+  if (w == wbk) {
     if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
     if (threadIdx.x == 0) {
       st_dev(&C->keep_slab, rs.ks);
