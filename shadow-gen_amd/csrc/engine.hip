@@ -324,13 +324,24 @@ __device__ __forceinline__ void spill_run(const DevSim& S, Outbox* ob, uint32_t 
 #pragma clang diagnostic ignored "-Walign-mismatch"
 typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
 typedef FifoEnt FifoEnt8 __attribute__((aligned(8)));
-struct LaneLDS {
-  sgn_drun run[3];   // tx, rx, app (sgn_workload.h)
+// CoDel drop state (interval end, drop next, current / previous count): in the lane's LDS
+// slot for TGEN and CPU-application traffic; PERIODIC kernels (configs B and D) keep it in the
+// host record only (HostRec::cq_*, touched only when the queue stands), which takes their
+// per-workgroup LDS from 26.1 to 23.1 KB at config D: 7 resident workgroups per CU, not 6.
+struct LaneCq {
+  uint64_t cq[4];
+};
+struct LaneNoCq {};
+// a pending digest run (sgn_drun of sgn_workload.h) with its count kept apart (LaneLDS::rn):
+// sgn_drun's 4-byte count pads it to 32 bytes, three of them 12 bytes of every lane's slot
+struct DRunL {
+  uint64_t a, b, c;
+};
+template <uint32_t kApp>
+struct LaneLDS : std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoCq, LaneCq> {
+  DRunL run[3];      // tx, rx, app pending runs (sgn_workload.h) ...
   uint64_t dig[3];   // tx, rx, app digests
   CodelEnt8 hd, tl;  // head run being consumed / tail run being extended
-  uint64_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU)
-  uint64_t cq[4];    // CoDel drop state: interval end, drop next, current / previous count
-  uint64_t app_k;    // synthetic app counter
   FifoEnt8 fh;       // copy of the send queue's head entry ...
   uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
   uint64_t rc_T;
@@ -338,6 +349,10 @@ struct LaneLDS {
   uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
   uint32_t rc_sid;   // ... whose slot id is this
   uint32_t cq_tp;    // CoDel chain's tail page
+  uint32_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU; sim_init
+                     // refuses a bandwidth whose increment does not fit 32 bits)
+  uint32_t app_k;    // synthetic app counter (the record keeps 64 bits; a wrap is reported)
+  uint32_t rn[3];    // ... and their counts
 };
 
 // kTrace: the per-packet trace can be on (k_execute). The persistent k_rounds is built
@@ -372,7 +387,7 @@ struct HostExec {
   bool hd_valid, tl_open;
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
-  LaneLDS* L;
+  LaneLDS<kApp>* L;
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint16_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
   Outbox* ob;             // the wave's outbox (LDS)
@@ -382,7 +397,7 @@ struct HostExec {
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS* l, const uint16_t* bs, Outbox* o)
+                      LaneLDS<kApp>* l, const uint16_t* bs, Outbox* o)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
@@ -431,11 +446,13 @@ struct HostExec {
     L->rc_T = r.rc_T;
     L->tbc[0] = r.tb_inc[0];
     L->tbc[1] = r.tb_inc[1];
-    L->cq[0] = r.cq_ie;
-    L->cq[1] = r.cq_dn;
-    L->cq[2] = r.cq_cur;
-    L->cq[3] = r.cq_prev;
-    L->app_k = r.app_k;
+    if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
+      L->cq[0] = r.cq_ie;
+      L->cq[1] = r.cq_dn;
+      L->cq[2] = r.cq_cur;
+      L->cq[3] = r.cq_prev;
+    }
+    L->app_k = (uint32_t)r.app_k;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
@@ -452,7 +469,7 @@ struct HostExec {
       L->fh = *fq_slot(0);
       L->fh_idx = fq_head;
     }
-    L->run[0].n = L->run[1].n = L->run[2].n = 0;
+    L->rn[0] = L->rn[1] = L->rn[2] = 0;
 #ifdef SGN_DIAG
     for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
     for (int i = 0; i < 5; i++) wk[i] = 0;
@@ -530,10 +547,12 @@ struct HostExec {
     r.n_sent += c_sent;
     r.n_popped += c_popped;
     r.n_delivered += c_deliv;
-    r.cq_ie = L->cq[0];
-    r.cq_dn = L->cq[1];
-    r.cq_cur = L->cq[2];
-    r.cq_prev = L->cq[3];
+    if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
+      r.cq_ie = L->cq[0];
+      r.cq_dn = L->cq[1];
+      r.cq_cur = L->cq[2];
+      r.cq_prev = L->cq[3];
+    }
     r.app_k = L->app_k;
     S.nextloc[h] = next_local_time();
     if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
@@ -695,6 +714,75 @@ struct HostExec {
     return true;
   }
 
+  // sgn_drun_{flush,add}_{seq,same} (sgn_workload.h) over LaneLDS::run / rn
+  template <int K>
+  __device__ __forceinline__ void dr_flush_seq() {
+#ifndef SGN_EXP_NODIGEST
+    const uint32_t n = L->rn[K];
+    if (n) L->dig[K] = sgn_digest3(L->dig[K], L->run[K].a, L->run[K].b | ((uint64_t)n << 32), L->run[K].c - n);
+    L->rn[K] = 0;
+#endif
+  }
+  template <int K>
+  __device__ __forceinline__ void dr_flush_same() {
+#ifndef SGN_EXP_NODIGEST
+    const uint32_t n = L->rn[K];
+    if (n) L->dig[K] = sgn_digest3(L->dig[K], L->run[K].a, L->run[K].b | ((uint64_t)n << 34), L->run[K].c);
+    L->rn[K] = 0;
+#endif
+  }
+  template <int K>
+  __device__ __forceinline__ void dr_add_seq(uint64_t a, uint64_t b, uint64_t c0, uint32_t n) {
+#ifndef SGN_EXP_NODIGEST
+    DRunL& r = L->run[K];
+    if (L->rn[K] && r.a == a && r.b == b && r.c == c0) {
+      L->rn[K] += n;
+      r.c += n;
+      return;
+    }
+    dr_flush_seq<K>();
+    r.a = a;
+    r.b = b;
+    r.c = c0 + n;
+    L->rn[K] = n;
+#endif
+  }
+  template <int K>
+  __device__ __forceinline__ void dr_add_same(uint64_t a, uint64_t b, uint64_t c, uint32_t n) {
+#ifndef SGN_EXP_NODIGEST
+    DRunL& r = L->run[K];
+    if (L->rn[K] && r.a == a && r.b == b && r.c == c) {
+      L->rn[K] += n;
+      return;
+    }
+    dr_flush_same<K>();
+    r.a = a;
+    r.b = b;
+    r.c = c;
+    L->rn[K] = n;
+#endif
+  }
+
+  // the CoDel drop state (LaneCq / HostRec::cq_*, see LaneLDS)
+  template <int I>
+  __device__ __forceinline__ uint64_t cqg() const {
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC)
+      return I == 0 ? R->cq_ie : I == 1 ? R->cq_dn : I == 2 ? R->cq_cur : R->cq_prev;
+    else
+      return L->cq[I];
+  }
+  template <int I>
+  __device__ __forceinline__ void cqs(uint64_t v) {
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+      if (I == 0) R->cq_ie = v;
+      if (I == 1) R->cq_dn = v;
+      if (I == 2) R->cq_cur = v;
+      if (I == 3) R->cq_prev = v;
+    } else {
+      L->cq[I] = v;
+    }
+  }
+
   // ---- CoDel (router/codel_queue.rs) on a chain of pool pages ----
   // The queue's runs in order fill the head page from cq_head's offset, whole pages, and the
   // tail page (L->cq_tp) up to run cq_nr - 1; only the head and tail runs are ever touched.
@@ -777,9 +865,9 @@ struct HostExec {
       fl &= ~F_CODEL_IE;
       return false;
     }
-    if (fl & F_CODEL_IE) return now >= L->cq[0];
+    if (fl & F_CODEL_IE) return now >= cqg<0>();
     fl |= F_CODEL_IE;
-    L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
+    cqs<0>(emu_sat_add(now, CODEL_INTERVAL));
     return false;
   }
   // the head run into registers (queue not empty)
@@ -823,12 +911,12 @@ struct HostExec {
   __device__ __forceinline__ void codel_drop(const Pkt& p) {  // drop_packet (:319-321)
     cnt_add(&R->n_codel, 1);
     if (external()) drain_rec(SGN_DRAIN_CODEL, p.src, gid, p.eid, p.payload, p.tag);
-    sgn_drun_add_seq(&L->dig[2], &L->run[2], now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
+    dr_add_seq<2>(now, (uint64_t)p.src | (1ULL << 63), p.eid, 1);
     trace(SGN_TRACE_CODEL_DROP, p.src, 0, now, 0, p.eid);
   }
   __device__ __forceinline__ bool codel_was_dropping_recently() const {  // :273-281
     if (!(fl & F_CODEL_DN)) return false;
-    return sat_sub(now, L->cq[1]) < CODEL_INTERVAL * 16;
+    return sat_sub(now, cqg<1>()) < CODEL_INTERVAL * 16;
   }
   // CoDelQueue::pop (:125-201)
   __device__ __forceinline__ bool codel_pop(Pkt* out) {
@@ -850,24 +938,25 @@ struct HostExec {
       bool nok;
       bool has_n = codel_pop_raw(&n, &nok);
       fl |= F_CODEL_DROP;
-      uint64_t delta = sat_sub(L->cq[2], L->cq[3]);
-      L->cq[2] = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      uint64_t delta = sat_sub(cqg<2>(), cqg<3>());
+      const uint64_t cur = (codel_was_dropping_recently() && delta > 1) ? delta : 1;
+      cqs<2>(cur);
       fl |= F_CODEL_DN;
-      L->cq[1] = codel_law(now, L->cq[2]);
-      L->cq[3] = L->cq[2];
+      cqs<1>(codel_law(now, cur));
+      cqs<3>(cur);
       if (has_n) *out = n;
       return has_n;
     }
     // drop_from_drop_mode (:172-201)
     bool has_item = true;
     Pkt item = p;
-    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= L->cq[1]) {
+    while (has_item && (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now >= cqg<1>()) {
       codel_drop(item);
-      L->cq[2]++;
+      cqs<2>(cqg<2>() + 1);
       bool iok = false;
       has_item = codel_pop_raw(&item, &iok);
       if (has_item && iok)
-        L->cq[1] = codel_law(L->cq[1], L->cq[2]);
+        cqs<1>(codel_law(cqg<1>(), cqg<2>()));
       else
         fl &= ~F_CODEL_DROP;
     }
@@ -937,7 +1026,7 @@ struct HostExec {
                               uint32_t tag) {
     c_deliv += m;
     c_bytes += (uint64_t)m * payload;
-    sgn_drun_add_seq(&L->dig[2], &L->run[2], now, src, e0, m);
+    dr_add_seq<2>(now, src, e0, m);
     if (tr())
       for (uint32_t k = 0; k < m; k++)
         trace(SGN_TRACE_DELIVER, src, 0, now, (uint64_t)payload | ((uint64_t)tag << 32), e0 + k);
@@ -961,7 +1050,7 @@ struct HostExec {
     cnt_add(&R->n_local_deliv, 1);
     if (tr()) trace(SGN_TRACE_LOCAL, gid, 0, now, (uint64_t)p.payload | ((uint64_t)p.tag << 32), 0);
     if (external()) drain_rec(SGN_DRAIN_LOCAL, gid, gid, 0, p.payload, p.tag);
-    sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
+    dr_flush_seq<2>();
     L->dig[2] = sgn_digest3(L->dig[2], now, (uint64_t)p.src | (1ULL << 62) | (1ULL << 32), p.payload);
   }
 
@@ -995,8 +1084,8 @@ struct HostExec {
           // (drop_from_drop_mode's loop does not run, :172-201) and changes nothing until a
           // pop leaves <= MTU queued (then interval_end and drop mode end).
           const bool standing = sat_sub(now, L->hd.enqueue_ts) >= CODEL_TARGET;
-          const bool ie_due = (fl & F_CODEL_IE) && now >= L->cq[0];
-          const bool drop_quiet = (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now < L->cq[1];
+          const bool ie_due = (fl & F_CODEL_IE) && now >= cqg<0>();
+          const bool drop_quiet = (fl & F_CODEL_DROP) && (fl & F_CODEL_DN) && now < cqg<1>();
           if (!standing || !ie_due || drop_quiet) {
             const uint32_t n = L->hd.count;
             const uint64_t wire = (uint64_t)L->hd.payload + sgn_header_bytes(L->hd.tag);
@@ -1030,7 +1119,7 @@ struct HostExec {
               fl &= ~F_CODEL_DROP;
               if (!(fl & F_CODEL_IE)) {
                 fl |= F_CODEL_IE;
-                L->cq[0] = emu_sat_add(now, CODEL_INTERVAL);
+                cqs<0>(emu_sat_add(now, CODEL_INTERVAL));
               }
             }  // else drop mode before drop_next: unchanged
             if (L->hd.count == 0) {
@@ -1091,9 +1180,9 @@ struct HostExec {
                                             uint64_t deliver) {
     if (lost) {
       c_loss++;
-      if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
+      if (run) dr_add_same<0>(now, (uint64_t)dst, deliver, run);
       run = 0;
-      sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
+      dr_add_same<0>(now, (uint64_t)dst | (1ULL << 32), 0, 1);
     } else {
       run++;
       sent++;
@@ -1111,7 +1200,7 @@ struct HostExec {
     const bool boot = now < S.boot_end;
     if (dst == NO_HOST) {  // resolve_ip_to_host_id failed: InetDropped (worker.rs:347-357)
       cnt_add(&R->n_unknown, n);
-      sgn_drun_add_same(&L->dig[0], &L->run[0], now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
+      dr_add_same<0>(now, 0xFFFFFFFFULL | (2ULL << 32), 0, n);
       if (tr())
         for (uint32_t j = 0; j < n; j++) {
           if (pop) trace_pop(NO_HOST, payload, tag);
@@ -1168,9 +1257,9 @@ struct HostExec {
         if (tr()) R->rng_pos++;
         if (can_drop && x >= T) {
           c_loss++;
-          if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
+          if (run) dr_add_same<0>(now, (uint64_t)dst, deliver, run);
           run = 0;
-          sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst | (1ULL << 32), 0, 1);
+          dr_add_same<0>(now, (uint64_t)dst | (1ULL << 32), 0, 1);
           if (tr()) trace(SGN_TRACE_SEND, dst, 1, now, 0, 0);
           if (external()) drain_rec(SGN_DRAIN_LOSS, gid, dst, 0, payload, tag);
         } else {
@@ -1226,7 +1315,7 @@ struct HostExec {
       eid += sent;
     }
     DGT_END(DGT_APP, tr0);
-    if (run) sgn_drun_add_same(&L->dig[0], &L->run[0], now, (uint64_t)dst, deliver, run);
+    if (run) dr_add_same<0>(now, (uint64_t)dst, deliver, run);
     const uint32_t nsent = (uint32_t)(eid - eid0);
     if (nsent == 0) return;
     c_sent += nsent;
@@ -1429,6 +1518,7 @@ struct HostExec {
 
   __device__ __forceinline__ void app_task() {
     const uint64_t k = L->app_k++;
+    if (L->app_k == 0) overflow(OVF_APPK);  // 2^32 app events on one host: the LDS copy wrapped
     uint32_t dst, payload, tag, uip = 0;
     uint64_t next_delay;
     if (kApp == SGN_TRAFFIC_PERIODIC) {
@@ -1544,7 +1634,7 @@ struct HostExec {
           const uint32_t src = e.src;
           const uint64_t eid0 = e.eid;
           c_popped += n;
-          sgn_drun_add_seq(&L->dig[1], &L->run[1], now, src, eid0, n);
+          dr_add_seq<1>(now, src, eid0, n);
           if (tr())
             for (uint32_t k = 0; k < n; k++) trace(SGN_TRACE_POP, src, 0, now, 0, eid0 + k);
           // Router::route_incoming_packet (router/mod.rs:55-57)
@@ -1585,9 +1675,9 @@ struct HostExec {
       forward_out_step();
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
-    sgn_drun_flush_same(&L->dig[0], &L->run[0]);
-    sgn_drun_flush_seq(&L->dig[1], &L->run[1]);
-    sgn_drun_flush_seq(&L->dig[2], &L->run[2]);
+    dr_flush_same<0>();
+    dr_flush_seq<1>();
+    dr_flush_seq<2>();
   }
 };
 
@@ -1756,7 +1846,7 @@ struct ExecLDS {
   uint16_t* lc;       // ... ordered inside each destination segment
   uint32_t* lcnt;
   uint32_t* lcur;     // placement cursors (after placement: segment ends, start = end - count)
-  LaneLDS* lslot;     // the lanes' LDS slots
+  void* lslot;        // the lanes' LDS slots (LaneLDS<kApp>[64])
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   Outbox* ob;         // the wave's outbox
   uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
@@ -1784,7 +1874,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint16_t* lc = X.lc;
   uint32_t* lcnt = X.lcnt;
   uint32_t* lcur = X.lcur;
-  LaneLDS* lslot = X.lslot;
+  LaneLDS<kApp>* lslot = (LaneLDS<kApp>*)X.lslot;
   uint16_t* lbs = X.lbs;
   const uint32_t lane = threadIdx.x;
   const uint32_t gsz = 1u << S.gsh;
@@ -2095,7 +2185,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 #define SGN_EXEC_LDS(X)                                                              \
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];                     \
   __shared__ uint32_t lcnt_[64], lcur_[64];                                         \
-  __shared__ LaneLDS lslot_[64];                                                     \
+  __shared__ LaneLDS<kApp> lslot_[64];                                               \
   __shared__ uint16_t lbs_[LDS_BSLAB];                                               \
   __shared__ Outbox ob_;                                                             \
   ExecLDS X;                                                                         \
@@ -2999,6 +3089,7 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow & OVF_TRACE) what += " trace buffer";
   if (c.overflow & OVF_TIMEOUT) what += " persistent grid barrier timed out (grid not resident)";
   if (c.overflow & OVF_HORIZON) what += " event calendar horizon (a delivery beyond the calendar's buckets)";
+  if (c.overflow & OVF_APPK) what += " synthetic app counter (2^32 app events on one host)";
   if (c.overflow & OVF_DRAIN) what += " drain buffer (raise sgn_drain_enable's capacity or drain more often)";
   return set_error(ctx, SGN_EOVERFLOW,
                    "device capacity exceeded:" + what + " (info " +
@@ -3454,6 +3545,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     for (int w = 0; w < 2; w++) {
       const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
       const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
+      if (inc > 0xFFFFFFFFull)  // (the round kernels keep the increment as 32 bits: > 34 Pbit/s)
+        return set_error(ctx, SGN_EINVAL, "host bandwidth above 34 Pbit/s (token-bucket increment > 2^32 bytes)");
       r.tb_inc[w] = inc;
       r.tb_cap[w] = inc + SGN_CONFIG_MTU;
       r.tb_bal[w] = inc + SGN_CONFIG_MTU;
