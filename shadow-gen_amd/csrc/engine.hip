@@ -324,34 +324,43 @@ __device__ __forceinline__ void spill_run(const DevSim& S, Outbox* ob, uint32_t 
 #pragma clang diagnostic ignored "-Walign-mismatch"
 typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
 typedef FifoEnt FifoEnt8 __attribute__((aligned(8)));
-// CoDel drop state (interval end, drop next, current / previous count): in the lane's LDS
-// slot for TGEN and CPU-application traffic; PERIODIC kernels (configs B and D) keep it in the
-// host record only (HostRec::cq_*, touched only when the queue stands), which takes their
-// per-workgroup LDS from 26.1 to 23.1 KB at config D: 7 resident workgroups per CU, not 6.
+// Per-lane state in the lane's LDS slot or, for the PERIODIC kernels (configs B and D, whose
+// occupancy LDS limits: config D's 15,625 groups on the resident grid), elsewhere:
+// * CoDel drop state (interval end, drop next, current / previous count): the PERIODIC
+//   kernels keep it in the host record only (HostRec::cq_*, touched only when the queue
+//   stands);
+// * route cache, token-bucket increments, app counter, send-queue head index: the PERIODIC
+//   kernels keep them in registers (they have ~40 VGPRs to spare below the 256 of two waves
+//   per SIMD; the TGEN kernel, whose occupancy is fine, keeps its registers).
+// Config D's per-workgroup LDS went 26.1 -> 23.1 -> 20.0 KB: 6 -> 7 -> 8 workgroups per CU.
 struct LaneCq {
   uint64_t cq[4];
 };
 struct LaneNoCq {};
+struct LaneRc {
+  uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
+  uint64_t rc_T;
+  uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
+  uint32_t rc_sid;   // ... whose slot id is this
+  uint32_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU; sim_init
+                     // refuses a bandwidth whose increment does not fit 32 bits)
+  uint32_t app_k;    // synthetic app counter (the record keeps 64 bits; a wrap is reported)
+  uint32_t fh_idx;   // the send queue head copy's ring index (NO_HOST: none)
+};
+struct LaneNoRc {};
 // a pending digest run (sgn_drun of sgn_workload.h) with its count kept apart (LaneLDS::rn):
 // sgn_drun's 4-byte count pads it to 32 bytes, three of them 12 bytes of every lane's slot
 struct DRunL {
   uint64_t a, b, c;
 };
 template <uint32_t kApp>
-struct LaneLDS : std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoCq, LaneCq> {
+struct LaneLDS : std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoCq, LaneCq>,
+                 std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoRc, LaneRc> {
   DRunL run[3];      // tx, rx, app pending runs (sgn_workload.h) ...
   uint64_t dig[3];   // tx, rx, app digests
   CodelEnt8 hd, tl;  // head run being consumed / tail run being extended
-  FifoEnt8 fh;       // copy of the send queue's head entry ...
-  uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
-  uint64_t rc_T;
-  uint32_t fh_idx;   // ... at this ring index (NO_HOST: none)
-  uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
-  uint32_t rc_sid;   // ... whose slot id is this
+  FifoEnt8 fh;       // copy of the send queue's head entry (ring index: LaneRc::fh_idx)
   uint32_t cq_tp;    // CoDel chain's tail page
-  uint32_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU; sim_init
-                     // refuses a bandwidth whose increment does not fit 32 bits)
-  uint32_t app_k;    // synthetic app counter (the record keeps 64 bits; a wrap is reported)
   uint32_t rn[3];    // ... and their counts
 };
 
@@ -388,6 +397,15 @@ struct HostExec {
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS<kApp>* L;
+  std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneRc, LaneNoRc> rr;  // (see LaneLDS)
+  __device__ __forceinline__ LaneRc& lr() {
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) return rr;
+    else return *L;
+  }
+  __device__ __forceinline__ const LaneRc& lr() const {
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) return rr;
+    else return *L;
+  }
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint16_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
   Outbox* ob;             // the wave's outbox (LDS)
@@ -440,19 +458,19 @@ struct HostExec {
     // with the rest of the record (no dependent round trip later in the round): route
     // cache, token-bucket constants, digests; then the CoDel queue's head run and the send
     // queue's head entry
-    L->rc_dst = r.rc_dst;
-    L->rc_sid = r.rc_sid;
-    L->rc_lat = r.rc_lat;
-    L->rc_T = r.rc_T;
-    L->tbc[0] = r.tb_inc[0];
-    L->tbc[1] = r.tb_inc[1];
+    lr().rc_dst = r.rc_dst;
+    lr().rc_sid = r.rc_sid;
+    lr().rc_lat = r.rc_lat;
+    lr().rc_T = r.rc_T;
+    lr().tbc[0] = r.tb_inc[0];
+    lr().tbc[1] = r.tb_inc[1];
     if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
       L->cq[0] = r.cq_ie;
       L->cq[1] = r.cq_dn;
       L->cq[2] = r.cq_cur;
       L->cq[3] = r.cq_prev;
     }
-    L->app_k = (uint32_t)r.app_k;
+    lr().app_k = (uint32_t)r.app_k;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
@@ -464,10 +482,10 @@ struct HostExec {
       L->hd = ld_dev_cq(cq_head_slot());
       hd_valid = true;
     }
-    L->fh_idx = NO_HOST;
+    lr().fh_idx = NO_HOST;
     if (fq_len > 0) {
       L->fh = *fq_slot(0);
-      L->fh_idx = fq_head;
+      lr().fh_idx = fq_head;
     }
     L->rn[0] = L->rn[1] = L->rn[2] = 0;
 #ifdef SGN_DIAG
@@ -491,16 +509,16 @@ struct HostExec {
   }
   __device__ __forceinline__ uint32_t next_peer() const {
     uint32_t peer = NO_HOST, uip = 0;
-    if (!sgn_periodic_dst(S.flow_seed, gid, L->app_k, S.n_all, S.unknown_permille, &peer, &uip)) peer = NO_HOST;
+    if (!sgn_periodic_dst(S.flow_seed, gid, lr().app_k, S.n_all, S.unknown_permille, &peer, &uip)) peer = NO_HOST;
     return peer;
   }
   __device__ __forceinline__ void prefetch_route() {
     if (pf_peer == NO_HOST) return;
     const RouteEnt re = S.route[(size_t)my_unode * S.U + (uint32_t)(pf_pi >> 32)];
-    L->rc_dst = pf_peer;
-    L->rc_sid = (uint32_t)pf_pi;
-    L->rc_lat = re.lat;
-    L->rc_T = re.T;
+    lr().rc_dst = pf_peer;
+    lr().rc_sid = (uint32_t)pf_pi;
+    lr().rc_lat = re.lat;
+    lr().rc_T = re.T;
   }
 
   __device__ __forceinline__ void store() {
@@ -522,8 +540,8 @@ struct HostExec {
     r.tb_last[0] = tbl0;
     r.tb_last[1] = tbl1;
     r.cq_bytes = cq_bytes;
-    r.rc_lat = L->rc_lat;
-    r.rc_T = L->rc_T;
+    r.rc_lat = lr().rc_lat;
+    r.rc_T = lr().rc_T;
     r.dig[0] = L->dig[0];
     r.dig[1] = L->dig[1];
     r.dig[2] = L->dig[2];
@@ -541,8 +559,8 @@ struct HostExec {
     r.cq_len = cq_len;
     r.fq_head = fq_head;
     r.fq_len = fq_len;
-    r.rc_dst = L->rc_dst;
-    r.rc_sid = L->rc_sid;
+    r.rc_dst = lr().rc_dst;
+    r.rc_sid = lr().rc_sid;
     r.max_codel = c_maxcodel;
     r.n_sent += c_sent;
     r.n_popped += c_popped;
@@ -553,7 +571,7 @@ struct HostExec {
       r.cq_cur = L->cq[2];
       r.cq_prev = L->cq[3];
     }
-    r.app_k = L->app_k;
+    r.app_k = lr().app_k;
     S.nextloc[h] = next_local_time();
     if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
     if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
@@ -674,7 +692,7 @@ struct HostExec {
     // when a refill is due or a removal fails, not on the per-packet fast path).
     uint64_t span = now - last;
     if (span >= interval) {
-      const uint64_t inc = L->tbc[W];
+      const uint64_t inc = lr().tbc[W];
       uint64_t nref = span / interval;
       uint64_t ntok = mul_sat(inc, nref, ~0ULL);
       uint64_t b = bal + ntok;
@@ -688,7 +706,7 @@ struct HostExec {
     uint64_t next_refill_span = interval - span;
     if (dec > bal) {
       // compute_conforming_duration (:91-117)
-      const uint64_t inc = L->tbc[W];
+      const uint64_t inc = lr().tbc[W];
       uint64_t req = dec - bal;
       uint64_t n;
       if (((req | inc) >> 32) == 0) {  // u32 division: the u64 routine is long
@@ -986,7 +1004,7 @@ struct HostExec {
       // here would hold up the wave's next dependent load (stores and loads share vmcnt);
       // store() writes it back if it is still queued
       L->fh = e;
-      L->fh_idx = fq_head;
+      lr().fh_idx = fq_head;
       fl |= F_FH_DIRTY;
     } else {
       *fq_slot(fq_len) = e;
@@ -996,13 +1014,13 @@ struct HostExec {
   }
   // the head entry (from the LDS copy when it is current)
   __device__ __forceinline__ FifoEnt fifo_head() {
-    if (L->fh_idx == fq_head) return L->fh;
+    if (lr().fh_idx == fq_head) return L->fh;
     DGT_BEGIN(tf);
     const FifoEnt e = *fq_slot(0);
     DGT_WAIT();
     DGT_END(DGT_FHLD, tf);
     L->fh = e;
-    L->fh_idx = fq_head;
+    lr().fh_idx = fq_head;
     return e;
   }
 
@@ -1214,10 +1232,10 @@ struct HostExec {
     // one peer for many rounds, so the host keeps its last (peer, latency, threshold)
     uint64_t delay, T;
     uint32_t dsid;  // the destination's slot id (where its events are filed)
-    if (L->rc_dst == dst) {
-      delay = L->rc_lat;
-      T = L->rc_T;
-      dsid = L->rc_sid;
+    if (lr().rc_dst == dst) {
+      delay = lr().rc_lat;
+      T = lr().rc_T;
+      dsid = lr().rc_sid;
     } else {
       DG(DG_RMISS);
       DGT_BEGIN(trt);
@@ -1233,10 +1251,10 @@ struct HostExec {
       T = re.T;
       DGT_WAIT();
       DGT_END(DGT_RTLD, trt);
-      L->rc_dst = dst;
-      L->rc_sid = dsid;
-      L->rc_lat = delay;
-      L->rc_T = T;
+      lr().rc_dst = dst;
+      lr().rc_sid = dsid;
+      lr().rc_lat = delay;
+      lr().rc_T = T;
     }
     uint64_t deliver = now + delay;
     if (deliver < we) deliver = we;
@@ -1484,7 +1502,7 @@ struct HostExec {
         m.count = e.count - consumed;
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         *fq_slot(fq_len - 1) = m;
-        L->fh_idx = NO_HOST;  // the cached head is stale
+        lr().fh_idx = NO_HOST;  // the cached head is stale
         fl &= ~F_FH_DIRTY;
       } else {
         if (!(fl & F_FH_DIRTY)) fq_slot(0)->count = e.count - consumed;
@@ -1517,8 +1535,8 @@ struct HostExec {
   }
 
   __device__ __forceinline__ void app_task() {
-    const uint64_t k = L->app_k++;
-    if (L->app_k == 0) overflow(OVF_APPK);  // 2^32 app events on one host: the LDS copy wrapped
+    const uint64_t k = lr().app_k++;
+    if (lr().app_k == 0) overflow(OVF_APPK);  // 2^32 app events on one host: the LDS copy wrapped
     uint32_t dst, payload, tag, uip = 0;
     uint64_t next_delay;
     if (kApp == SGN_TRAFFIC_PERIODIC) {
