@@ -348,6 +348,8 @@ struct LaneRc {
   uint32_t fh_idx;   // the send queue head copy's ring index (NO_HOST: none)
 };
 struct LaneNoRc {};
+template <uint32_t kApp>
+constexpr bool kRcReg = kApp == SGN_TRAFFIC_PERIODIC;  // (TGEN with them in registers: C unchanged)
 // a pending digest run (sgn_drun of sgn_workload.h) with its count kept apart (LaneLDS::rn):
 // sgn_drun's 4-byte count pads it to 32 bytes, three of them 12 bytes of every lane's slot
 struct DRunL {
@@ -355,7 +357,7 @@ struct DRunL {
 };
 template <uint32_t kApp>
 struct LaneLDS : std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoCq, LaneCq>,
-                 std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoRc, LaneRc> {
+                 std::conditional_t<kRcReg<kApp>, LaneNoRc, LaneRc> {
   DRunL run[3];      // tx, rx, app pending runs (sgn_workload.h) ...
   uint64_t dig[3];   // tx, rx, app digests
   CodelEnt8 hd, tl;  // head run being consumed / tail run being extended
@@ -397,13 +399,13 @@ struct HostExec {
   // state touched O(1) times per run lives in this lane's LDS slot (registers are the
   // scarce resource: they set how many waves are resident)
   LaneLDS<kApp>* L;
-  std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneRc, LaneNoRc> rr;  // (see LaneLDS)
+  std::conditional_t<kRcReg<kApp>, LaneRc, LaneNoRc> rr;  // (see LaneLDS)
   __device__ __forceinline__ LaneRc& lr() {
-    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) return rr;
+    if constexpr (kRcReg<kApp>) return rr;
     else return *L;
   }
   __device__ __forceinline__ const LaneRc& lr() const {
-    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) return rr;
+    if constexpr (kRcReg<kApp>) return rr;
     else return *L;
   }
   SGN_GLB HostRec* R;     // this host's record (set by load())
