@@ -73,6 +73,11 @@ def build_workload_b(n_hosts, V, seed=1):
                           start_jitter_ns=10_000_000, payload_len=1024, unknown_dst_permille=1)
     cfg = sgn.make_config(10_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64, codel_cap=64,
                           event_capacity=1 << 22)
+    # 16 hosts per execute wave: B's 10k hosts are 157 waves at 64, one per CU on 157 of the
+    # 256 CUs; 625 waves of 16 spread the (per-lane serial) host work (same-box A/B: 2827 ->
+    # 2770 us per 100-round launch; 8 and 4 hosts per wave were slower). A performance knob:
+    # results do not depend on it (tests/test_gpu_fuzz.py mixes it).
+    cfg.hosts_per_wave = 16
     return g, used, hosts, cfg, tr
 
 
