@@ -2330,10 +2330,11 @@ constexpr uint32_t RB_CH = 64;  // chunk slots per buffer (persistent grids up t
 // Strides between chunks (u32 counters, u64 minimum pairs, u64 occupancy sums). TGEN rounds
 // (config C: 1563 workgroups in 25 chunks) give every chunk its own 128-B line for each, so
 // the ~4.7 k arrival atomics of a round do not queue on a few shared lines: same-box A/B on
-// C 3549 -> 3513 us per 100-round launch; the PERIODIC kernels keep them packed (D 0.2 %
-// slower padded, B unchanged). Buffers are allocated for the padded layout.
+// C 3549 -> 3513 us per 100-round launch; with config B at 16 hosts per wave (625 workgroups)
+// and D at 8 workgroups per CU (2048), padding plus a poll sleep of 8 is -0.6 % on B and
+// -0.3 % on D. Buffers are allocated for the padded layout.
 template <uint32_t kApp> struct RbLayout {
-  static constexpr bool pad = kApp == SGN_TRAFFIC_TGEN;
+  static constexpr bool pad = kApp != SGN_TRAFFIC_EXTERNAL;
   static constexpr uint32_t CS = pad ? 32 : 1, MS = pad ? 16 : 2, OS = pad ? 16 : 1;
   static constexpr uint32_t CB = (RB_CH + 1) * CS;  // u32 per buffer of counters (chunks, then the top)
 };
@@ -2591,8 +2592,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     while (ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
       // (TGEN: 1563 workgroups poll one word; a longer sleep between polls leaves the memory
       // side to the last arrivals' atomics: same-box A/B on C, 3639 -> 3586 us per 100-round
-      // launch; B, with 157 workgroups, was 0.3 % slower with it, D unchanged)
-      __builtin_amdgcn_s_sleep(kApp == SGN_TRAFFIC_TGEN ? 16 : 1);
+      // launch; PERIODIC: 8, see RbLayout)
+      __builtin_amdgcn_s_sleep(kApp == SGN_TRAFFIC_TGEN ? 16 : kApp == SGN_TRAFFIC_PERIODIC ? 8 : 1);
       if (++spins > (1u << 22)) {
         ok = false;
         break;
