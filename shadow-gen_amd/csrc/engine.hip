@@ -350,6 +350,11 @@ struct LaneRc {
 struct LaneNoRc {};
 template <uint32_t kApp>
 constexpr bool kRcReg = kApp == SGN_TRAFFIC_PERIODIC;  // (TGEN with them in registers: C unchanged)
+// the kernels whose sends fold their bucket minima in an LDS table (S.agg_bmin, flush_bmin):
+// PERIODIC (configs B and D: ~1 M sends a round on a few bucket words at D). TGEN has the LDS
+// since round 3's slimmer lane slots, but measured 2 % slower with the table on C.
+template <uint32_t kApp>
+constexpr bool kAggBmin = kApp == SGN_TRAFFIC_PERIODIC;
 // a pending digest run (sgn_drun of sgn_workload.h) with its count kept apart (LaneLDS::rn):
 // sgn_drun's 4-byte count pads it to 32 bytes, three of them 12 bytes of every lane's slot
 struct DRunL {
@@ -1363,7 +1368,7 @@ struct HostExec {
       // (flush_bmin publishes it before the round's arrival), else one device atomic per run
       // (compiled for PERIODIC traffic only — configs B and D, where every host sends every
       // round; the TGEN kernel of config C keeps its per-run atomic, uncontended there)
-      if (kApp == SGN_TRAFFIC_PERIODIC && S.agg_bmin)
+      if (kAggBmin<kApp> && S.agg_bmin)
         atomicMin(&ob->bmin[b == b1 ? S.NB : b], (uint32_t)(deliver - ob->bbase));
       else
         min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
@@ -2230,12 +2235,12 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 // fits 32 bits).
 template <uint32_t kApp>
 __device__ __forceinline__ void init_bmin(const DevSim& S, const ExecLDS& X) {
-  if (kApp == SGN_TRAFFIC_PERIODIC && X.bmin)
+  if (kAggBmin<kApp> && X.bmin)
     for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) X.bmin[i] = 0xFFFFFFFFu;
 }
 template <uint32_t kApp>
 __device__ __forceinline__ void flush_bmin(const DevSim& S, const ExecLDS& X) {
-  if (kApp != SGN_TRAFFIC_PERIODIC || !X.bmin) return;
+  if (!kAggBmin<kApp> || !X.bmin) return;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i <= S.NB; i += blockDim.x) {
     const uint32_t v = X.bmin[i];
@@ -3075,7 +3080,7 @@ uint32_t max_slab_capacity(sgn_ctx* ctx, const DevSim& S) {
 // round, and so does a traced run (k_rounds is built without the per-packet trace).
 void size_round_kernels(sgn_ctx* ctx, DevSim& S) {
   const uint64_t G = S.G, NB = S.NB;
-  bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic
+  bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic (kAggBmin)
   for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind, S.trace_on)}) {
     const uint64_t r0 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP)), r1 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP, S.NB));
     if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
