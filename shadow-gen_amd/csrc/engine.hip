@@ -325,7 +325,8 @@ __device__ __forceinline__ void spill_run(const DevSim& S, Outbox* ob, uint32_t 
 typedef CodelEnt CodelEnt8 __attribute__((aligned(8)));
 typedef FifoEnt FifoEnt8 __attribute__((aligned(8)));
 // Per-lane state in the lane's LDS slot or, for the PERIODIC kernels (configs B and D, whose
-// occupancy LDS limits: config D's 15,625 groups on the resident grid), elsewhere:
+// occupancy LDS limits: config D's 15,625 groups on the resident grid), elsewhere (every
+// field keeps its full width: no limit beyond the reference's):
 // * CoDel drop state (interval end, drop next, current / previous count): the PERIODIC
 //   kernels keep it in the host record only (HostRec::cq_*, touched only when the queue
 //   stands);
@@ -340,11 +341,10 @@ struct LaneNoCq {};
 struct LaneRc {
   uint64_t rc_lat;   // route cache: latency and loss threshold (send_batch) ...
   uint64_t rc_T;
+  uint64_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU)
+  uint64_t app_k;    // synthetic app counter
   uint32_t rc_dst;   // ... to this peer (NO_HOST: none)
   uint32_t rc_sid;   // ... whose slot id is this
-  uint32_t tbc[2];   // token buckets' refill increments (capacity = increment + MTU; sim_init
-                     // refuses a bandwidth whose increment does not fit 32 bits)
-  uint32_t app_k;    // synthetic app counter (the record keeps 64 bits; a wrap is reported)
   uint32_t fh_idx;   // the send queue head copy's ring index (NO_HOST: none)
 };
 struct LaneNoRc {};
@@ -477,7 +477,7 @@ struct HostExec {
       L->cq[2] = r.cq_cur;
       L->cq[3] = r.cq_prev;
     }
-    lr().app_k = (uint32_t)r.app_k;
+    lr().app_k = r.app_k;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
@@ -1543,7 +1543,6 @@ struct HostExec {
 
   __device__ __forceinline__ void app_task() {
     const uint64_t k = lr().app_k++;
-    if (lr().app_k == 0) overflow(OVF_APPK);  // 2^32 app events on one host: the LDS copy wrapped
     uint32_t dst, payload, tag, uip = 0;
     uint64_t next_delay;
     if (kApp == SGN_TRAFFIC_PERIODIC) {
@@ -3115,7 +3114,6 @@ int check_overflow(sgn_ctx* ctx) {
   if (c.overflow & OVF_TRACE) what += " trace buffer";
   if (c.overflow & OVF_TIMEOUT) what += " persistent grid barrier timed out (grid not resident)";
   if (c.overflow & OVF_HORIZON) what += " event calendar horizon (a delivery beyond the calendar's buckets)";
-  if (c.overflow & OVF_APPK) what += " synthetic app counter (2^32 app events on one host)";
   if (c.overflow & OVF_DRAIN) what += " drain buffer (raise sgn_drain_enable's capacity or drain more often)";
   return set_error(ctx, SGN_EOVERFLOW,
                    "device capacity exceeded:" + what + " (info " +
@@ -3571,8 +3569,6 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     for (int w = 0; w < 2; w++) {
       const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
       const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
-      if (inc > 0xFFFFFFFFull)  // (the round kernels keep the increment as 32 bits: > 34 Pbit/s)
-        return set_error(ctx, SGN_EINVAL, "host bandwidth above 34 Pbit/s (token-bucket increment > 2^32 bytes)");
       r.tb_inc[w] = inc;
       r.tb_cap[w] = inc + SGN_CONFIG_MTU;
       r.tb_bal[w] = inc + SGN_CONFIG_MTU;

@@ -155,7 +155,6 @@ enum : uint32_t {
   OVF_TIMEOUT = 64u,  // a persistent grid barrier gave up (grid not resident)
   OVF_DRAIN = 128u,   // drain buffer full (raise sgn_drain_enable's capacity)
   OVF_HORIZON = 256u, // a delivery beyond the event calendar's horizon
-  OVF_APPK = 512u,    // a host's synthetic app counter passed 2^32 events
 };
 
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).

@@ -113,3 +113,20 @@ def test_two_shards_grow_together(ctxf, oracle, monkeypatch, slot):
             assert len(bad) == 0, (r, f, len(bad), lo.value + bad[:5], [x.engine_info() for x in shards])
         assert s.window() == one.window()
         _pages_ok(s.engine_info())
+
+
+def test_bandwidths_beyond_32bit_increments(ctxf, oracle):
+    """Token-bucket refill increments (bytes per ms) above 2^32 — a host above 34 Tbit/s — run
+    bit-exact: the round kernels keep every per-host field at its full width (LaneRc), in
+    registers for PERIODIC traffic and in LDS for TGEN, so no bandwidth the reference accepts
+    is refused or truncated."""
+    for kind in (sgn.TRAFFIC_PERIODIC, sgn.TRAFFIC_TGEN):
+        n = 60
+        args = list(scenario(n=n, V=8, kind=kind, stop_ns=60_000_000))
+        bwv = np.full(n, 10_000_000, dtype=np.uint64)
+        bwv[::7] = 40_000_000_000_000  # 40 Tbit/s: 5e9 bytes per ms
+        h = args[2]
+        args[2] = sgn.HostArrays(h.ip, h.node_id, bwv, bwv, h.seed)
+        o, c = run_both(ctxf, oracle, tuple(args), trace=True)
+        assert c.stats()["rounds"] > 0
+        assert_same_run(o, c, n, trace=True)
