@@ -388,8 +388,8 @@ def main():
     else:
         g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes)
         # calendar slabs of 128 runs per host group and bucket: ~64 due on average, 108 at most
-        # measured (a 128-run slab keeps the round kernel at 6 workgroups per CU; overflow is
-        # detected and reported, never silent)
+        # measured (a 128-run slab keeps the round kernel at 8 workgroups per CU; a fuller slab
+        # spills and the calendar is re-laid out with larger slabs, never silently)
         groups = -(-n_shard // 64)
         cfg.event_capacity = 257 * groups * 128
     if cfg.event_capacity and world > 1 and not args.weak and args.workload != "D":
