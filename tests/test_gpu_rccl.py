@@ -60,3 +60,20 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload, pool
         assert x["spills"] >= 1
     if pools:
         assert x["slot_runs"] > 64 and x["spills"] >= 1
+
+
+def test_rccl_eight_ranks_one_gpu_match_unsharded():
+    """The driver's N = 8 configuration: config C's 100 k hosts over eight ranks (12.5 k each),
+    every rank exchanging with seven peers each round, against one unsharded run."""
+    env = dict(os.environ, NCCL_DEBUG="WARN", TMPDIR="/tmp")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", "29546", "bench.py", "--gpus", "8",
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--hosts", "100000", "--rounds-per-step", "40"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 8 and line["config"]["hosts_per_gpu"] == 12_500
+    assert line["apsp_sharded"]["equal_on_all_ranks"] is True
+    assert line["parity"] is True, line.get("parity_detail")
+    assert line["parity_detail"]["hosts_compared"] == 100_000
+    assert line["rounds_timed"] == 80
