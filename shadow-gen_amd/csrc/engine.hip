@@ -114,6 +114,10 @@ __device__ __forceinline__ void xoshiro_step(uint64_t& s0, uint64_t& s1, uint64_
   s2 = n2;
 }
 __device__ __forceinline__ uint64_t xoshiro_out(uint64_t s0, uint64_t s3) { return rotl64c<23>(s0 + s3) + s0; }
+__device__ __forceinline__ uint32_t xoshiro_out_hi_nc(uint64_t s0, uint64_t s3) {
+  const uint64_t a = s0 + s3;
+  return __builtin_amdgcn_alignbit(hi32(a), lo32(a), 9) + hi32(s0);  // hi32(rotl(a, 23)) + hi32(s0)
+}
 __device__ __forceinline__ uint64_t sat_sub(uint64_t a, uint64_t b) { return a > b ? a - b : 0; }
 __device__ __forceinline__ uint64_t mul_sat(uint64_t a, uint64_t b, uint64_t cap) {
   uint64_t hi = __umul64hi(a, b);
@@ -602,6 +606,13 @@ struct HostExec {
     return result;
   }
   __device__ __forceinline__ void rng_skip() { xoshiro_step(r0, r1, r2, r3); }  // rng_next without its output
+  // rng_next's high word without the carry out of its low word (the true high word is this
+  // or this + 1): three VALU ops where the whole output takes six
+  __device__ __forceinline__ uint32_t rng_next_hi_nc() {
+    const uint32_t h = xoshiro_out_hi_nc(r0, r3);
+    xoshiro_step(r0, r1, r2, r3);
+    return h;
+  }
   __device__ __forceinline__ double rng_f64() {
     return (double)(rng_next() >> 11) * 0x1.0p-53;
   }
@@ -1305,7 +1316,42 @@ struct HostExec {
       const uint64_t Tx = T << 11;
       uint32_t sent = 0, j = 0;
       // eight draws per test (same-box A/B on config C: +1.3 % over four, sixteen was slower;
-      // the loop's scalar control and test sit on the slowest waves' chain)
+      // the loop's scalar control and test sit on the slowest waves' chain). The test is a
+      // screen: a draw drops only if its high word is >= Tx's, and the high word is at most
+      // the carry-less one + 1, so when the eight carry-less high words' maximum + 1 is below
+      // Tx's high word none drops; otherwise the eight draws are redone exactly from the saved
+      // state (probability ~ 8 x the path's loss). The stream advances the same either way.
+      // Paths losing more than 1/32 of their packets would redo most batches (~1.7x the
+      // exact test's cost), so they keep the exact test below. Same-box A/B: C -2.2 % per
+      // launch (3486 -> 3411 us); micro-benchmark 126 -> 87 cycles per draw for a lone lane.
+      // (TGEN kernel only: its servers send trains; a PERIODIC host sends single datagrams,
+      // and the screen's registers took that kernel from 231 to 256 VGPRs)
+      const uint32_t Th = (uint32_t)(Tx >> 32);
+      if (kApp == SGN_TRAFFIC_TGEN && Th >= 0xF8000000u) for (; j + 8 <= n; j += 8) {
+        const uint64_t a0 = r0, a1 = r1, a2 = r2, a3 = r3;
+        const uint32_t h0 = rng_next_hi_nc(), h1 = rng_next_hi_nc(), h2 = rng_next_hi_nc(), h3 = rng_next_hi_nc();
+        const uint32_t h4 = rng_next_hi_nc(), h5 = rng_next_hi_nc(), h6 = rng_next_hi_nc(), h7 = rng_next_hi_nc();
+        const uint32_t hm = max(max(max(h0, h1), max(h2, h3)), max(max(h4, h5), max(h6, h7)));
+        if (hm >= Th - 1 || Th == 0) {  // (hm + 1 >= Th without the wrap)
+          r0 = a0;
+          r1 = a1;
+          r2 = a2;
+          r3 = a3;
+          const uint64_t x0 = rng_next(), x1 = rng_next(), x2 = rng_next(), x3 = rng_next();
+          const uint64_t x4 = rng_next(), x5 = rng_next(), x6 = rng_next(), x7 = rng_next();
+          loss_step(x0 >= Tx, run, sent, dst, deliver);
+          loss_step(x1 >= Tx, run, sent, dst, deliver);
+          loss_step(x2 >= Tx, run, sent, dst, deliver);
+          loss_step(x3 >= Tx, run, sent, dst, deliver);
+          loss_step(x4 >= Tx, run, sent, dst, deliver);
+          loss_step(x5 >= Tx, run, sent, dst, deliver);
+          loss_step(x6 >= Tx, run, sent, dst, deliver);
+          loss_step(x7 >= Tx, run, sent, dst, deliver);
+        } else {
+          run += 8;
+          sent += 8;
+        }
+      }
       for (; j + 8 <= n; j += 8) {
         const uint64_t x0 = rng_next(), x1 = rng_next(), x2 = rng_next(), x3 = rng_next();
         const uint64_t x4 = rng_next(), x5 = rng_next(), x6 = rng_next(), x7 = rng_next();
@@ -1944,7 +1990,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     for (uint32_t j0 = 0; j0 < n; j0 += 64) {
       const uint32_t j = j0 + lane;
       EvRec r = r0;
-      if ((j0 > 0 || lane >= GATHER_SPEC) && j < n) r = ld_dev_rec(pb + j);
+      if ((j0 > 0 || lane >= S.gspec) && j < n) r = ld_dev_rec(pb + j);
       const bool due = j < n && (!last || r.time < we);
       const bool keep = j < n && !due;
       const uint64_t dm = __ballot(due), km = __ballot(keep);
@@ -1988,7 +2034,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
     const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
     // the slab's fill and its first GATHER_SPEC records in ONE round trip: the records are
-    // loaded before the fill is known (CAP >= 64; slots past the fill are ignored) — nothing
+    // loaded before the fill is known (S.gspec <= CAP; slots past the fill are ignored) — nothing
     // appends to a bucket's slab while its window runs (new runs for the window's last
     // bucket go to the spare slab set). Only GATHER_SPEC lanes load speculatively: a slab
     // holds ~4 runs on average, and loading all 64 slots pulled 2 KB of cold HBM lines per
@@ -2007,7 +2053,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       ib1 = (size_t)(S.NB <= LDS_BSLAB ? lbs[(b + 1) & (S.NB - 1)] : ld_dev(&S.bucket_slab[(b + 1) & (S.NB - 1)])) * S.G + g;
       pb1 = S.pool + ib1 * S.CAP;
     }
-    if (lane < GATHER_SPEC) {
+    if (lane < S.gspec) {
       r0 = ld_dev_rec(pb + lane);
       if (pair) r1 = ld_dev_rec(pb1 + lane);
     }
@@ -3768,6 +3814,17 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   *ctx->h_ctrl = c;
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
+  // PERIODIC traffic: each host receives ~BW / period runs per bucket, so a group's slab holds
+  // ~gsz * BW / period; when that is a full wave (config D: 64 hosts, one send per window) all
+  // 64 lanes load speculatively and the second round trip goes (same-box A/B: D +1.3 %, while
+  // B's ~2-run slabs measured 1 % slower at 64 and unchanged at 4 and 8)
+  S.gspec = GATHER_SPEC;
+  if (S.tkind == SGN_TRAFFIC_PERIODIC && S.period) {
+    const uint64_t fill = ((uint64_t)gsz * BW + S.period - 1) / S.period;
+    while (S.gspec < 64 && S.gspec < fill) S.gspec *= 2;
+  }
+  if (const char* e = getenv("SGN_GATHER_SPEC")) S.gspec = std::min<uint32_t>(64, (uint32_t)atoi(e));
+  S.gspec = (uint32_t)std::min<uint64_t>(S.gspec, S.CAP);  // speculative loads stay inside the slab
   size_round_kernels(ctx, S);
   // persistent-round buffers (three, by round % 3): chunk minima + keep minima, counters
   S.rb_min = (decltype(S.rb_min))dalloc<uint64_t>(ctx, 3 * RB_CH * RB_MS_MAX + 4);

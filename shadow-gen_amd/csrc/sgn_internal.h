@@ -341,9 +341,9 @@ struct DevSim {
   SGN_GLB uint32_t* rb_cnt;       // [3][65], then one monotone counter: the gap barrier (k_rounds)
   SGN_GLB uint64_t* rb_occ;       // [3][64] per-chunk calendar occupancy change of the round,
                                   // then rb_alloc [3] (pages allocated) and rb_spill [3] (runs spilled)
+  uint32_t gspec;         // slab slots a gather loads before the fill is known (sim_init)
   uint32_t fuse_finalize; // single shard: k_execute's last wave runs the round edge
   uint32_t agg_bmin;      // the round kernels fold bucket minima in an LDS table (see engine.hip)
-  uint32_t pad3;
   uint64_t BW;
   UDiv64 bw_div;          // division by BW
   SGN_GLB uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)

@@ -206,8 +206,13 @@ def test_codel_control_law_on_device(ctxf, oracle):
 def scenario(n=200, V=50, *, kind=sgn.TRAFFIC_PERIODIC, stop_ns=500_000_000, bw=10_000_000,
              seed=1, graph_seed=1, dynamic=False, runahead_ns=1_000_000, bootstrap_ns=0,
              unknown=10, period_ns=1_000_000, fifo=64, codel=4096, tgen_think=50_000_000,
-             tor=False, qdisc=0):
-    g = sgn.tor_graph(V, seed=graph_seed) if tor else sgn.random_graph(V, seed=graph_seed)
+             tor=False, qdisc=0, loss_hi=None):
+    if tor:
+        g = sgn.tor_graph(V, seed=graph_seed)
+    elif loss_hi is not None:
+        g = sgn.random_graph(V, seed=graph_seed, loss_frac=0.5, loss_hi=loss_hi)
+    else:
+        g = sgn.random_graph(V, seed=graph_seed)
     used = np.arange(V)
     names = sgn.host_names(n)
     seeds = sgn.derive_seeds(seed, names)
@@ -277,6 +282,19 @@ def test_engine_periodic_trace(ctxf, oracle):
     assert c.stats()["packets_sent"] > 10000
     assert c.stats()["packets_unknown_dst"] > 0 and c.stats()["packets_loss_dropped"] > 0
     assert_same_run(o, c, args[2].n)
+
+
+@pytest.mark.parametrize("loss_hi", [0.02, 0.2])
+def test_engine_tgen_untraced_loss_tests(ctxf, oracle, loss_hi):
+    """Untraced TGEN trains take the batched loss test (engine.hip send_batch): eight draws
+    per test, screened on the carry-less high words for paths losing <= 1/32, exact for
+    lossier ones. Edges losing up to 2 % (mostly screened) and up to 20 % (both forms)."""
+    args = scenario(n=300, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=2_000_000_000, loss_hi=loss_hi,
+                    tgen_think=100_000_000)
+    o, c = run_both(ctxf, oracle, args, trace=False)
+    st = c.stats()
+    assert st["packets_sent"] > 40_000 and st["packets_loss_dropped"] > (400 if loss_hi < 0.1 else 4000), st
+    assert_same_run(o, c, args[2].n, trace=False)
 
 
 def test_engine_tgen_trace_codel(ctxf, oracle):
