@@ -290,11 +290,14 @@ constexpr uint32_t GATHER_SPEC = 16;  // slab slots a gather loads before the fi
 // by all 64 lanes at once (one round trip for all the slab reservations of the wave instead
 // of one per send in the sending lane's serial path). A full outbox falls back to placing
 // the record at once.
-constexpr uint32_t OBOX = 24;
-struct Outbox {
-  EvRec rec[OBOX];
-  uint32_t idx[OBOX];  // (slab set, group) slab index
-  uint32_t n;          // records appended (may exceed OBOX: those were placed directly)
+// Its size is per kernel: 40 records for TGEN (config C: ~100 of 1563 server groups send more
+// than 24 records a round, up to ~90; same-box A/B 24 -> 40: -0.5 % per launch, and 40 still
+// leaves C at 7 workgroups per CU), 24 for the others (config D's PERIODIC kernel is at 8
+// workgroups per CU with 512 B of LDS to spare).
+template <uint32_t kApp>
+constexpr uint32_t kObox = kApp == SGN_TRAFFIC_TGEN ? 40 : 24;
+struct OutboxHdr {
+  uint32_t n;          // records appended (may exceed the outbox: those were placed directly)
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
   uint64_t hz;         // calendar horizon: a run at or after it would alias a live bucket
   SGN_GLB uint64_t* keepmin;  // minimum of this round's new runs for the window's last bucket
@@ -305,11 +308,18 @@ struct Outbox {
   SGN_GLB uint64_t* pg_allocd;// ... and allocated-page counter (the round edge's guard)
   SGN_GLB uint64_t* spilled;  // runs this round put in the calendar's spill area
 };
+template <uint32_t N>
+struct OutboxN : OutboxHdr {
+  EvRec rec[N];
+  uint32_t idx[N];  // (slab set, group) slab index
+};
+template <uint32_t kApp>
+using Outbox = OutboxN<kObox<kApp>>;
 
 // A run whose calendar slab is full goes to the spill area with its slab index (lossless; the
 // round edge holds and the host re-lays the calendar out before the run can be due). Only a
 // full spill area is an overflow.
-__device__ __forceinline__ void spill_run(const DevSim& S, Outbox* ob, uint32_t idx, const EvRec& r) {
+__device__ __forceinline__ void spill_run(const DevSim& S, OutboxHdr* ob, uint32_t idx, const EvRec& r) {
   SGN_GLB Ctrl* C = S.ctrl;
   const uint64_t i = __hip_atomic_fetch_add(&C->spill_n, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ob) cnt_add(ob->spilled, 1);
@@ -419,14 +429,14 @@ struct HostExec {
   }
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint16_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
-  Outbox* ob;             // the wave's outbox (LDS)
+  Outbox<kApp>* ob;       // the wave's outbox (LDS)
 #ifdef SGN_DIAG
   uint32_t dgt[DGT_N];
   uint32_t wk[5];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS<kApp>* l, const uint16_t* bs, Outbox* o)
+                      LaneLDS<kApp>* l, const uint16_t* bs, Outbox<kApp>* o)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
 
   // the host's state into registers (once per round, only for hosts with something due)
@@ -1420,7 +1430,7 @@ struct HostExec {
         min_nr(b == b1 ? ob->keepmin : &S.bucket_min[b], deliver);
       if (nrec == 1) {
         const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
-        if (k < OBOX) {
+        if (k < kObox<kApp>) {
           EvRec& r = ob->rec[k];
           r.time = deliver;
           r.eid = eid0;
@@ -1918,7 +1928,7 @@ struct ExecLDS {
   uint32_t* lcur;     // placement cursors (after placement: segment ends, start = end - count)
   void* lslot;        // the lanes' LDS slots (LaneLDS<kApp>[64])
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
-  Outbox* ob;         // the wave's outbox
+  OutboxHdr* ob;      // the wave's outbox (an Outbox<kApp>)
   uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
 };
 
@@ -1968,7 +1978,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     lmin = S.nextloc[h];
     if (kApp == SGN_TRAFFIC_PERIODIC) np = S.npeer[h];
   }
-  Outbox* ob = X.ob;
+  Outbox<kApp>* ob = static_cast<Outbox<kApp>*>(X.ob);
   if (lane == 0) {
     ob->n = 0;
     ob->xmin = INVALID;
@@ -2004,7 +2014,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
         k = __shfl(k, 0, 64) + lanes_below(km);
         if (keep) {
           kmin = r.time < kmin ? r.time : kmin;
-          if (k < OBOX) {
+          if (k < kObox<kApp>) {
             ob->rec[k] = r;
             ob->idx[k] = (uint32_t)ik;
           } else {
@@ -2161,7 +2171,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   // the outbox's records into their slabs, all lanes at once (the arrival's vmcnt(0)
   // completes them before the round edge)
   {
-    const uint32_t no = min(ob->n, OBOX);
+    const uint32_t no = min(ob->n, kObox<kApp>);
     for (uint32_t i = lane; i < no; i += 64) {
       const uint32_t idx = ob->idx[i];
       const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
@@ -2214,6 +2224,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       st[5] = t_gather;
       st[6] = t_exec;
       st[7] = rt0;  // 100 MHz constant clock: wave start / end across the chip
+      st[8] = ob->n;  // records sent to this shard's calendar (past the outbox: placed at once)
       st[30] = __builtin_amdgcn_s_memrealtime();
     }
 #ifdef SGN_DIAG
@@ -2257,7 +2268,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   __shared__ uint32_t lcnt_[64], lcur_[64];                                         \
   __shared__ LaneLDS<kApp> lslot_[64];                                               \
   __shared__ uint16_t lbs_[LDS_BSLAB];                                               \
-  __shared__ Outbox ob_;                                                             \
+  __shared__ Outbox<kApp> ob_;                                                       \
   ExecLDS X;                                                                         \
   X.lev = (EvRec*)lds_dyn;                                                           \
   X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \

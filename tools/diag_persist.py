@@ -55,6 +55,7 @@ for rep in range(3):
     s = out.reshape(W, sgn.STAMP_WORDS).astype(np.int64)
     cyc, ev, mx, busy, runs, tg, tx, t0, t1 = (s[:, 0], s[:, 1], s[:, 2], s[:, 3], s[:, 4], s[:, 5], s[:, 6],
                                                s[:, 7], s[:, 30])
+    obx = s[:, 8]
     base = t0.min()
     st_us, en_us = (t0 - base) / 100.0, (t1 - base) / 100.0
     mhz = np.median(cyc / np.maximum(t1 - t0, 1) * 100.0)
@@ -65,7 +66,8 @@ for rep in range(3):
     order = np.argsort(en_us)[::-1]
     for i in order[:8]:
         print(f"     group {i:5d} end={en_us[i]:6.1f}us start={st_us[i]:5.2f} cycles={cyc[i]:7d} gather={tg[i]:6d} "
-              f"exec={tx[i]:6d} busy={busy[i]:2d} events={ev[i]:5d} max_lane={mx[i]:4d} runs={runs[i]:4d}")
+              f"exec={tx[i]:6d} busy={busy[i]:2d} events={ev[i]:5d} max_lane={mx[i]:4d} runs={runs[i]:4d} sent_recs={obx[i]:4d}")
+    print(f"     records sent per group: p50={np.median(obx):.0f} max={obx.max()} groups past the outbox (24): {(obx > 24).sum()}")
     # the distribution of group cycles by kind of group (first groups are TGEN servers)
     dec = np.array_split(np.arange(W), 10)
     print("     cycles p50 by tenth of the groups: " + " ".join(f"{np.median(cyc[d]):.0f}" for d in dec))
