@@ -81,10 +81,11 @@ def build_workload_b(n_hosts, V, seed=1):
     return g, used, hosts, cfg, tr
 
 
-def build_workload_d(n_hosts, V, seed=1):
+def build_workload_d(n_hosts, V, seed=1, stop_ns=1_000_000_000):
     """Config D (BASELINE.json configs[3]): the config-B graph (1000-node random GML, mean
     degree 6, 20 % lossy edges, 100 Mbit), every host sends a 64 B datagram to a uniform
-    random peer every 1 ms (dense all-to-all)."""
+    random peer every 1 ms (dense all-to-all). The bench sets stop_ns so that every timed
+    step has its full rounds (1 ms each)."""
     g = sgn.random_graph(V, seed=42)
     used = np.arange(V, dtype=np.uint32)
     seeds = sgn.derive_seeds(seed, sgn.host_names(n_hosts))
@@ -92,7 +93,7 @@ def build_workload_d(n_hosts, V, seed=1):
     hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), (np.arange(n_hosts) % V).astype(np.uint32), bw, bw, seeds)
     tr = sgn.make_traffic(sgn.TRAFFIC_PERIODIC, flow_seed=7, start_ns=0, start_jitter_ns=1_000_000,
                           period_ns=1_000_000, payload_len=64, unknown_dst_permille=0)
-    cfg = sgn.make_config(1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=16, codel_cap=64,
+    cfg = sgn.make_config(stop_ns, runahead_ns=1_000_000, out_fifo_cap=16, codel_cap=64,
                           event_capacity=0)
     return g, used, hosts, cfg, tr
 
@@ -386,7 +387,8 @@ def main():
     elif args.workload == "B":
         g, used, hosts, cfg, tr = build_workload_b(n_total, args.nodes)
     else:
-        g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes)
+        stop = max(1_000_000_000, (args.warmup + args.steps + 1) * args.rounds_per_step * 1_000_000)
+        g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes, stop_ns=stop)
         # calendar slabs of 128 runs per host group and bucket: ~64 due on average, 108 at most
         # measured (a 128-run slab keeps the round kernel at 8 workgroups per CU; a fuller slab
         # spills and the calendar is re-laid out with larger slabs, never silently)
