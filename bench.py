@@ -98,6 +98,27 @@ def build_workload_d(n_hosts, V, seed=1, stop_ns=1_000_000_000):
     return g, used, hosts, cfg, tr
 
 
+def build_workload_h(n_hosts, V, seed=1):
+    """Hot-spot fan-in (a test workload, not a BASELINE config): 8 TGEN servers (the first
+    HostIds: shard 0) and every other host a client that first fetches a one-packet
+    file from one of them at the same instant, then every ~50 ms. Thousands of request runs land
+    in the servers' (bucket, host group) slabs each round — the fan-in the reference's unbounded
+    per-host EventQueue takes (core/work/event_queue.rs:12,57-66) — and with N > 1 most of them
+    arrive through the round exchange (k_import)."""
+    g = sgn.tor_graph(V, seed=42)
+    used = np.arange(V, dtype=np.uint32)
+    seeds = sgn.derive_seeds(seed, sgn.host_names(n_hosts))
+    bw = np.full(n_hosts, 1_000_000_000, dtype=np.uint64)
+    hosts = sgn.HostArrays(sgn.assign_ips(n_hosts), (np.arange(n_hosts) % V).astype(np.uint32), bw, bw, seeds)
+    servers = np.arange(8, dtype=np.uint32)
+    tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, flow_seed=7, start_ns=0, start_jitter_ns=0,
+                          period_ns=50_000_000, period_jitter_ns=50_000_000, req_payload=64,
+                          servers=servers, file_bytes=(1000, 1400, 1400))
+    cfg = sgn.make_config(3600 * 1_000_000_000, runahead_ns=1_000_000, out_fifo_cap=64,
+                          codel_cap=64, event_capacity=1 << 22)
+    return g, used, hosts, cfg, tr
+
+
 def events_of(st):
     return st["packets_sent"] + st["packets_loss_dropped"] + st["packet_events_popped"]
 
@@ -339,9 +360,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=("B", "C", "D"), default="C",
+    ap.add_argument("--workload", choices=("B", "C", "D", "H"), default="C",
                     help="C: the headline 100k-host Tor-like tgen workload; B: 10k hosts, UDP every 10 ms "
-                         "on a random graph; D: 1M hosts, dense all-to-all")
+                         "on a random graph; D: 1M hosts, dense all-to-all; H: hot-spot fan-in (a test "
+                         "workload: 8 servers, every client fetches at once)")
     ap.add_argument("--hosts", type=int, default=None,
                     help="hosts in the simulation (B: 10k, C: 100k, D: 1M), sharded over the GPUs; "
                          "with --weak: hosts per GPU")
@@ -379,13 +401,15 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
     if args.hosts is None:
-        args.hosts = {"B": 10_000, "C": 100_000, "D": 1_000_000}[args.workload]
+        args.hosts = {"B": 10_000, "C": 100_000, "D": 1_000_000, "H": 20_000}[args.workload]
     n_total = args.hosts * world if args.weak else args.hosts
     n_shard = -(-n_total // world)  # hosts per GPU (the last shard may hold fewer)
     if args.workload == "C":
         g, used, hosts, cfg, tr = build_workload(n_total, args.nodes)
     elif args.workload == "B":
         g, used, hosts, cfg, tr = build_workload_b(n_total, args.nodes)
+    elif args.workload == "H":
+        g, used, hosts, cfg, tr = build_workload_h(n_total, args.nodes)
     else:
         stop = max(1_000_000_000, (args.warmup + args.steps + 1) * args.rounds_per_step * 1_000_000)
         g, used, hosts, cfg, tr = build_workload_d(n_total, args.nodes, stop_ns=stop)
@@ -551,6 +575,7 @@ def main():
             "workload": {"C": "C: Tor-like 1000-node complete graph, tgen-style UDP trains",
                          "B": "B: 1000-node random graph (20 % lossy edges), 1024 B UDP every 10 ms to random peers",
                          "D": "D: 1000-node random graph, every host sends 64 B to a uniform random peer every 1 ms",
+                         "H": "H (test workload): hot-spot fan-in, every client fetches from one of 8 servers",
                          }[args.workload],
             "hosts_per_gpu": n_shard, "hosts_total": n_total, "graph_nodes": args.nodes,
             "rounds_per_step": args.rounds_per_step, "runahead_ms": 1,
@@ -572,7 +597,8 @@ def main():
         "engine": {k: info[k] for k in ("calendar_buckets", "bucket_width_ns", "host_groups", "slab_capacity",
                                         "persistent_grid", "persistent_fallbacks", "codel_pages",
                                         "codel_page_allocs", "bucket_min_lds", "codel_pool_grows",
-                                        "calendar_grows", "exchange_slot_grows", "rounds_held")},
+                                        "calendar_grows", "exchange_slot_grows", "rounds_held",
+                                        "slab_extensions", "big_slab_pieces", "calendar_spill_runs")},
     }
     if world > 1:
         # the round exchange: per-peer slot, runs per peer a round moves now

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 7
+#define SGN_ABI_VERSION 8
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -445,6 +445,16 @@ typedef struct sgn_engine_info {
   uint64_t calendar_spill_runs;  /* runs that went to the calendar's spill area (then re-filed) */
   uint64_t exchange_slot_grows;  /* multi-shard exchange slot enlargements */
   uint64_t rounds_held;          /* rounds held at their start for a pool to grow */
+  /* ABI 8: hot slabs. A (bucket, host group) slab past its capacity continues in an extension
+   * (laid out at a held round edge); a slab holding more runs than one workgroup's LDS orders
+   * at once is ordered and executed in pieces in Shadow's key order (event.rs:84-155), so no
+   * fan-in is refused (the reference's EventQueue is an unbounded BinaryHeap,
+   * core/work/event_queue.rs:12,57-66). */
+  uint64_t slab_extensions;      /* slabs with an extension now */
+  uint64_t slab_extension_runs;  /* runs the extensions hold in total */
+  uint64_t big_slab_pieces;      /* pieces run by the big-slab path since sim_init */
+  uint64_t spill_area_runs;      /* the spill area's capacity */
+  uint64_t spill_area_grows;     /* spill area enlargements */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

@@ -247,6 +247,68 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return v;
 }
 
+// wave-uniform values (the same in every lane) into scalar registers: vector registers are the
+// round kernels' scarce resource
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    uint32_t lo = __shfl_xor((uint32_t)v, off, 64);
+    uint32_t hi = __shfl_xor((uint32_t)(v >> 32), off, 64);
+    uint64_t o = ((uint64_t)hi << 32) | lo;
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// ---- a big slab's order key: Shadow's (time, src host, src event id) (core/work/event.rs:84-155)
+// as one 160-bit string (time - tmin, src, eid) in three words, for a radix select over it ----
+struct BigKey {
+  uint64_t hi, mid, lo;  // time - tmin | src << 32 | eid >> 32 | eid << 32 (low 32 bits zero)
+};
+__device__ __forceinline__ BigKey big_key(const EvRec& r, uint64_t tmin) {
+  return {r.time - tmin, ((uint64_t)r.src << 32) | (r.eid >> 32), r.eid << 32};
+}
+__device__ __forceinline__ bool bk_less(const BigKey& a, const BigKey& b) {
+  return a.hi != b.hi ? a.hi < b.hi : a.mid != b.mid ? a.mid < b.mid : a.lo < b.lo;
+}
+// the 8-bit digit at bit p from the top (p a multiple of 8, < 192)
+__device__ __forceinline__ uint32_t bk_digit(const BigKey& k, uint32_t p) {
+  const uint64_t w = p < 64 ? k.hi : p < 128 ? k.mid : k.lo;
+  return (uint32_t)(w >> (56 - (p & 63))) & 0xFFu;
+}
+__device__ __forceinline__ BigKey bk_set_digit(BigKey k, uint32_t p, uint32_t d) {
+  const uint64_t v = (uint64_t)d << (56 - (p & 63));
+  if (p < 64) k.hi |= v; else if (p < 128) k.mid |= v; else k.lo |= v;
+  return k;
+}
+// k with every bit below the top p set (the largest key with k's top p bits)
+__device__ __forceinline__ uint64_t bk_fill_w(uint64_t w, int keep) {
+  return keep >= 64 ? w : keep <= 0 ? ~0ULL : (w | (~0ULL >> keep));
+}
+__device__ __forceinline__ BigKey bk_fill(const BigKey& k, uint32_t p) {
+  return {bk_fill_w(k.hi, (int)p), bk_fill_w(k.mid, (int)p - 64), bk_fill_w(k.lo, (int)p - 128)};
+}
+// the masks of a key's top p bits (wave-uniform: scalar registers)
+__device__ __forceinline__ BigKey bk_mask(uint32_t p) {
+  auto m = [](int keep) -> uint64_t { return keep >= 64 ? ~0ULL : keep <= 0 ? 0ULL : ~(~0ULL >> keep); };
+  return {m((int)p), m((int)p - 64), m((int)p - 128)};
+}
+__device__ __forceinline__ bool bk_prefix_eq(const BigKey& a, const BigKey& b, const BigKey& m) {
+  return (((a.hi ^ b.hi) & m.hi) | ((a.mid ^ b.mid) & m.mid) | ((a.lo ^ b.lo) & m.lo)) == 0;
+}
+// the key fields of a record written by another workgroup (device-scope loads)
+__device__ __forceinline__ void ld_dev_key(SGN_GLB const EvRec* p, uint64_t& t, uint64_t& e, uint32_t& src) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  t = ld_dev(q);
+  e = ld_dev(q + 1);
+  src = (uint32_t)ld_dev(q + 2);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int off) {
   const uint32_t lo = __shfl_xor((uint32_t)v, off, 64);
   const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), off, 64);
@@ -286,6 +348,14 @@ struct Pkt {
 // A lane's LDS slot: the pending digest runs and the digests themselves (touched once per
 // run), and the CoDel queue's cached head and open tail runs.
 constexpr uint32_t GATHER_SPEC = 16;  // slab slots a gather loads before the fill is known
+// The round kernels' dynamic LDS before the optional bucket-minimum table: CAP event runs and
+// two u16 index arrays (padded to 8 bytes), at least 1 KB — a big slab's radix select keeps its
+// 256-bin histogram there (exec_group), and test hooks may set CAP below 32
+__host__ __device__ __forceinline__ size_t exec_lds_runs_bytes(uint32_t cap) {
+  const size_t b = (size_t)cap * sizeof(EvRec) + 2 * (size_t)((cap + 3) & ~3u) * 2;
+  return b > 1024 ? b : 1024;
+}
+
 // The wave's outbox: event records for this shard's calendar, placed after the event loop
 // by all 64 lanes at once (one round trip for all the slab reservations of the wave instead
 // of one per send in the sending lane's serial path). A full outbox falls back to placing
@@ -329,6 +399,21 @@ __device__ __forceinline__ void spill_run(const DevSim& S, OutboxHdr* ob, uint32
   } else if ((atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0) {
     C->overflow_info = r.dst;
   }
+}
+
+// A run at position pos >= CAP of slab idx: the slab's extension when it has room, else the
+// spill area (lossless either way).
+__device__ __forceinline__ void place_overflow(const DevSim& S, OutboxHdr* ob, uint32_t idx, uint32_t pos,
+                                               const EvRec& r) {
+  if (S.ext) {
+    const uint64_t x = S.ext[idx];
+    const uint32_t k = pos - S.CAP;
+    if (k < (uint32_t)(x >> 40)) {
+      st_dev_rec(S.ext_pool + (x & EXT_OFF_MASK) + k, r);
+      return;
+    }
+  }
+  spill_run(S, ob, idx, r);
 }
 
 // LDS copies of queue entries need only 8-byte alignment (a 16-byte-aligned member would
@@ -439,8 +524,9 @@ struct HostExec {
                       LaneLDS<kApp>* l, const uint16_t* bs, Outbox<kApp>* o)
       : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
 
-  // the host's state into registers (once per round, only for hosts with something due)
-  __device__ __forceinline__ void load() {
+  // the host's state into registers (once per round, only for hosts with something due);
+  // fresh = false: a reload after park() (the pending digest runs in LDS continue)
+  __device__ __forceinline__ void load(bool fresh = true) {
     R = S.hrec + h;
     const HostRec& r = *R;
     gid = r.gid;
@@ -508,7 +594,7 @@ struct HostExec {
       L->fh = *fq_slot(0);
       lr().fh_idx = fq_head;
     }
-    L->rn[0] = L->rn[1] = L->rn[2] = 0;
+    if (fresh) L->rn[0] = L->rn[1] = L->rn[2] = 0;
 #ifdef SGN_DIAG
     for (int i = 0; i < DGT_N; i++) dgt[i] = 0;
     for (int i = 0; i < 5; i++) wk[i] = 0;
@@ -599,7 +685,26 @@ struct HostExec {
     if (tl_open) st_dev_cq(cq_tail_slot(), L->tl);
   }
 
-  // rare counters go straight to memory (registers are kept for the per-packet ones)
+  // The register state is dead from here (a big slab's passes run with the whole register file;
+  // park: the state went to memory with store(), and loaded lanes reload it): constants in every
+  // field that load() defines, on every path, so no earlier value stays live across the passes.
+  __device__ __forceinline__ void kill() {
+    gid = my_ip = my_unode = 0;
+    r0 = r1 = r2 = r3 = eid = 0;
+    st0 = st1 = st2 = se0 = se1 = se2 = 0;
+    fl = ro_dst = ro_pay = ro_tag = ri_src = ri_pay = ri_tag = 0;
+    ri_eid = tbb0 = tbl0 = tbb1 = tbl1 = 0;
+    cq_head = cq_nr = cq_len = fq_head = fq_len = 0;
+    cq_bytes = 0;
+    c_sent = c_loss = c_popped = c_deliv = c_localev = c_maxcodel = c_runs = 0;
+    c_bytes = 0;
+    hd_valid = tl_open = false;
+    if constexpr (kRcReg<kApp>) rr = LaneRc{};
+    pf_peer = 0;
+    pf_pi = 0;
+    R = nullptr;
+  }
+
 
 
   __device__ __forceinline__ uint64_t next_local_time() const {
@@ -1472,7 +1577,9 @@ struct HostExec {
       r.tag = tag;
       if (pos + m < cap)
         st_dev_rec(dstp + pos + m, r);
-      else  // the slab (or the peer's exchange slot) is full
+      else if (owned)  // the slab is full: its extension, or the spill area
+        place_overflow(S, ob, sidx, pos + m, r);
+      else  // the peer's exchange slot is full
         spill_run(S, ob, sidx, r);
     }
   }
@@ -1659,10 +1766,14 @@ struct HostExec {
   // time < until. A window is executed as consecutive sub-windows (one per calendar
   // bucket): nothing created inside a window is due in it (packet deliveries are >= the
   // window end, worker.rs:386-390), so this is the same sequence of events.
+  // tail: the time of the host's next packet run after ev[ord[s1 - 1]] (INVALID: none) — a
+  // slab ordered in pieces (exec_group's big-slab path) runs a host's runs over several calls,
+  // each up to the next piece's first time; flush: close the digests' pending runs (the last
+  // piece of the sub-window only, so the digest steps are those of one call over all runs)
   __device__ __forceinline__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
-                      uint64_t until) {
+                      uint64_t until, uint64_t tail, bool flush) {
     uint32_t pi = s0;
-    uint64_t pt = pi < s1 ? ev[ord[pi]].time : INVALID;  // next due packet run's time
+    uint64_t pt = pi < s1 ? ev[ord[pi]].time : tail;  // next due packet run's time
 #ifdef SGN_DIAG
 #endif
     while (true) {
@@ -1699,7 +1810,7 @@ struct HostExec {
         if (pi < s1 && pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           const EvRec& e = ev[ord[pi]];
           pi++;
-          pt = pi < s1 ? ev[ord[pi]].time : INVALID;  // the next run's time, ahead of need
+          pt = pi < s1 ? ev[ord[pi]].time : tail;  // the next run's time, ahead of need
           now = e.time;
           if (external() && e.src == gid) {  // a CPU application's datagram (sgn_submit)
             app_submit(e);
@@ -1725,7 +1836,7 @@ struct HostExec {
           // `now` (Packet < Local at equal times) and no other local event precedes it by
           // (time, event id): it runs in this iteration (the same sequence of events; the wave
           // saves a trip round the loop)
-          if (!next_local_now<1>(pi < s1 ? pt : INVALID)) continue;
+          if (!next_local_now<1>(pt)) continue;
           run_ls = 1;
         } else {
           if (lt >= until) break;
@@ -1744,7 +1855,7 @@ struct HostExec {
             DGT_END(DGT_LOAD, t0);
           }
           // a send queued at `now` makes relay_inet_out's task the next event: start it here
-          if (!next_local_now<0>(pi < s1 ? pt : INVALID)) continue;
+          if (!next_local_now<0>(pt)) continue;
           c_localev++;
         }
         // run_forward_task for relay_inet_out (relay/mod.rs:166-187): Idle, then Forwarding
@@ -1755,6 +1866,9 @@ struct HostExec {
       forward_out_step();
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
+    if (flush) flush_digests();
+  }
+  __device__ __forceinline__ void flush_digests() {
     dr_flush_same<0>();
     dr_flush_seq<1>();
     dr_flush_seq<2>();
@@ -1788,7 +1902,7 @@ __host__ __device__ __forceinline__ uint64_t codel_pages_bound(uint64_t due, uin
 }
 __device__ __forceinline__ uint64_t codel_round_bound(const DevSim& S, uint64_t occ, uint64_t ws, uint64_t we) {
   const uint32_t nbk = ((bucket_of(S, we - 1) - bucket_of(S, ws)) & (S.NB - 1)) + 1;
-  const uint64_t capb = (uint64_t)nbk * S.G * S.CAP;
+  const uint64_t capb = (uint64_t)nbk * S.G * S.CAP + S.ext_total;
   return codel_pages_bound(occ < capb ? occ : capb, S.nH);
 }
 __device__ __forceinline__ uint64_t pages_free(uint64_t avail, uint64_t alloc) {
@@ -1880,7 +1994,7 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
         st_dev(o + 4, pfree);
         st_dev(o + 5, occ);
         st_dev(o + 6, xsum);
-        st_dev(o + 7, (uint64_t)S.G * S.CAP);
+        st_dev(o + 7, (uint64_t)S.G * S.CAP + S.ext_total);
       }
       return;
     }
@@ -1930,6 +2044,16 @@ struct ExecLDS {
   uint16_t* lbs;      // bucket -> slab table for this round (when NB <= LDS_BSLAB; ids <= NB)
   OutboxHdr* ob;      // the wave's outbox (an Outbox<kApp>)
   uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
+  struct BigLDS* big; // a big slab's piece state (exec_group)
+};
+// A slab with more due runs than the LDS holds (a hot spot: thousands of sources sending to one
+// host group within a bucket width) is ordered and executed in pieces of at most CAP runs in
+// Shadow's key order: piece k holds the runs with keys in (bound k-1, bound k]. The piece state
+// lives in LDS across the pieces' event loops (registers are the round kernel's scarce resource).
+struct BigLDS {
+  uint64_t tmin, range;  // earliest due run's time, latest - earliest
+  uint64_t kp[3];        // the last piece's upper bound (BigKey)
+  uint32_t ndue, done, have_prev, pad;
 };
 
 // One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
@@ -1994,6 +2118,44 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 #ifdef SGN_DIAG
   uint64_t w_load = 0, w_run = 0;
 #endif
+  // a big slab's passes run with the lanes' host state parked in memory: store() (its round
+  // counters here), then the registers are dead until the lanes that had state reload it
+  uint32_t pk_runs = 0, pk_loss = 0, pk_lev = 0, n_pieces = 0;
+  uint64_t pk_bytes = 0;
+  auto park = [&]() {
+    if (loaded) {
+      ex.store();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (its write-through stores are asm)
+      pk_runs += ex.c_runs;
+      pk_loss += ex.c_loss;
+      pk_lev += ex.c_localev;
+      pk_bytes += ex.c_bytes;
+    }
+    ex.kill();
+  };
+  // the last bucket's later runs (keep: this lane's r) move to the spare slab set: through the
+  // outbox (placed with the sends after the event loop), or at once when it is full
+  auto keep_runs = [&](const EvRec& r, bool keep) {
+    const uint64_t km = __ballot(keep);
+    if (km) {
+      uint32_t k = 0;
+      if (lane == 0) k = atomicAdd(&ob->n, (uint32_t)__popcll(km));
+      k = __shfl(k, 0, 64) + lanes_below(km);
+      if (keep) {
+        kmin = r.time < kmin ? r.time : kmin;
+        if (k < kObox<kApp>) {
+          ob->rec[k] = r;
+          ob->idx[k] = (uint32_t)ik;
+        } else {
+          const uint32_t base = atomicAdd(&S.slab_n[ik], 1u);
+          if (base < S.CAP)
+            st_dev_rec(pk + base, r);
+          else
+            place_overflow(S, ob, (uint32_t)ik, base, r);
+        }
+      }
+    }
+  };
   // Append the runs of one slab (fill n, its first GATHER_SPEC records already in r0) that
   // are due to lev[N..]; in the window's last bucket the runs at >= we move to the spare slab.
   auto gather_slab = [&](SGN_GLB const EvRec* pb, const EvRec& r0, uint32_t n, bool last, uint32_t& N) {
@@ -2003,30 +2165,203 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       if ((j0 > 0 || lane >= S.gspec) && j < n) r = ld_dev_rec(pb + j);
       const bool due = j < n && (!last || r.time < we);
       const bool keep = j < n && !due;
-      const uint64_t dm = __ballot(due), km = __ballot(keep);
+      const uint64_t dm = __ballot(due);
       if (due) lev[N + lanes_below(dm)] = r;
       N += (uint32_t)__popcll(dm);
-      if (km) {
-        // the last bucket's later runs move to the spare slab set: through the outbox
-        // (placed with the sends after the event loop), or at once when it is full
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(&ob->n, (uint32_t)__popcll(km));
-        k = __shfl(k, 0, 64) + lanes_below(km);
-        if (keep) {
-          kmin = r.time < kmin ? r.time : kmin;
-          if (k < kObox<kApp>) {
-            ob->rec[k] = r;
-            ob->idx[k] = (uint32_t)ik;
-          } else {
-            const uint32_t base = atomicAdd(&S.slab_n[ik], 1u);
-            if (base < S.CAP)
-              st_dev_rec(pk + base, r);
-            else
-              spill_run(S, ob, (uint32_t)ik, r);
-          }
-        }
+      keep_runs(r, keep);
+    }
+  };
+  // ---- a big slab (more runs than CAP: its extension, and multi-shard runs k_import spilled) ----
+  // every pass reads the slab's runs from memory: the pool part, the extension, and (only when
+  // the fill exceeds both) the spill area's entries tagged with this slab (f: per 64-run batch,
+  // every lane; ok = the lane holds one of the slab's runs, si = its spill-area index or ~0)
+  auto big_scan = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, auto&& f) {
+    const uint32_t np = min(nraw, S.CAP);
+    for (uint32_t j0 = 0; j0 < np; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      EvRec r{};
+      if (j < np) r = ld_dev_rec(pb + j);
+      f(r, j < np, ~0ULL);
+    }
+    const uint64_t x = S.ext ? S.ext[ib] : 0ULL;
+    const uint32_t ecap = (uint32_t)(x >> 40), ne = min(nraw - np, ecap);
+    SGN_GLB const EvRec* pe = S.ext_pool + (x & EXT_OFF_MASK);
+    for (uint32_t j0 = 0; j0 < ne; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      EvRec r{};
+      if (j < ne) r = ld_dev_rec(pe + j);
+      f(r, j < ne, ~0ULL);
+    }
+    if (nraw - np > ecap) {
+      const uint64_t ns = min(ld_dev(&C->spill_imp), S.spill_cap);
+      for (uint64_t i0 = 0; i0 < ns; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool mine = i < ns && ld_dev(&S.spill_idx[i]) == (uint32_t)ib;
+        EvRec r{};
+        if (mine) r = ld_dev_rec(S.spill + i);
+        f(r, mine, i);
       }
     }
+  };
+  // big_scan over the key fields only (the radix select's passes)
+  auto big_scan_keys = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, auto&& f) {
+    const uint32_t np = min(nraw, S.CAP);
+    for (uint32_t j0 = 0; j0 < np; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      uint64_t t = 0, e = 0;
+      uint32_t src = 0;
+      if (j < np) ld_dev_key(pb + j, t, e, src);
+      f(t, e, src, j < np);
+    }
+    const uint64_t x = S.ext ? S.ext[ib] : 0ULL;
+    const uint32_t ecap = (uint32_t)(x >> 40), ne = min(nraw - np, ecap);
+    SGN_GLB const EvRec* pe = S.ext_pool + (x & EXT_OFF_MASK);
+    for (uint32_t j0 = 0; j0 < ne; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      uint64_t t = 0, e = 0;
+      uint32_t src = 0;
+      if (j < ne) ld_dev_key(pe + j, t, e, src);
+      f(t, e, src, j < ne);
+    }
+    if (nraw - np > ecap) {
+      const uint64_t ns = min(ld_dev(&C->spill_imp), S.spill_cap);
+      for (uint64_t i0 = 0; i0 < ns; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool mine = i < ns && ld_dev(&S.spill_idx[i]) == (uint32_t)ib;
+        uint64_t t = 0, e = 0;
+        uint32_t src = 0;
+        if (mine) ld_dev_key(S.spill + i, t, e, src);
+        f(t, e, src, mine);
+      }
+    }
+  };
+  // first pass: the later runs of the window's last bucket move to the spare slab set; the due
+  // runs' count and time range go to the piece state
+  auto big_prepare = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, bool last) {
+    uint64_t tmin = INVALID, tmax = 0;
+    uint32_t nd = 0;
+    big_scan(ib, pb, nraw, [&](const EvRec& r, bool ok, uint64_t) {
+      const bool due = ok && (!last || r.time < we);
+      if (due) {
+        tmin = r.time < tmin ? r.time : tmin;
+        tmax = r.time > tmax ? r.time : tmax;
+      }
+      nd += (uint32_t)__popcll(__ballot(due));
+      keep_runs(r, ok && !due);
+    });
+    tmin = wave_min_u64(tmin);
+    tmax = wave_max_u64(tmax);
+    if (lane == 0) {
+      X.big->tmin = tmin;
+      X.big->range = nd ? tmax - tmin : 0;
+      X.big->ndue = nd;
+      X.big->done = 0;
+      X.big->have_prev = 0;
+    }
+    __syncthreads();
+  };
+  // The next piece into lev[0, N): the due runs with keys above the last piece's bound, up to CAP
+  // of them in key order. Its bound is found by a radix select over the 160-bit key (8-bit
+  // digits from the top, one pass and an LDS histogram per digit): the largest prefix range
+  // holding at most CAP of the remaining keys, taken at the first digit where it holds at least
+  // half of what is still wanted. Returns true for the last piece; else *bound_t = the bound's
+  // time part: the piece's runs are at or before it, every later run at or after it.
+  auto big_piece = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, bool last, uint32_t& N,
+                       uint64_t* bound_t) -> bool {
+    BigLDS& B = *X.big;
+    const uint64_t tmin = uni64(B.tmin);
+    const bool have = uni32(B.have_prev) != 0;
+    const BigKey kp = {uni64(B.kp[0]), uni64(B.kp[1]), uni64(B.kp[2])};
+    const bool fin = uni32(B.ndue - B.done) <= S.CAP;
+    auto in_s = [&](const EvRec& r, bool ok, BigKey& k) {
+      k = big_key(r, tmin);
+      return ok && (!last || r.time < we) && (!have || bk_less(kp, k));
+    };
+    BigKey kt = {~0ULL, ~0ULL, ~0ULL};
+    if (!fin) {
+      uint32_t* hist = (uint32_t*)lev;  // (lev is free until the piece is loaded)
+      const uint64_t range = uni64(B.range);
+      uint32_t p = range ? ((uint32_t)__builtin_clzll(range) & ~7u) : 64u;  // first digit that varies
+      BigKey P = {0, 0, 0};
+      uint32_t acc = 0;
+      while (true) {
+        for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
+        __syncthreads();
+        const BigKey pm = bk_mask(p);
+        big_scan_keys(ib, pb, nraw, [&](uint64_t t, uint64_t e, uint32_t src, bool ok) {
+          const BigKey k = {t - tmin, ((uint64_t)src << 32) | (e >> 32), e << 32};
+          if (ok && (!last || t < we) && (!have || bk_less(kp, k)) && bk_prefix_eq(k, P, pm))
+            atomicAdd(&hist[bk_digit(k, p)], 1u);
+        });
+        __syncthreads();
+        const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+        const uint32_t ls = h0 + h1 + h2 + h3;
+        uint32_t incl = ls;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(incl, off, 64);
+          if ((int)lane >= off) incl += y;
+        }
+        const uint32_t want = S.CAP - acc;
+        const uint32_t c0 = incl - ls + h0, c1 = c0 + h1, c2 = c1 + h2, c3 = c2 + h3;
+        // this lane's largest bin whose cumulative count is <= want (-1: none)
+        int dl = -1;
+        uint32_t cl = 0;
+        if (c0 <= want) { dl = 4 * (int)lane; cl = c0; }
+        if (c1 <= want) { dl = 4 * (int)lane + 1; cl = c1; }
+        if (c2 <= want) { dl = 4 * (int)lane + 2; cl = c2; }
+        if (c3 <= want) { dl = 4 * (int)lane + 3; cl = c3; }
+        int df = dl;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const int o = __shfl_xor(df, off, 64);
+          df = o > df ? o : df;
+        }
+        df = (int)uni32((uint32_t)df);
+        const uint32_t cf = uni32(df >= 0 ? __shfl(cl, df >> 2, 64) : 0u);
+        __syncthreads();  // every lane has read the histogram
+        if (df >= 0 && (2 * cf >= want || p + 8 >= 160 || df == 255)) {
+          kt = bk_fill(bk_set_digit(P, p, (uint32_t)df), p + 8);
+          break;
+        }
+        // descend into the bin that crosses: every key of the bins before it is in the piece
+        acc += cf;
+        P = bk_set_digit(P, p, (uint32_t)(df + 1));
+        p += 8;
+      }
+    }
+    N = 0;
+    big_scan(ib, pb, nraw, [&](const EvRec& r, bool ok, uint64_t) {
+      BigKey k;
+      const bool sel = in_s(r, ok, k) && !bk_less(kt, k);
+      const uint64_t m = __ballot(sel);
+      if (sel && N + lanes_below(m) < S.CAP) lev[N + lanes_below(m)] = r;
+      N += (uint32_t)__popcll(m);
+    });
+    if (N > S.CAP || (!fin && N == 0)) {  // (cannot happen: the select bounds every piece by
+      // CAP and takes at least one run) never silent, and the pieces end
+      if (lane == 0 && (atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0) C->overflow_info = gbase;
+      N = min(N, S.CAP);
+      B.done = B.ndue;
+      return true;
+    }
+    if (fin) {
+      // runs taken from the spill area are tagged done (the re-layout must not file them again)
+      big_scan(ib, pb, nraw, [&](const EvRec&, bool ok, uint64_t si) {
+        if (ok && si != ~0ULL) st_dev(&S.spill_idx[si], SPILL_DEAD);
+      });
+    } else {
+      *bound_t = uni64(kt.hi > EMU_MAX - tmin ? EMU_MAX : tmin + kt.hi);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      B.done += N;
+      B.have_prev = 1;
+      B.kp[0] = kt.hi;
+      B.kp[1] = kt.mid;
+      B.kp[2] = kt.lo;
+    }
+    return fin;
   };
   auto slab_done = [&](size_t ib, uint32_t n) {
     if (lane == 0) {
@@ -2042,7 +2377,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     uint64_t sub_end = last ? we : SIM_START + (S.bw_div.div(ws - SIM_START) + bi + 1) * S.BW;
     // ---- 1. gather the group's runs of bucket b that are due (all but the last bucket's
     //      runs at >= we, which join this round's new runs for it in the spare slab) ----
-    const size_t ib = (size_t)(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
+    const size_t ib = (size_t)uni32(S.NB <= LDS_BSLAB ? lbs[b] : ld_dev(&S.bucket_slab[b])) * S.G + g;
     // the slab's fill and its first GATHER_SPEC records in ONE round trip: the records are
     // loaded before the fill is known (S.gspec <= CAP; slots past the fill are ignored) — nothing
     // appends to a bucket's slab while its window runs (new runs for the window's last
@@ -2067,8 +2402,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       r0 = ld_dev_rec(pb + lane);
       if (pair) r1 = ld_dev_rec(pb1 + lane);
     }
-    const uint32_t nraw = ld_dev(&S.slab_n[ib]);
-    const uint32_t n1raw = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
+    const uint32_t nraw = uni32(ld_dev(&S.slab_n[ib]));
+    const uint32_t n1raw = pair ? uni32(ld_dev(&S.slab_n[ib1])) : 0u;
     // PERIODIC traffic (configs B and D: most executed hosts have their app timer due): the
     // host record of a lane whose local event is due in the window loads in the same round trip
     // as the gather, and the app's next route is prefetched behind the sort
@@ -2078,26 +2413,39 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       ex.prefetch_peer(np);
       loaded = true;
     }
+    // more runs than the LDS holds: the big-slab path (ordered and executed in pieces)
+    const bool big = nraw > S.CAP;
     const uint32_t n = min(nraw, S.CAP);
-    const uint32_t n1 = min(n1raw, S.CAP);
-    // a slab with runs in the spill area: the calendar was not re-laid out before the runs are
-    // due (single shard: impossible, the round edge holds first; multi-shard: a spill by
-    // k_import due within the batch) — reported, never silent
-    if (lane == 0 && (nraw > S.CAP || n1raw > S.CAP) && (atomicOr(&C->overflow, OVF_BUCKET) & OVF_BUCKET) == 0)
-      C->overflow_info = gbase;
-    lcnt[lane] = 0;
     uint32_t N = 0;
-    gather_slab(pb, r0, n, last, N);
-    slab_done(ib, n);
-    // (merged only while the pair fits one 64-run pass: config D's slabs hold ~64 runs each,
-    // and merging them made its longer per-lane rank sorts cost more than the pass saved)
-    if (pair && n + n1 <= min(S.CAP, 64u)) {
-      gather_slab(pb1, r1, n1, true, N);
-      slab_done(ib1, n1);
-      bi = 1;  // the second bucket is done: this is the window's last sub-window
-      last = true;
-      sub_end = we;
+    if (!big) {
+      lcnt[lane] = 0;
+      gather_slab(pb, r0, n, last, N);
+      slab_done(ib, n);
+      // (merged only while the pair fits one 64-run pass: config D's slabs hold ~64 runs each,
+      // and merging them made its longer per-lane rank sorts cost more than the pass saved)
+      if (pair && n + n1raw <= min(S.CAP, 64u)) {
+        gather_slab(pb1, r1, n1raw, true, N);
+        slab_done(ib1, n1raw);
+        bi = 1;  // the second bucket is done: this is the window's last sub-window
+        last = true;
+        sub_end = we;
+      }
     }
+    for (bool first = true;; first = false) {  // pieces (one unless big)
+      uint64_t until = sub_end, tail = INVALID;
+      bool fin = true;
+      if (big) {
+        park();
+        if (first) {
+          big_prepare(ib, pb, nraw, last);
+          slab_done(ib, nraw);
+        }
+        lcnt[lane] = 0;
+        fin = big_piece(ib, pb, nraw, last, N, &tail);
+        if (!fin) until = tail;
+        n_pieces++;
+        if (loaded) ex.load(false);
+      }
     N_all += N;
     __syncthreads();
     // ---- 2. order: counting sort by destination lane, then rank sort by Shadow's key ----
@@ -2133,13 +2481,13 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       lc[a + rank] = (uint16_t)idx;
     }
     sorted += cnt > 1 ? 1u : 0u;
-    if (early) ex.prefetch_route();
+    if (early && !big) ex.prefetch_route();
     __syncthreads();
-    // ---- 3. execute the sub-window [.., sub_end) ----
+    // ---- 3. execute the sub-window [.., sub_end) (a big slab's piece: up to its bound) ----
     const uint64_t c1 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
 #ifdef SGN_DIAG
     // wave-level phase times (the loads are drained inside the load phase here)
-    const bool go = valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end);
+    const bool go = valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < until);
     const uint64_t ta = __builtin_amdgcn_s_memtime();
     if (go && !loaded) {
       ex.load();
@@ -2147,24 +2495,29 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       loaded = true;
     }
     const uint64_t tb = __builtin_amdgcn_s_memtime();
-    if (go) ex.run(lev, lc, start, start + cnt, sub_end);
+    if (go) ex.run(lev, lc, start, start + cnt, until, tail, fin);
     const uint64_t tc = __builtin_amdgcn_s_memtime();
     w_load += tb - ta;
     w_run += tc - tb;
 #else
-    if (valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < sub_end)) {
+    const bool go = valid && (cnt > 0 || (loaded ? ex.next_local_time() : lmin) < until);
+    if (go) {
       if (!loaded) {
         ex.load();
         loaded = true;
       }
-      ex.run(lev, lc, start, start + cnt, sub_end);
+      ex.run(lev, lc, start, start + cnt, until, tail, fin);
     }
 #endif
-    __syncthreads();  // LDS is reused by the next bucket
+    // a big slab's host that ran in an earlier piece closes its digest runs with the last one
+    if (big && fin && !go && loaded) ex.flush_digests();
+    __syncthreads();  // LDS is reused by the next piece or bucket
     if (S.stamps) {
       const uint64_t c2 = __builtin_amdgcn_s_memtime();
       t_gather += c1 - c0;
       t_exec += c2 - c1;
+    }
+      if (fin) break;
     }
   }
 
@@ -2178,7 +2531,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       if (pos < S.CAP)
         st_dev_rec(S.pool + (size_t)idx * S.CAP + pos, ob->rec[i]);
       else
-        spill_run(S, ob, idx, ob->rec[i]);
+        place_overflow(S, ob, idx, pos, ob->rec[i]);
     }
   }
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
@@ -2190,7 +2543,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   *next_out = m;
   // the calendar's occupancy change: runs this group appended minus the due runs it took out
   // (the last bucket's later runs moved to the spare slab set count out and in)
-  const uint64_t occd = (uint64_t)wave_sum_u32(loaded ? ex.c_runs : 0u) - (uint64_t)N_all;
+  const uint64_t occd = (uint64_t)wave_sum_u32((loaded ? ex.c_runs : 0u) + pk_runs) - (uint64_t)N_all;
   at_end(kmin, m, occd);
   uint32_t n_ev = 0;
 #ifdef SGN_DIAG
@@ -2247,9 +2600,9 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   // ---- 4. hosts that ran (roofline accounting): per-wave counters, no-return adds ----
   const uint64_t ex_mask = __ballot(loaded);
   const uint32_t n_sorted = wave_sum_u32(sorted);
-  const uint32_t w_loss = wave_sum_u32(loaded ? ex.c_loss : 0u);
-  const uint32_t w_lev = wave_sum_u32(loaded ? ex.c_localev : 0u);
-  uint64_t w_bytes = loaded ? ex.c_bytes : 0;
+  const uint32_t w_loss = wave_sum_u32((loaded ? ex.c_loss : 0u) + pk_loss);
+  const uint32_t w_lev = wave_sum_u32((loaded ? ex.c_localev : 0u) + pk_lev);
+  uint64_t w_bytes = (loaded ? ex.c_bytes : 0) + pk_bytes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) w_bytes += shfl_xor64(w_bytes, off);
   if (lane == 0) {
@@ -2260,6 +2613,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     if (w_loss) cnt_add(&S.w_cnt[W_LOSS * G + g], w_loss);
     if (w_lev) cnt_add(&S.w_cnt[W_LOCAL_EV * G + g], w_lev);
     if (w_bytes) cnt_add(&S.w_cnt[W_BYTES * G + g], w_bytes);
+    if (n_pieces) cnt_add(&S.w_cnt[W_BIG * G + g], n_pieces);
   }
 }
 
@@ -2269,16 +2623,18 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   __shared__ LaneLDS<kApp> lslot_[64];                                               \
   __shared__ uint16_t lbs_[LDS_BSLAB];                                               \
   __shared__ Outbox<kApp> ob_;                                                       \
+  __shared__ BigLDS big_;                                                            \
   ExecLDS X;                                                                         \
   X.lev = (EvRec*)lds_dyn;                                                           \
   X.lb = (uint16_t*)(X.lev + S.CAP);                                                 \
   X.lc = X.lb + ((S.CAP + 3) & ~3u);                                                 \
-  X.bmin = S.agg_bmin ? (uint32_t*)(X.lc + ((S.CAP + 3) & ~3u)) : nullptr;           \
+  X.bmin = S.agg_bmin ? (uint32_t*)(lds_dyn + exec_lds_runs_bytes(S.CAP)) : nullptr;  \
   X.lcnt = lcnt_;                                                                    \
   X.lcur = lcur_;                                                                    \
   X.lslot = lslot_;                                                                  \
   X.lbs = lbs_;                                                                      \
   X.ob = &ob_;                                                                       \
+  X.big = &big_;                                                                     \
   if (threadIdx.x == 0) ob_.bmin = X.bmin;
 
 // The workgroup's LDS table of bucket minima (S.agg_bmin): its sends of the round fold their
@@ -2574,8 +2930,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     rs.pg_alloc = ld_dev(&C->pg_alloc);
     rs.occ = ld_dev(&C->cal_occ);
     rs.nspill = ld_dev(&C->spill_n);
-    rs.hold = 0;
-    rs.hold_need = 0;
+    rs.hold = ld_dev(&C->hold);  // (a round still held: the launch returns at once)
+    rs.hold_need = ld_dev(&C->hold_need);
   }
   const uint64_t rounds0 = ld_dev(&C->rounds);
   const bool lds_tab = S.NB <= LDS_BSLAB;
@@ -2583,10 +2939,6 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
   init_bmin<kApp>(S, X);
   __syncthreads();
-  auto uni64 = [](uint64_t v) -> uint64_t {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  };
   uint32_t r = 0;
   for (; r < max_rounds; r++) {
     // (a held round: the host grows a pool between launches, then the round runs)
@@ -2814,8 +3166,9 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
       atomicMin((unsigned long long*)&S.bucket_min[b], (unsigned long long)e.time);
       if (pos < S.CAP)
         S.pool[idx * S.CAP + pos] = e;
-      else
-        spill_run(S, nullptr, (uint32_t)idx, e);  // re-laid out at the batch's host sync
+      else  // the extension, or the spill area: the next round's gather reads it (lossless), and
+            // the spill flag holds the round after that on every shard for the re-layout
+        place_overflow(S, nullptr, (uint32_t)idx, pos, e);
       filed++;
     }
   }
@@ -2831,6 +3184,8 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   __syncthreads();
   if (!last || threadIdx.x != 0) return;
   C->imp_done = 0;
+  // the spill-area entries the next round's gathers scan for runs imported past their slab
+  C->spill_imp = ld_dev(&S.ctrl->spill_n);
   if (gm > C->xhwm) C->xhwm = gm;
   if (hold) {
     C->xspill = 1;
@@ -2849,7 +3204,8 @@ __global__ __launch_bounds__(256) void k_import(DevSim S) {
   uint64_t own = 0;
   for (uint32_t q = 0; q < S.n_ranks; q++) {
     const uint64_t* msg = (const uint64_t*)(S.xin + (size_t)q * (S.xslot + XHDR));
-    const uint64_t occ = msg[5] + xs, capb = (uint64_t)nbk * msg[7];
+    // (msg[7]: the shard's runs per bucket, extensions included; imported runs may go past it)
+    const uint64_t occ = msg[5] + xs, capb = (uint64_t)nbk * msg[7] + xs;
     const uint64_t need = codel_pages_bound(occ < capb ? occ : capb, S.rank_lo[q + 1] - S.rank_lo[q]);
     if (msg[4] < need) hflags |= HOLD_CODEL;
     if ((msg[3] >> 32) & 1) hflags |= HOLD_SPILL;
@@ -2884,30 +3240,53 @@ __global__ void k_inject(const DevSim* Sp, const EvRec* recs, uint32_t n) {
   if (pos < S.CAP)
     S.pool[idx * S.CAP + pos] = r;
   else
-    spill_run(S, nullptr, (uint32_t)idx, r);  // sgn_submit re-lays the calendar out right after
+    place_overflow(S, nullptr, (uint32_t)idx, pos, r);  // (a spill: sgn_submit re-lays out right after)
 }
 
-// Calendar re-layout (a held round edge after a spill): every slab's runs into a pool of
-// larger slabs, then the spilled runs after them. Order inside a slab is free (the gather
-// sorts by Shadow's key); slab_n already counts every run of a slab, spilled ones included.
-__global__ void k_relayout(const EvRec* __restrict__ old_pool, uint32_t old_cap, EvRec* __restrict__ pool,
-                           uint32_t cap, const uint32_t* __restrict__ slab_n, uint32_t* cursor, uint64_t n_slabs) {
+// Calendar re-layout (a held round edge after a spill, or sgn_submit): every slab's runs into
+// the new layout — slabs of cap runs, and extensions (ext: offset | capacity << 40) for the hot
+// ones — then the spilled runs after them. Order inside a slab is free (the gather sorts by
+// Shadow's key); slab_n already counts every run of a slab, spilled ones included.
+__device__ __forceinline__ EvRec* relayout_dst(EvRec* pool, uint32_t cap, const uint64_t* ext, EvRec* ext_pool,
+                                               uint64_t idx, uint32_t j) {
+  return j < cap ? pool + idx * cap + j : ext_pool + (ext[idx] & EXT_OFF_MASK) + (j - cap);
+}
+// the pool part of every slab (thread = (slab, position)); sets each slab's respill cursor
+__global__ void k_relayout(const EvRec* __restrict__ old_pool, uint32_t old_cap, const uint64_t* __restrict__ old_ext,
+                           EvRec* pool, uint32_t cap, const uint64_t* __restrict__ ext, EvRec* ext_pool,
+                           const uint32_t* __restrict__ slab_n, uint32_t* cursor, uint64_t n_slabs) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t idx = t / old_cap;
   const uint32_t j = (uint32_t)(t % old_cap);
   if (idx >= n_slabs) return;
-  const uint32_t n = min(slab_n[idx], old_cap);
-  if (j < n) pool[idx * cap + j] = old_pool[idx * old_cap + j];
-  if (j == 0) cursor[idx] = n;
+  const uint32_t fill = slab_n[idx];
+  if (j < min(fill, old_cap)) *relayout_dst(pool, cap, ext, ext_pool, idx, j) = old_pool[idx * old_cap + j];
+  if (j == 0) cursor[idx] = min(fill, old_cap + (old_ext ? (uint32_t)(old_ext[idx] >> 40) : 0u));
+}
+// the old extensions' runs (thread = (hot slab k of the list, position))
+__global__ void k_relayout_ext(const uint64_t* __restrict__ hot, uint64_t n_hot, uint32_t max_ecap,
+                               const EvRec* __restrict__ old_ext_pool, const uint64_t* __restrict__ old_ext,
+                               uint32_t old_cap, EvRec* pool, uint32_t cap, const uint64_t* __restrict__ ext,
+                               EvRec* ext_pool, const uint32_t* __restrict__ slab_n) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t k = t / max_ecap;
+  const uint32_t j = (uint32_t)(t % max_ecap);
+  if (k >= n_hot) return;
+  const uint64_t idx = hot[k], x = old_ext[idx];
+  const uint32_t fill = slab_n[idx];
+  if (j < (uint32_t)(x >> 40) && old_cap + j < fill)
+    *relayout_dst(pool, cap, ext, ext_pool, idx, old_cap + j) = old_ext_pool[(x & EXT_OFF_MASK) + j];
 }
 __global__ void k_respill(const EvRec* __restrict__ spill, const uint32_t* __restrict__ spill_idx, uint64_t n,
-                          EvRec* __restrict__ pool, uint32_t cap, uint32_t* cursor) {
+                          EvRec* pool, uint32_t cap, const uint64_t* __restrict__ ext, EvRec* ext_pool,
+                          uint32_t* cursor) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t idx = spill_idx[i];
-  if (idx & SPILL_PEER) return;  // a run for another shard (grow_exchange_slot)
+  if (idx & SPILL_PEER) return;  // a run for another shard (grow_exchange_slot), or one a gather took
   const uint32_t pos = atomicAdd(&cursor[idx], 1u);
-  if (pos < cap) pool[(size_t)idx * cap + pos] = spill[i];
+  const uint32_t room = cap + (ext ? (uint32_t)(ext[idx] >> 40) : 0u);
+  if (pos < room) *relayout_dst(pool, cap, ext, ext_pool, idx, pos) = spill[i];
 }
 
 // sgn_rng_*: draws of host Xoshiro256++ streams (the state stays on the device). One thread
@@ -2971,9 +3350,11 @@ __global__ void k_next_packet(const DevSim* Sp, uint32_t lo, uint32_t n, uint32_
   const uint32_t w = blockIdx.x;  // (bucket, group) pair
   const uint32_t b = w / ng, g = g0 + w % ng;
   const size_t idx = (size_t)S.bucket_slab[b] * S.G + g;
-  const uint32_t fill = min(S.slab_n[idx], S.CAP);
-  for (uint32_t j = threadIdx.x; j < fill; j += blockDim.x) {
-    const EvRec& e = S.pool[idx * S.CAP + j];
+  const uint32_t fill = S.slab_n[idx];
+  const uint64_t x = S.ext && fill > S.CAP ? S.ext[idx] : 0ULL;
+  const uint32_t np = min(fill, S.CAP), ne = min(fill - np, (uint32_t)(x >> 40));
+  for (uint32_t j = threadIdx.x; j < np + ne; j += blockDim.x) {
+    const EvRec& e = j < np ? S.pool[idx * S.CAP + j] : S.ext_pool[(x & EXT_OFF_MASK) + j - np];
     const uint32_t d = S.host_of[e.dst - S.lo];
     if (d >= lo && d < lo + n) atomicMin((unsigned long long*)&out[d - lo], (unsigned long long)e.time);
   }
@@ -3010,7 +3391,7 @@ int launch_round(sgn_ctx* ctx);
 // (the u16 index arrays are padded to 8 bytes so the optional bucket-minimum table that
 // follows them is aligned)
 inline size_t exec_lds_bytes(uint32_t cap, uint32_t agg_nb = 0) {
-  return (size_t)cap * sizeof(EvRec) + 2 * (size_t)((cap + 3) & ~3u) * 2 + (agg_nb ? (size_t)(agg_nb + 1) * 4 : 0);
+  return exec_lds_runs_bytes(cap) + (agg_nb ? (size_t)(agg_nb + 1) * 4 : 0);
 }
 constexpr uint32_t kPersistRounds = 128;  // rounds per persistent launch (then a host sync)
 constexpr uint64_t kTimeEvery = 8;        // per-round launches: one timed in kTimeEvery
@@ -3122,6 +3503,8 @@ uint32_t max_slab_capacity(sgn_ctx* ctx, const DevSim& S) {
   }
   uint32_t cap = CAP_MIN;
   while (cap < (1u << 15) && st + exec_lds_bytes(cap * 2, S.NB) <= (size_t)per_block) cap *= 2;
+  // test hook: a lower limit, so that hot slabs take extensions and the big-slab path at small sizes
+  if (const char* e = getenv("SGN_SLAB_LIM")) cap = std::max<uint32_t>(16, std::min<uint32_t>(cap, (uint32_t)atoi(e)));
   return cap;
 }
 
@@ -3178,6 +3561,7 @@ int check_overflow(sgn_ctx* ctx) {
 }
 
 int sync_ctrl(sgn_ctx* ctx) {
+  if (!ctx->failed.empty()) return set_error(ctx, SGN_ESTATE, "simulation unusable: " + ctx->failed);
   SGN_HIP(ctx, hipMemcpyAsync(ctx->h_ctrl, ctx->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost,
                               ctx->stream));
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -3192,49 +3576,142 @@ int upload_sim(sgn_ctx* ctx) {
   return 0;
 }
 
-// The calendar with larger slabs: the fullest slab (spilled runs counted) plus a quarter,
-// within what one workgroup's LDS holds; the spill area is emptied into it.
+// The calendar re-laid out after runs went past their slabs (a held round edge, or sgn_submit).
+// The slab capacity CAP doubles while more than 1/256 of the slabs (and more than 16) would
+// still overflow, up to what one workgroup's LDS orders at once; the few hot slabs past it get
+// extensions of 1.5x their fill (a slab keeps the capacity it had). Every run moves into the
+// new layout, the spilled runs after them; the spill area empties, and grows when it was more
+// than a quarter full. Device memory grows with the hot slabs only (sizing every
+// slab for the fullest cost config D ~8 -> ~16 GB for one hot slab).
 int relayout_calendar(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
+  Ctrl& c = *ctx->h_ctrl;
   const uint64_t n_slabs = (uint64_t)(S.NB + 1) * S.G;
-  const uint64_t nsp = std::min<uint64_t>(ctx->h_ctrl->spill_n, S.spill_cap);
-  if (ctx->h_ctrl->spill_n > S.spill_cap)
+  if (c.spill_n > S.spill_cap)
     return set_error(ctx, SGN_EOVERFLOW, "calendar spill area exhausted within one round (" +
-                                             std::to_string(ctx->h_ctrl->spill_n) + " runs)");
+                                             std::to_string(c.spill_n) + " runs, capacity " +
+                                             std::to_string(S.spill_cap) + ")");
+  const uint64_t nsp = c.spill_n;
   std::vector<uint32_t> fill(n_slabs);
   SGN_HIP(ctx, hipMemcpy(fill.data(), (const void*)S.slab_n, n_slabs * 4, hipMemcpyDeviceToHost));
-  const uint32_t mx = *std::max_element(fill.begin(), fill.end());
-  const uint32_t lim = max_slab_capacity(ctx, S);
+  const std::vector<uint64_t>& oext = ctx->h_ext;  // (empty: no extensions yet)
+  auto oecap = [&](uint64_t i) -> uint64_t { return oext.empty() ? 0 : oext[i] >> 40; };
+  // the new slab capacity
+  const uint32_t lim = std::max(S.CAP, max_slab_capacity(ctx, S));
+  const uint64_t few = std::max<uint64_t>(16, n_slabs / 256);
   uint32_t cap = S.CAP;
-  while (cap < mx + mx / 4 && cap < lim) cap *= 2;
-  cap = std::min(cap, lim);
-  if (cap < mx)
-    return set_error(ctx, SGN_EOVERFLOW, "calendar slab needs " + std::to_string(mx) +
-                                             " runs; one workgroup's LDS holds " + std::to_string(lim) +
-                                             " (raise the bucket width: runahead)");
-  if (cap > S.CAP) {
-    EvRec* np = (EvRec*)dev_alloc(ctx, n_slabs * cap * sizeof(EvRec), false);
+  size_t mfree = 0, mtot = 0;
+  if (hipMemGetInfo(&mfree, &mtot) != hipSuccess) mfree = 0;
+  while (cap * 2 <= lim && n_slabs * cap * 2 * sizeof(EvRec) < mfree / 2) {
+    uint64_t over = 0;
+    for (uint64_t i = 0; i < n_slabs; i++) over += fill[i] > cap;
+    if (over <= few) break;
+    cap *= 2;
+  }
+  // extensions: hot slabs keep room for 1.5x their fill, and never less than they had
+  std::vector<uint64_t> next(n_slabs, 0), hot_old;
+  uint64_t etot = 0, nhot = 0, max_oecap = 0;
+  for (uint64_t i = 0; i < n_slabs; i++) {
+    const uint64_t had = oecap(i) ? S.CAP + oecap(i) : 0;
+    if (oecap(i)) {
+      hot_old.push_back(i);
+      max_oecap = std::max(max_oecap, oecap(i));
+    }
+    const uint64_t need = std::max<uint64_t>(fill[i], had);
+    if (need <= cap) continue;
+    const uint64_t e = ((need + need / 2 - cap) + 63) / 64 * 64;
+    if (e >= (1ULL << 24))
+      return set_error(ctx, SGN_EOVERFLOW, "a calendar slab above 2^24 runs (slab " + std::to_string(i) + ", fill " +
+                                               std::to_string(fill[i]) + ", had " + std::to_string(had) + ", cap " +
+                                               std::to_string(S.CAP) + " -> " + std::to_string(cap) + ")");
+    next[i] = etot | (e << 40);
+    etot += e;
+    nhot++;
+  }
+  if (etot >= (1ULL << 40)) return set_error(ctx, SGN_EOVERFLOW, "calendar extensions above 2^40 runs");
+  const bool changed = cap != S.CAP || next != (oext.empty() ? std::vector<uint64_t>(n_slabs, 0) : oext);
+  if (changed) {
+    EvRec* np = cap != S.CAP ? (EvRec*)dev_alloc(ctx, n_slabs * cap * sizeof(EvRec), false) : (EvRec*)S.pool;
+    EvRec* nep = etot ? (EvRec*)dev_alloc(ctx, etot * sizeof(EvRec), false) : nullptr;
+    uint64_t* nxt = etot ? (uint64_t*)dev_alloc(ctx, n_slabs * 8, false) : nullptr;
     uint32_t* cur = (uint32_t*)dev_alloc(ctx, n_slabs * 4, false);
-    if (!np || !cur) return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar re-layout)");
+    uint64_t* dhot = hot_old.empty() ? nullptr : (uint64_t*)dev_alloc(ctx, hot_old.size() * 8, false);
+    auto undo = [&]() {
+      if (np && np != (EvRec*)S.pool) dev_free(ctx, np, n_slabs * cap * sizeof(EvRec));
+      if (nep) dev_free(ctx, nep, etot * sizeof(EvRec));
+      if (nxt) dev_free(ctx, nxt, n_slabs * 8);
+      if (cur) dev_free(ctx, cur, n_slabs * 4);
+      if (dhot) dev_free(ctx, dhot, hot_old.size() * 8);
+    };
+    if (!np || (etot && (!nep || !nxt)) || !cur || (!hot_old.empty() && !dhot)) {
+      undo();
+      return set_error(ctx, SGN_ENOMEM, "device allocation failed (calendar re-layout)");
+    }
+    if (nxt) SGN_HIP(ctx, hipMemcpy(nxt, next.data(), n_slabs * 8, hipMemcpyHostToDevice));
+    if (dhot) SGN_HIP(ctx, hipMemcpy(dhot, hot_old.data(), hot_old.size() * 8, hipMemcpyHostToDevice));
+    // the pool part moves only when the slabs grow (in place it stays where it is)
     const uint64_t nt = n_slabs * S.CAP;
-    hipLaunchKernelGGL(k_relayout, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, ctx->stream,
-                       (const EvRec*)S.pool, S.CAP, np, cap, (const uint32_t*)S.slab_n, cur, n_slabs);
+    if (np != (EvRec*)S.pool) {
+      hipLaunchKernelGGL(k_relayout, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, ctx->stream,
+                         (const EvRec*)S.pool, S.CAP, (const uint64_t*)S.ext, np, cap, (const uint64_t*)nxt, nep,
+                         (const uint32_t*)S.slab_n, cur, n_slabs);
+    } else {
+      std::vector<uint32_t> hc(n_slabs);
+      for (uint64_t i = 0; i < n_slabs; i++) hc[i] = (uint32_t)std::min<uint64_t>(fill[i], S.CAP + oecap(i));
+      SGN_HIP(ctx, hipMemcpy(cur, hc.data(), n_slabs * 4, hipMemcpyHostToDevice));
+    }
+    if (!hot_old.empty()) {
+      const uint64_t ne = hot_old.size() * max_oecap;
+      hipLaunchKernelGGL(k_relayout_ext, dim3((uint32_t)((ne + 255) / 256)), dim3(256), 0, ctx->stream,
+                         (const uint64_t*)dhot, (uint64_t)hot_old.size(), (uint32_t)max_oecap,
+                         (const EvRec*)S.ext_pool, (const uint64_t*)S.ext, S.CAP, np, cap, (const uint64_t*)nxt, nep,
+                         (const uint32_t*)S.slab_n);
+    }
     if (nsp)
       hipLaunchKernelGGL(k_respill, dim3((uint32_t)((nsp + 255) / 256)), dim3(256), 0, ctx->stream,
-                         (const EvRec*)S.spill, (const uint32_t*)S.spill_idx, nsp, np, cap, cur);
+                         (const EvRec*)S.spill, (const uint32_t*)S.spill_idx, nsp, np, cap, (const uint64_t*)nxt,
+                         nep, cur);
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    dev_free(ctx, (void*)S.pool, n_slabs * S.CAP * sizeof(EvRec));
+    if (np != (EvRec*)S.pool) dev_free(ctx, (void*)S.pool, n_slabs * S.CAP * sizeof(EvRec));
+    if (S.ext_pool) dev_free(ctx, (void*)S.ext_pool, S.ext_total * sizeof(EvRec));
+    if (S.ext) dev_free(ctx, (void*)S.ext, n_slabs * 8);
     dev_free(ctx, cur, n_slabs * 4);
+    if (dhot) dev_free(ctx, dhot, hot_old.size() * 8);
+    if (cap != S.CAP) ctx->cal_grows++;
     S.pool = (decltype(S.pool))np;
     S.CAP = cap;
+    S.ext = (decltype(S.ext))nxt;
+    S.ext_pool = (decltype(S.ext_pool))nep;
+    S.ext_total = etot;
+    ctx->h_ext = etot ? next : std::vector<uint64_t>();
+    ctx->ext_slabs = nhot;
+    S.gspec = std::min<uint32_t>(S.gspec, S.CAP);
     size_round_kernels(ctx, S);
-    ctx->cal_grows++;
   }
   ctx->cal_spill_runs += nsp;
-  const uint64_t zero = 0;
-  SGN_HIP(ctx, hipMemcpy((char*)S.ctrl + offsetof(Ctrl, spill_n), &zero, 8, hipMemcpyHostToDevice));
-  ctx->h_ctrl->spill_n = 0;
+  // the spill area: emptied; grown when this round used more than a quarter of it
+  if (nsp > S.spill_cap / 4) {
+    const uint64_t ncap = std::min<uint64_t>(1ULL << 30, std::max<uint64_t>(2 * S.spill_cap, 4 * nsp));
+    EvRec* sp = (EvRec*)dev_alloc(ctx, ncap * sizeof(EvRec), false);
+    uint32_t* si = (uint32_t*)dev_alloc(ctx, ncap * 4, false);
+    if (sp && si) {
+      dev_free(ctx, (void*)S.spill, S.spill_cap * sizeof(EvRec));
+      dev_free(ctx, (void*)S.spill_idx, S.spill_cap * 4);
+      S.spill = (decltype(S.spill))sp;
+      S.spill_idx = (decltype(S.spill_idx))si;
+      S.spill_cap = ncap;
+      ctx->spill_grows++;
+    } else {  // (the area as it was still works)
+      if (sp) dev_free(ctx, sp, ncap * sizeof(EvRec));
+      if (si) dev_free(ctx, si, ncap * 4);
+    }
+  }
+  const uint64_t zero[2] = {0, 0};
+  SGN_HIP(ctx, hipMemcpy((char*)S.ctrl + offsetof(Ctrl, spill_n), zero, 8, hipMemcpyHostToDevice));
+  SGN_HIP(ctx, hipMemcpy((char*)S.ctrl + offsetof(Ctrl, spill_imp), zero, 8, hipMemcpyHostToDevice));
+  c.spill_n = 0;
+  c.spill_imp = 0;
   return upload_sim(ctx);
 }
 
@@ -3245,7 +3722,7 @@ uint64_t codel_need_host(const sgn_ctx* ctx) {
   if (!c.active || c.we <= c.ws) return 0;
   auto bk = [&](uint64_t t) { return (uint32_t)((t - SIM_START) / S.BW) & (S.NB - 1); };
   const uint64_t nbk = ((bk(c.we - 1) - bk(c.ws)) & (S.NB - 1)) + 1;
-  return codel_pages_bound(std::min<uint64_t>(c.cal_occ, nbk * S.G * S.CAP), S.nH);
+  return codel_pages_bound(std::min<uint64_t>(c.cal_occ, nbk * S.G * S.CAP + S.ext_total), S.nH);
 }
 
 // A CoDel page pool with at least `extra` more free pages (and at least double the size): the
@@ -3316,7 +3793,7 @@ int grow_exchange_slot_impl(sgn_ctx* ctx) {
     SGN_HIP(ctx, hipMemcpy(rec.data(), (const void*)S.spill, n * sizeof(EvRec), hipMemcpyDeviceToHost));
     std::vector<std::vector<EvRec>> per(R);
     for (uint64_t i = 0; i < n; i++)
-      if (idx[i] & SPILL_PEER) per[idx[i] & ~SPILL_PEER].push_back(rec[i]);
+      if ((idx[i] & SPILL_PEER) && idx[i] != SPILL_DEAD) per[idx[i] & ~SPILL_PEER].push_back(rec[i]);
     for (size_t p = 0; p < R; p++)
       if (!per[p].empty())
         SGN_HIP(ctx, hipMemcpy(nxo + p * nb + ob, per[p].data(), per[p].size() * sizeof(EvRec), hipMemcpyHostToDevice));
@@ -3343,8 +3820,10 @@ int resolve_hold(sgn_ctx* ctx) {
   }
   int rc = 0;
   if (c.spill_n && (rc = relayout_calendar(ctx))) return rc;
+  // (the bound again for the layout as it is now: spilled runs may be due in the held round)
+  const uint64_t need = std::max(c.hold_need, codel_need_host(ctx));
   const uint64_t free = c.pg_avail > c.pg_alloc ? c.pg_avail - c.pg_alloc : 0;
-  if (free < c.hold_need && (rc = grow_codel(ctx, c.hold_need - free))) return rc;
+  if (free < need && (rc = grow_codel(ctx, need - free))) return rc;
   ctx->rounds_held++;
   c.hold = 0;
   c.hold_need = 0;
@@ -3522,6 +4001,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   ctx->persist_off = false;
   ctx->codel_grows = ctx->cal_grows = ctx->cal_spill_runs = ctx->xslot_grows = ctx->rounds_held = 0;
   ctx->codel_allocs_before = 0;
+  ctx->ext_slabs = ctx->spill_grows = 0;
+  ctx->h_ext.clear();
+  ctx->failed.clear();
   S.n_all = N;
   S.lo = ctx->lo;
   S.nH = nH;
@@ -3885,6 +4367,7 @@ int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
   if (!ctx->h_ctrl->active) return set_error(ctx, SGN_ESTATE, "simulation already finished");
+  if (ctx->h_ctrl->hold && (rc = resolve_hold(ctx))) return rc;  // (an earlier growth failed)
   if ((rc = launch_round(ctx))) return rc;
   rc = sync_ctrl(ctx);
   if (!rc && ctx->h_ctrl->xspill) rc = comm_complete_spill(ctx);
@@ -3900,6 +4383,8 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_run");
   int rc = sync_ctrl(ctx);
   if (rc) return rc;
+  // a round still held (an earlier pool growth failed and the caller runs again): grow first
+  if ((ctx->h_ctrl->hold || ctx->h_ctrl->spill_n) && (rc = resolve_hold(ctx))) return rc;
   const uint64_t r_start = ctx->h_ctrl->rounds;
   uint64_t enq = 0;
   // Rounds are enqueued in batches with one host synchronisation per batch (the window
@@ -4182,6 +4667,18 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   out->calendar_spill_runs = ctx->cal_spill_runs;
   out->exchange_slot_grows = ctx->xslot_grows;
   out->rounds_held = ctx->rounds_held;
+  out->slab_extensions = ctx->ext_slabs;
+  out->slab_extension_runs = ctx->S.ext_total;
+  {
+    const size_t G = ctx->S.G;
+    std::vector<uint64_t> wb(G);
+    SGN_HIP(ctx, hipMemcpy(wb.data(), (const void*)(ctx->S.w_cnt + W_BIG * G), G * 8, hipMemcpyDeviceToHost));
+    uint64_t t = 0;
+    for (uint64_t v : wb) t += v;
+    out->big_slab_pieces = t;
+  }
+  out->spill_area_runs = ctx->S.spill_cap;
+  out->spill_area_grows = ctx->spill_grows;
   return 0;
 }
 
@@ -4299,8 +4796,14 @@ int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
   hipLaunchKernelGGL(k_inject, dim3((uint32_t)((b->n + 255) / 256)), dim3(256), 0, ctx->stream,
                      (const DevSim*)ctx->d_S, (const EvRec*)ctx->d_stage, (uint32_t)b->n);
   SGN_HIP(ctx, hipGetLastError());
-  if ((rc = sync_ctrl(ctx))) return rc;
-  if (ctx->h_ctrl->spill_n && (rc = relayout_calendar(ctx))) return rc;
+  // the runs are in the device calendar from here: a failure past this point leaves them there
+  // with no handle, so the context is marked unusable (a retry would file them twice)
+  rc = sync_ctrl(ctx);
+  if (!rc && ctx->h_ctrl->spill_n) rc = relayout_calendar(ctx);
+  if (rc) {
+    ctx->failed = std::string("sgn_submit failed after filing its runs: ") + sgn_last_error(ctx);
+    return rc;
+  }
   for (uint64_t i = 0; i < b->n; i++) ctx->handles.push_back(b->handle ? b->handle[i] : 0);
   ctx->submit_seq.swap(seq);
   return 0;

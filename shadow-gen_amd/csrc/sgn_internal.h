@@ -105,7 +105,8 @@ struct Ctrl {
   uint64_t rounds;
   uint64_t max_bucket;    // high-water mark of any (bucket, host group) slab fill
   uint64_t trace_n;       // trace records produced
-  uint64_t pad1;
+  uint64_t spill_imp;     // multi-shard: spill-area entries written by the last k_import (read by
+                          // the next round's gathers: runs imported past their slab, lossless)
   uint64_t epoch;         // persistent rounds: round edges published (grid barrier)
   uint64_t prev_we;       // end of the last executed window (sgn_set_window's lower bound)
   uint64_t drain_n;       // drain records produced since the last sgn_drain
@@ -195,7 +196,8 @@ static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
 
 // per-wave counters (DevSim::w_cnt rows of G)
-enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_MAXFILL, W_N };  // W_MAXFILL: max, not sum
+enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_MAXFILL, W_BIG, W_N };  // W_MAXFILL: max, not sum
+                                                                                            // W_BIG: big-slab pieces
 
 // host flag bits
 enum : uint32_t {
@@ -324,6 +326,13 @@ struct DevSim {
   SGN_GLB EvRec* spill;           // [spill_cap]
   SGN_GLB uint32_t* spill_idx;    // [spill_cap] (slab set, group) index of each spilled run
   uint64_t spill_cap;
+  // slab extensions (a hot slab: thousands of sources sending to one host group in one bucket
+  // width): runs past a slab's CAP continue in its extension, ext[slab] = offset into ext_pool
+  // | capacity << 40 (0: none), laid out by the host at a held round edge (relayout_calendar).
+  // A slab with more runs than the LDS holds is ordered in pieces (exec_group's big-slab path).
+  SGN_GLB const uint64_t* ext;    // [(NB + 1) * G] or null (no slab has an extension)
+  SGN_GLB EvRec* ext_pool;
+  uint64_t ext_total;             // runs in all extensions (the CoDel guard's due-run bound)
   uint32_t NB, G;         // NB: a power of two (bucket index = (t / BW) & (NB - 1))
   uint32_t CAP;
   uint32_t gsh;           // log2(hosts per group); a group is served by one 64-lane wave
@@ -371,6 +380,8 @@ struct DevSim {
 };
 
 constexpr uint32_t SPILL_PEER = 0x80000000u;  // spill area tag: a run for that peer shard's exchange slot
+constexpr uint32_t SPILL_DEAD = 0xFFFFFFFFu;  // spill area tag: a run a gather already took (multi-shard)
+constexpr uint64_t EXT_OFF_MASK = (1ULL << 40) - 1;  // DevSim::ext: offset bits (capacity above)
 constexpr uint32_t XHDR = 2;  // multi-shard: message records (64 B) at the head of a peer's block
 constexpr uint32_t GROUP_MAX = 64;  // hosts per group <= lanes of one k_execute wave
 // event runs per (bucket, group) slab: one bucket's due runs of a group are ordered in LDS
@@ -485,6 +496,9 @@ struct sgn_ctx {
   uint32_t lds_per_cu = 0;         // LDS bytes per CU (device attribute; the residency model)
   // pool growth (a held round, then a larger pool): counts for sgn_engine_info
   uint64_t codel_grows = 0, cal_grows = 0, cal_spill_runs = 0, xslot_grows = 0, rounds_held = 0;
+  uint64_t ext_slabs = 0, spill_grows = 0;  // slabs with an extension; spill-area growths
+  std::vector<uint64_t> h_ext;              // host mirror of DevSim::ext (empty: none)
+  std::string failed;  // sticky: an operation left the device state unusable (every call fails)
   uint64_t codel_allocs_before = 0;  // page allocations before the last pool growth (its ring restarts)
   bool capturing = false;
 

@@ -178,7 +178,8 @@ class EngineInfo(C.Structure):
         "exchange_send_runs", "exchange_hwm_runs", "exchange_spills", "exchange_bytes", "codel_pages",
         "codel_page_allocs", "codel_pages_free", "codel_pages_chained",
         "compute_units", "bucket_min_lds", "lds_per_cu", "codel_pool_grows", "calendar_grows",
-        "calendar_spill_runs", "exchange_slot_grows", "rounds_held")]
+        "calendar_spill_runs", "exchange_slot_grows", "rounds_held", "slab_extensions",
+        "slab_extension_runs", "big_slab_pieces", "spill_area_runs", "spill_area_grows")]
 
 
 class KernelTimes(C.Structure):

@@ -130,3 +130,96 @@ def test_bandwidths_beyond_32bit_increments(ctxf, oracle):
         o, c = run_both(ctxf, oracle, tuple(args), trace=True)
         assert c.stats()["rounds"] > 0
         assert_same_run(o, c, n, trace=True)
+
+
+# ---- hot slabs: fan-in beyond one slab and beyond one workgroup's LDS (a10) ----
+def _hot_args(n, V=2, servers=4, stop_ns=300_000_000, think=1_000_000_000, seed=1):
+    """Every client fetches a one-packet file from one of `servers` TGEN servers (HostIds
+    0..servers-1: slots put servers first, so all of them share host group 0) at the same
+    instant: the requests land in the servers' (bucket, group) slabs, ~n / V runs each — the
+    fan-in the reference's unbounded per-host BinaryHeap takes (core/work/event_queue.rs:12,
+    57-66; pushes from any thread, core/worker.rs:603-613)."""
+    g = sgn.tor_graph(V, seed=3)
+    used = np.arange(V)
+    names = sgn.host_names(n)
+    hosts = sgn.HostArrays(sgn.assign_ips(n), (np.arange(n) * 7) % V, np.full(n, 1_000_000_000, np.uint64),
+                           np.full(n, 1_000_000_000, np.uint64), sgn.derive_seeds(seed, names))
+    cfg = sgn.make_config(stop_ns, event_capacity=1 << 20, codel_cap=64)
+    tr = sgn.make_traffic(sgn.TRAFFIC_TGEN, period_ns=think, period_jitter_ns=think, start_jitter_ns=0,
+                          servers=np.arange(servers), file_bytes=(1000, 1400, 1400))
+    return g, used, hosts, cfg, tr
+
+
+@pytest.mark.parametrize("persistent,trace", [("1", False), ("0", False), ("0", True)])
+def test_hot_slab_extension_and_pieces(ctxf, oracle, monkeypatch, persistent, trace):
+    """16-run slabs that may grow to 32 (test hooks): ~600 request runs per (bucket, server
+    group) slab spill, the re-layout gives the hot slabs extensions, and their gathers order the
+    runs in pieces of at most 32 (radix-selected bounds on Shadow's key) — bit-exact, per packet
+    when traced."""
+    monkeypatch.setenv("SGN_PERSISTENT", persistent)
+    monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    monkeypatch.setenv("SGN_SLAB_LIM", "32")
+    n = 1200
+    args = _hot_args(n)
+    o, c = run_both(ctxf, oracle, args, trace=trace)
+    info, st = c.engine_info(), c.stats()
+    assert info["slab_extensions"] >= 1 and info["slab_extension_runs"] > 0, info
+    assert info["big_slab_pieces"] > 10 and info["slab_capacity"] <= 32, info
+    assert st["max_pending_events"] > 500, st
+    assert (info["persistent_grid"] > 0) == (persistent == "1" and not trace), info
+    assert_same_run(o, c, n, trace=trace)
+
+
+def test_hot_slab_beyond_lds(ctxf, oracle):
+    """No hooks: 12 k clients hit 4 servers at once, ~6 k request runs per (bucket, group) slab
+    — more than one workgroup's LDS orders (sgn_engine_info.slab_capacity stays at the default
+    since few slabs overflow). Persistent rounds, bit-exact against the oracle."""
+    n = 12_000
+    args = _hot_args(n)
+    o, c = run_both(ctxf, oracle, args, trace=False)
+    info, st = c.engine_info(), c.stats()
+    assert st["max_pending_events"] > 4000, st
+    assert info["big_slab_pieces"] > 0 and info["slab_extensions"] >= 1, info
+    assert info["persistent_grid"] > 0 and info["persistent_fallbacks"] == 0, info
+    assert_same_run(o, c, n, trace=False)
+
+
+def test_hot_slab_two_shards(ctxf, oracle, monkeypatch):
+    """The multi-shard device path with hot slabs: servers in shard 0, clients in both, so the
+    requests of shard 1's clients reach the servers' slabs through k_import (local shard-group
+    transport); identical to one unsharded shard."""
+    monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    monkeypatch.setenv("SGN_SLAB_LIM", "32")
+    n = 1200
+    args = _hot_args(n)
+    g, used, hosts, cfg, tr = args
+    one = ctxf()
+    one.routes_build(g, used)
+    one.hosts_set(hosts)
+    one.sim_init(cfg, tr)
+    one.run()
+    lat, loss = oracle.routes(g, used)
+    o = oracle.Sim(used, lat, loss, hosts, cfg, tr)
+    o.run()
+    assert_same_run(o, one, n, trace=False)
+    shards = [ctxf(shard_rank=r, shard_count=2) for r in range(2)]
+    arr = (C.c_void_p * 2)(*[s.h.value for s in shards])
+    for s in shards:
+        s.routes_build(g, used)
+        s.hosts_set(hosts)
+    shards[0].check(shards[0].L.sgn_comm_init_local(arr, 2, 1 << 16))
+    for s in shards:
+        s.sim_init(cfg, tr)
+    done = C.c_uint64()
+    shards[0].check(shards[0].L.sgn_run_local_group(arr, 2, 1 << 40, C.byref(done)))
+    assert done.value == one.stats()["rounds"]
+    assert shards[0].engine_info()["big_slab_pieces"] > 0
+    for r, s in enumerate(shards):
+        lo, hi = C.c_uint32(), C.c_uint32()
+        s.L.sgn_shard_range(n, r, 2, C.byref(lo), C.byref(hi))
+        d1, d2 = one.digests(lo.value, hi.value), s.digests(lo.value, hi.value)
+        for f in ("tx", "rx", "app", "rng", "next_event_id", "n_sent", "n_popped", "n_delivered",
+                  "n_codel_dropped"):
+            bad = np.nonzero(d1[f] != d2[f])[0] if d1[f].ndim == 1 else np.nonzero((d1[f] != d2[f]).any(1))[0]
+            assert len(bad) == 0, (r, f, len(bad), lo.value + bad[:5])
+        assert s.window() == one.window()

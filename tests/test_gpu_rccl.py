@@ -77,3 +77,24 @@ def test_rccl_eight_ranks_one_gpu_match_unsharded():
     assert line["parity"] is True, line.get("parity_detail")
     assert line["parity_detail"]["hosts_compared"] == 100_000
     assert line["rounds_timed"] == 80
+
+
+def test_rccl_two_ranks_import_spill_hot_slabs():
+    """Imported runs past their slab: workload H's servers sit in
+    rank 0 and ~10 k clients of rank 1 fetch from them at the same instant, so k_import files thousands of
+    runs into the servers' 16-run slabs (SGN_SLAB_CAP; SGN_SLAB_LIM keeps them small): they go
+    past the slab into the spill area, the next round's gathers read them from there (the
+    big-slab path), every rank holds the round after alike and the calendars are re-laid out
+    with extensions. Eager 32-round batches over real RCCL, against the unsharded run."""
+    env = dict(os.environ, SGN_GRAPH="0", NCCL_DEBUG="WARN", TMPDIR="/tmp", SGN_SLAB_CAP="16", SGN_SLAB_LIM="32")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--workload", "H", "--hosts", "20000",
+           "--nodes", "50", "--rounds-per-step", "40"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["parity"] is True, line.get("parity_detail")
+    assert line["parity_detail"]["hosts_compared"] == 20_000
+    e = line["engine"]
+    assert e["calendar_spill_runs"] > 0 and e["rounds_held"] >= 1 and e["slab_extensions"] >= 1, e
