@@ -529,61 +529,75 @@ struct HostExec {
   __device__ __forceinline__ void load(bool fresh = true) {
     R = S.hrec + h;
     const HostRec& r = *R;
-    gid = r.gid;
-    my_ip = r.ip;
-    my_unode = r.unode;
+    const HostConst& k = S.hconst[h];
+    gid = k.gid;
+    my_ip = k.ip;
+    my_unode = k.unode;
+    lr().tbc[0] = k.tb_inc[0];
+    lr().tbc[1] = k.tb_inc[1];
+    // the hot line
     r0 = r.rng[0];
     r1 = r.rng[1];
     r2 = r.rng[2];
     r3 = r.rng[3];
     eid = r.eid;
-    st0 = r.slot_t[0];
-    st1 = r.slot_t[1];
-    st2 = r.slot_t[2];
-    se0 = r.slot_e[0];
-    se1 = r.slot_e[1];
-    se2 = r.slot_e[2];
+    st2 = r.st2;
+    se2 = r.se2;
     fl = r.flags;
-    ro_dst = r.ro_dst;
-    ro_pay = r.ro_pay;
-    ro_tag = r.ro_tag;
-    ri_src = r.ri_src;
-    ri_pay = r.ri_pay;
-    ri_tag = r.ri_tag;
-    ri_eid = r.ri_eid;
     tbb0 = r.tb_bal[0];
     tbl0 = r.tb_last[0];
     tbb1 = r.tb_bal[1];
     tbl1 = r.tb_last[1];
     cq_head = r.cq_head;
-    L->cq_tp = r.cq_tp;
-    cq_nr = r.cq_nr;
-    cq_len = r.cq_len;
-    cq_bytes = r.cq_bytes;
-    fq_head = r.fq_head;
-    fq_len = r.fq_len;
-    // with the rest of the record (no dependent round trip later in the round): route
-    // cache, token-bucket constants, digests; then the CoDel queue's head run and the send
-    // queue's head entry
-    lr().rc_dst = r.rc_dst;
-    lr().rc_sid = r.rc_sid;
-    lr().rc_lat = r.rc_lat;
-    lr().rc_T = r.rc_T;
-    lr().tbc[0] = r.tb_inc[0];
-    lr().tbc[1] = r.tb_inc[1];
-    if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
-      L->cq[0] = r.cq_ie;
-      L->cq[1] = r.cq_dn;
-      L->cq[2] = r.cq_cur;
-      L->cq[3] = r.cq_prev;
-    }
     lr().app_k = r.app_k;
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
+    // the cold lines (PERIODIC: only when the host ended its last round with state there)
+    if (kApp != SGN_TRAFFIC_PERIODIC || (fl & F_COLD)) {
+      st0 = r.st0;
+      st1 = r.st1;
+      se0 = r.se0;
+      se1 = r.se1;
+      ro_dst = r.ro_dst;
+      ro_pay = r.ro_pay;
+      ro_tag = r.ro_tag;
+      ri_src = r.ri_src;
+      ri_pay = r.ri_pay;
+      ri_tag = r.ri_tag;
+      ri_eid = r.ri_eid;
+      L->cq_tp = r.cq_tp;
+      cq_nr = r.cq_nr;
+      cq_len = r.cq_len;
+      cq_bytes = r.cq_bytes;
+      fq_head = r.fq_head;
+      fq_len = r.fq_len;
+      lr().rc_dst = r.rc_dst;
+      lr().rc_sid = r.rc_sid;
+      lr().rc_lat = r.rc_lat;
+      lr().rc_T = r.rc_T;
+      if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
+        L->cq[0] = r.cq_ie;
+        L->cq[1] = r.cq_dn;
+        L->cq[2] = r.cq_cur;
+        L->cq[3] = r.cq_prev;
+      }
+    } else {  // an idle host: both relays idle, no cached packets, both queues empty
+      st0 = st1 = INVALID;
+      se0 = se1 = 0;
+      ro_dst = ro_pay = ro_tag = ri_src = ri_pay = ri_tag = 0;
+      ri_eid = 0;
+      L->cq_tp = cq_head / CQ_PAGE;  // (an empty queue keeps its page: head and tail)
+      cq_nr = cq_len = 0;
+      cq_bytes = 0;
+      fq_head = fq_len = 0;
+      lr().rc_dst = NO_HOST;
+      lr().rc_sid = 0;
+      lr().rc_lat = lr().rc_T = 0;
+    }
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
     c_runs = 0;
-    c_maxcodel = r.max_codel;
+    c_maxcodel = 0;
     hd_valid = tl_open = false;
     if (cq_nr > 0) {
       L->hd = ld_dev_cq(cq_head_slot());
@@ -616,8 +630,20 @@ struct HostExec {
   }
   __device__ __forceinline__ uint32_t next_peer() const {
     uint32_t peer = NO_HOST, uip = 0;
-    if (!sgn_periodic_dst(S.flow_seed, gid, lr().app_k, S.n_all, S.unknown_permille, &peer, &uip)) peer = NO_HOST;
+    if (!periodic_dst(lr().app_k, &peer, &uip)) peer = NO_HOST;
     return peer;
+  }
+  // sgn_periodic_dst / sgn_tgen_fetch (sgn_workload.h) with the remainders by multiply-high
+  // (u64 % is a long software routine on the GPU; the results are the same integers)
+  __device__ __forceinline__ uint64_t mod_by(const UDiv64& d, uint64_t x, uint64_t n) const { return x - d.div(x) * n; }
+  __device__ __forceinline__ bool periodic_dst(uint64_t k, uint32_t* peer, uint32_t* uip) const {
+    const uint64_t r = sgn_flow_hash(S.flow_seed, gid, k);
+    if ((uint32_t)mod_by(S.div_1000, r, 1000u) < S.unknown_permille) {
+      *uip = SGN_UNKNOWN_IP_BASE + (uint32_t)((r >> 32) & 0xFFFFu);
+      return false;
+    }
+    *peer = (uint32_t)mod_by(S.div_n, r >> 16, S.n_all);
+    return true;
   }
   __device__ __forceinline__ void prefetch_route() {
     if (pf_peer == NO_HOST) return;
@@ -635,50 +661,61 @@ struct HostExec {
     r.rng[2] = r2;
     r.rng[3] = r3;
     r.eid = eid;
-    r.ri_eid = ri_eid;
-    r.slot_t[0] = st0;
-    r.slot_t[1] = st1;
-    r.slot_t[2] = st2;
-    r.slot_e[0] = se0;
-    r.slot_e[1] = se1;
-    r.slot_e[2] = se2;
+    r.st2 = st2;
+    r.se2 = se2;
     r.tb_bal[0] = tbb0;
     r.tb_bal[1] = tbb1;
     r.tb_last[0] = tbl0;
     r.tb_last[1] = tbl1;
-    r.cq_bytes = cq_bytes;
-    r.rc_lat = lr().rc_lat;
-    r.rc_T = lr().rc_T;
     r.dig[0] = L->dig[0];
     r.dig[1] = L->dig[1];
     r.dig[2] = L->dig[2];
-    if (fl & F_FH_DIRTY) *fq_slot(0) = L->fh;  // a queued head that lived in LDS
-    r.flags = fl & ~F_FH_DIRTY;
-    r.ro_dst = ro_dst;
-    r.ro_pay = ro_pay;
-    r.ro_tag = ro_tag;
-    r.ri_src = ri_src;
-    r.ri_pay = ri_pay;
-    r.ri_tag = ri_tag;
-    r.cq_head = cq_head;
-    r.cq_tp = L->cq_tp;
-    r.cq_nr = cq_nr;
-    r.cq_len = cq_len;
-    r.fq_head = fq_head;
-    r.fq_len = fq_len;
-    r.rc_dst = lr().rc_dst;
-    r.rc_sid = lr().rc_sid;
-    r.max_codel = c_maxcodel;
-    r.n_sent += c_sent;
-    r.n_popped += c_popped;
-    r.n_delivered += c_deliv;
-    if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
-      r.cq_ie = L->cq[0];
-      r.cq_dn = L->cq[1];
-      r.cq_cur = L->cq[2];
-      r.cq_prev = L->cq[3];
-    }
     r.app_k = lr().app_k;
+    r.cq_head = cq_head;
+    if (fl & F_FH_DIRTY) *fq_slot(0) = L->fh;  // a queued head that lived in LDS
+    // the cold lines: PERIODIC writes them only when the host leaves state there (load() gives
+    // an idle host its defaults: this must list every field that differs from them)
+    const bool cold = kApp != SGN_TRAFFIC_PERIODIC || st0 != INVALID || st1 != INVALID ||
+                      (fl & (F_RO_STATE | (3u << F_RI_STATE_SHIFT) | F_RO_NEXT | F_RI_NEXT | F_CODEL_IE |
+                             F_CODEL_DN | F_CODEL_DROP)) ||
+                      cq_nr || cq_len || cq_bytes || fq_len || fq_head;
+    r.flags = (fl & ~(F_FH_DIRTY | F_COLD)) | (cold ? F_COLD : 0u);
+    if (cold) {
+      r.st0 = st0;
+      r.st1 = st1;
+      r.se0 = se0;
+      r.se1 = se1;
+      r.ri_eid = ri_eid;
+      r.cq_bytes = cq_bytes;
+      r.rc_lat = lr().rc_lat;
+      r.rc_T = lr().rc_T;
+      r.ro_dst = ro_dst;
+      r.ro_pay = ro_pay;
+      r.ro_tag = ro_tag;
+      r.ri_src = ri_src;
+      r.ri_pay = ri_pay;
+      r.ri_tag = ri_tag;
+      r.cq_tp = L->cq_tp;
+      r.cq_nr = cq_nr;
+      r.cq_len = cq_len;
+      r.fq_head = fq_head;
+      r.fq_len = fq_len;
+      r.rc_dst = lr().rc_dst;
+      r.rc_sid = lr().rc_sid;
+      if constexpr (kApp != SGN_TRAFFIC_PERIODIC) {
+        r.cq_ie = L->cq[0];
+        r.cq_dn = L->cq[1];
+        r.cq_cur = L->cq[2];
+        r.cq_prev = L->cq[3];
+      }
+    }
+    // the per-host totals: no-return adds (no load of the old value)
+    const size_t nH = S.nH;
+    if (c_sent) cnt_add(&S.n_cnt[N_SENT * nH + h], c_sent);
+    if (c_popped) cnt_add(&S.n_cnt[N_POPPED * nH + h], c_popped);
+    if (c_deliv) cnt_add(&S.n_cnt[N_DELIVERED * nH + h], c_deliv);
+    if (c_maxcodel)
+      (void)__hip_atomic_fetch_max(&S.maxq[h], c_maxcodel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.nextloc[h] = next_local_time();
     if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
     if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
@@ -1665,6 +1702,7 @@ struct HostExec {
       if (consumed == e.count) {
         fq_head = fq_head + 1 == S.fifo_cap ? 0 : fq_head + 1;
         fq_len--;
+        if (fq_len == 0) fq_head = 0;  // (an empty queue's head is 0: an idle host's default)
         fl &= ~F_FH_DIRTY;
       } else if (rr) {
         // the socket still has data: re-queued behind the others (same length)
@@ -1711,14 +1749,17 @@ struct HostExec {
     if (kApp == SGN_TRAFFIC_PERIODIC) {
       uint32_t peer = 0;
       // an address outside the simulation (10.255.0.0/16, never registered) is NO_HOST
-      dst = sgn_periodic_dst(S.flow_seed, gid, k, S.n_all, S.unknown_permille, &peer, &uip)
-                ? peer : NO_HOST;
+      dst = periodic_dst(k, &peer, &uip) ? peer : NO_HOST;
       payload = S.payload_len;
       tag = SGN_TAG_DATA;
       next_delay = S.period;
     } else {
       uint32_t si = 0, cls = 0;
-      sgn_tgen_fetch(S.flow_seed, gid, k, S.n_servers, &si, &cls);
+      {  // sgn_tgen_fetch
+        const uint64_t r = sgn_flow_hash(S.flow_seed, gid, k);
+        si = (uint32_t)mod_by(S.div_ns, r >> 8, S.n_servers);
+        cls = (uint32_t)((r >> 40) % 3u);
+      }
       DGT_BEGIN(tsv);
       dst = S.servers[si];
       DGT_WAIT();
@@ -3336,9 +3377,11 @@ __global__ void k_next_local(const DevSim* Sp, uint32_t lo, uint32_t n, uint64_t
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const HostRec& r = Sp->hrec[Sp->sid_of[lo + i] - Sp->lo];
-  uint64_t m = r.slot_t[0];
-  m = r.slot_t[1] < m ? r.slot_t[1] : m;
-  m = r.slot_t[2] < m ? r.slot_t[2] : m;
+  uint64_t m = r.st2;
+  if (Sp->tkind != SGN_TRAFFIC_PERIODIC || (r.flags & F_COLD)) {  // (else both relays idle)
+    m = r.st0 < m ? r.st0 : m;
+    m = r.st1 < m ? r.st1 : m;
+  }
   out[i] = m;
 }
 // ... and the earliest pending packet event: one wave per (bucket, host group) slab,
@@ -4094,22 +4137,26 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   }
   // ---- per-host state records (one per slot), initialised on the host ----
   std::vector<HostRec> recs(nH);
+  std::vector<HostConst> hk(nH);
   std::vector<uint64_t> nextloc(nH, INVALID);
   std::memset(recs.data(), 0, recs.size() * sizeof(HostRec));
+  std::memset(hk.data(), 0, hk.size() * sizeof(HostConst));
   for (uint32_t h = 0; h < nH; h++) {
     const uint32_t g = ctx->host_of[h];
     HostRec& r = recs[h];
-    r.gid = g;
+    HostConst& k = hk[h];
+    k.gid = g;
+    k.ip = ctx->ip[g];
+    k.unode = ctx->unode[g];
     // Xoshiro256PlusPlus::seed_from_u64 (SplitMix64 fill), host.rs:234
     uint64_t sm = ctx->seed[g];
     for (int i = 0; i < 4; i++) r.rng[i] = host_splitmix(sm);
-    for (int i = 0; i < 3; i++) r.slot_t[i] = INVALID;
+    r.st0 = r.st1 = r.st2 = INVALID;
     // create_token_bucket (relay/mod.rs:278-288) for inet_out (up) and inet_in (down)
     for (int w = 0; w < 2; w++) {
       const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
       const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
-      r.tb_inc[w] = inc;
-      r.tb_cap[w] = inc + SGN_CONFIG_MTU;
+      k.tb_inc[w] = inc;  // (capacity = inc + MTU, the bucket starts full)
       r.tb_bal[w] = inc + SGN_CONFIG_MTU;
       r.tb_last[w] = SIM_START;
     }
@@ -4117,8 +4164,6 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     r.rc_dst = NO_HOST;  // empty route cache
     r.cq_head = h * CQ_PAGE;  // CoDel chain: page h
     r.cq_tp = h;
-    r.ip = ctx->ip[g];
-    r.unode = ctx->unode[g];
     if (is_server[g]) r.flags |= F_SERVER;
     const bool has_app = tr->kind == SGN_TRAFFIC_PERIODIC || (tr->kind == SGN_TRAFFIC_TGEN && !is_server[g]);
     if (has_app) {
@@ -4126,8 +4171,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       const uint64_t t = SIM_START + sgn_app_start_rel(tr->flow_seed, g, tr->start_ns, tr->start_jitter_ns);
       const uint64_t e = r.eid++;
       if (t < S.end_time) {
-        r.slot_t[2] = t;
-        r.slot_e[2] = e;
+        r.st2 = t;
+        r.se2 = e;
         nextloc[h] = t;
       }
     }
@@ -4182,6 +4227,14 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!S.hrec || !S.codel || !S.fifo || !S.cq_next || !S.rb_free)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
+  {
+    HostConst* dk = dalloc<HostConst>(ctx, nH);
+    S.n_cnt = (decltype(S.n_cnt))dalloc<uint64_t>(ctx, (size_t)N_CNT * nH);
+    S.maxq = (decltype(S.maxq))dalloc<uint32_t>(ctx, nH);
+    if (!dk || !S.n_cnt || !S.maxq) return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
+    SGN_HIP(ctx, hipMemcpy(dk, hk.data(), hk.size() * sizeof(HostConst), hipMemcpyHostToDevice));
+    S.hconst = (decltype(S.hconst))dk;
+  }
   if ((rc = up64(nextloc, &S.nextloc))) return rc;
   S.npeer = nullptr;
   if (tr->kind == SGN_TRAFFIC_PERIODIC) {  // every app counter starts at 0
@@ -4226,6 +4279,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   S.CAP = (uint32_t)CAP;
   S.BW = BW;
   S.bw_div.init(BW);
+  S.div_n.init(std::max<uint64_t>(1, N));
+  S.div_1000.init(1000);
+  S.div_ns.init(std::max<uint64_t>(1, S.n_servers));
   S.pool = (decltype(S.pool))dalloc<EvRec>(ctx, (NB + 1) * G * CAP);
   S.w_cnt = (decltype(S.w_cnt))dalloc<uint64_t>(ctx, W_N * G);
   if (!S.w_cnt) return set_error(ctx, SGN_ENOMEM, "device allocation failed (wave slots)");
@@ -4311,10 +4367,14 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // ~gsz * BW / period; when that is a full wave (config D: 64 hosts, one send per window) all
   // 64 lanes load speculatively and the second round trip goes (same-box A/B: D +1.3 %, while
   // B's ~2-run slabs measured 1 % slower at 64 and unchanged at 4 and 8)
+  // (round 4: from 4 up, twice the expected fill: config B's ~2-run slabs of 16 hosts read 4
+  // records instead of 16 — its PMC traffic was 3.4x the algorithmic bytes, mostly these
+  // speculative heads, while B's time measured the same at 4, 8 and 16 in round 3)
   S.gspec = GATHER_SPEC;
   if (S.tkind == SGN_TRAFFIC_PERIODIC && S.period) {
     const uint64_t fill = ((uint64_t)gsz * BW + S.period - 1) / S.period;
-    while (S.gspec < 64 && S.gspec < fill) S.gspec *= 2;
+    S.gspec = 4;
+    while (S.gspec < 64 && S.gspec < 2 * fill) S.gspec *= 2;
   }
   if (const char* e = getenv("SGN_GATHER_SPEC")) S.gspec = std::min<uint32_t>(64, (uint32_t)atoi(e));
   S.gspec = (uint32_t)std::min<uint64_t>(S.gspec, S.CAP);  // speculative loads stay inside the slab
@@ -4497,6 +4557,22 @@ int read_recs(sgn_ctx* ctx, uint32_t off, uint32_t n, std::vector<HostRec>* out)
                                 hipMemcpyDeviceToHost));
   return 0;
 }
+// the per-host totals of owned slots [off, off + n): N_CNT rows, then the CoDel maxima
+int read_counts(sgn_ctx* ctx, uint32_t off, uint32_t n, std::vector<uint64_t>* cnt, std::vector<uint32_t>* mq) {
+  const size_t nH = ctx->S.nH;
+  cnt->assign((size_t)N_CNT * n, 0);
+  if (mq) mq->assign(n, 0);
+  if (!n) return 0;
+  for (int k = 0; k < N_CNT; k++)
+    SGN_HIP(ctx, hipMemcpy(cnt->data() + (size_t)k * n, (const void*)(ctx->S.n_cnt + k * nH + off), (size_t)n * 8,
+                           hipMemcpyDeviceToHost));
+  if (mq) SGN_HIP(ctx, hipMemcpy(mq->data(), (const void*)(ctx->S.maxq + off), (size_t)n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+// the cold lines hold the host's queue state (else it is an idle host's: empty queues)
+inline bool cold_valid(const sgn_ctx* ctx, const HostRec& r) {
+  return ctx->S.tkind != SGN_TRAFFIC_PERIODIC || (r.flags & F_COLD);
+}
 }  // namespace
 
 int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
@@ -4505,18 +4581,22 @@ int sgn_stats_get(sgn_ctx* ctx, sgn_stats* out) {
   int rc = sync_ctrl(ctx);
   const uint32_t nH = ctx->S.nH;
   std::vector<HostRec> recs;
+  std::vector<uint64_t> cnt;
+  std::vector<uint32_t> mq;
   if (int e = read_recs(ctx, 0, nH, &recs)) return e;
+  if (int e = read_counts(ctx, 0, nH, &cnt, &mq)) return e;
   sgn_stats s{};
   uint64_t mc = 0;
-  for (const HostRec& r : recs) {
-    s.packets_sent += r.n_sent;
+  for (uint32_t h = 0; h < nH; h++) {
+    const HostRec& r = recs[h];
+    s.packets_sent += cnt[(size_t)N_SENT * nH + h];
     s.packets_unknown_dst += r.n_unknown;
-    s.packet_events_popped += r.n_popped;
+    s.packet_events_popped += cnt[(size_t)N_POPPED * nH + h];
     s.codel_dropped += r.n_codel;
-    s.delivered += r.n_delivered;
+    s.delivered += cnt[(size_t)N_DELIVERED * nH + h];
     s.local_delivered += r.n_local_deliv;
     s.app_blocked += r.n_blocked;
-    mc = std::max<uint64_t>(mc, r.max_codel);
+    mc = std::max<uint64_t>(mc, mq[h]);
   }
   s.rounds = ctx->h_ctrl->rounds;
   s.min_used_latency_ns = ctx->h_ctrl->min_used;
@@ -4557,19 +4637,24 @@ int sgn_host_digests(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_host_digest* ou
     smax = std::max(smax, ctx->sid_of[i]);
   }
   std::vector<HostRec> recs;
-  if (n)
-    if (int e = read_recs(ctx, smin - ctx->lo, smax - smin + 1, &recs)) return e;
+  std::vector<uint64_t> cnt;
+  const uint32_t ns = n ? smax - smin + 1 : 0;
+  if (n) {
+    if (int e = read_recs(ctx, smin - ctx->lo, ns, &recs)) return e;
+    if (int e = read_counts(ctx, smin - ctx->lo, ns, &cnt, nullptr)) return e;
+  }
   for (uint32_t i = 0; i < n; i++) {
-    const HostRec& r = recs[ctx->sid_of[lo + i] - smin];
+    const uint32_t j = ctx->sid_of[lo + i] - smin;
+    const HostRec& r = recs[j];
     sgn_host_digest& o = out[i];
     o.tx = r.dig[0];
     o.rx = r.dig[1];
     o.app = r.dig[2];
     for (int k = 0; k < 4; k++) o.rng[k] = r.rng[k];
     o.next_event_id = r.eid;
-    o.n_sent = r.n_sent;
-    o.n_popped = r.n_popped;
-    o.n_delivered = r.n_delivered;
+    o.n_sent = cnt[(size_t)N_SENT * ns + j];
+    o.n_popped = cnt[(size_t)N_POPPED * ns + j];
+    o.n_delivered = cnt[(size_t)N_DELIVERED * ns + j];
     o.n_codel_dropped = r.n_codel;
   }
   return rc;
@@ -4654,8 +4739,10 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   std::vector<HostRec> recs;
   if (int e = read_recs(ctx, 0, ctx->S.nH, &recs)) return e;
   uint64_t chained = 0;
-  for (const HostRec& r : recs)
-    chained += r.cq_nr == 0 ? 1 : ((r.cq_head & (CQ_PAGE - 1)) + r.cq_nr + CQ_PAGE - 1) / CQ_PAGE;
+  for (const HostRec& r : recs) {
+    const uint32_t nr = cold_valid(ctx, r) ? r.cq_nr : 0;
+    chained += nr == 0 ? 1 : ((r.cq_head & (CQ_PAGE - 1)) + nr + CQ_PAGE - 1) / CQ_PAGE;
+  }
   out->codel_pages_chained = chained;
   int ncu = 0;
   SGN_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));

@@ -381,6 +381,59 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
       sweep_arc<S>(row, g0, auv[e], al32[e], e, capg, tcnt, tlist);
 }
 
+// The same sweep over the arc list in tail order (CSR: rowptr[u] .. rowptr[u + 1] are u's arcs,
+// dense graphs): a wave takes one tail u at a time, so its S distances d[s][u] are one LDS
+// broadcast read kept in registers, and the lanes' heads v are consecutive (conflict-free
+// reads of d[s][v]); a workgroup sweeps a range of tails. The test is d[s][v] - d[s][u] == l
+// with d[s][v] >= d[s][u] (u32; an arc of 2^32 - 1 ns or more is never tight).
+template <int S>
+__global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
+                                                      uint32_t U, uint32_t V, const uint32_t* rowptr,
+                                                      const uint32_t* auv, const uint32_t* al32, uint32_t capg,
+                                                      uint32_t* tcnt, uint32_t* tlist) {
+  static_assert(S % 4 == 0, "rows are read 4 sources at a time");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* row = (uint32_t*)smem;  // [Vp][S]
+  const uint32_t g0 = blockIdx.x * S;
+  for (uint32_t i = threadIdx.x; i < Vp * S; i += blockDim.x) {
+    const uint32_t u = i / S, k = i % S;
+    row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t u0 = (uint32_t)((uint64_t)V * blockIdx.y / gridDim.y);
+  const uint32_t u1 = (uint32_t)((uint64_t)V * (blockIdx.y + 1) / gridDim.y);
+  for (uint32_t u = u0 + wave; u < u1; u += nw) {
+    uint32_t du[S];
+#pragma unroll
+    for (int k = 0; k < S; k += 4) {
+      const uint4 x = *(const uint4*)(row + u * S + k);
+      du[k] = x.x;
+      du[k + 1] = x.y;
+      du[k + 2] = x.z;
+      du[k + 3] = x.w;
+    }
+    const uint32_t e1 = rowptr[u + 1];
+    for (uint32_t e = rowptr[u] + lane; e < e1; e += 64) {
+      const uint32_t l = al32[e];
+      if (l == SQ_INF) continue;
+      const uint32_t* dv = row + (auv[e] >> 16) * S;
+#pragma unroll
+      for (int k = 0; k < S; k += 4) {
+        const uint4 y = *(const uint4*)(dv + k);
+        const uint32_t b[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (b[j] < du[k + j] || b[j] - du[k + j] != l) continue;
+          const uint32_t src = g0 + k + j;
+          const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+          if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+        }
+      }
+    }
+  }
+}
+
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
 // then the fixed point as in loss_pass. (tcnt > capg: the caller reruns loss_pass instead.)
 __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
@@ -776,6 +829,28 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
     }
     const uint32_t E2 = (uint32_t)auv.size();
+    // dense graphs (the multi-source loss sweep): the arcs in tail order, with CSR offsets
+    // (every consumer of the arc list is order-free: relaxation and the loss folds reach the same
+    // fixed point); SGN_APSP_SWEEP_ARCS=1 keeps the edge order and the per-arc sweep (A/B)
+    const bool csr = E2 >= 32ull * Vp && !getenv("SGN_APSP_SWEEP_ARCS");
+    std::vector<uint32_t> rowptr;
+    if (csr) {
+      rowptr.assign(V + 1, 0);
+      for (uint32_t e = 0; e < E2; e++) rowptr[(auv[e] & 0xFFFFu) + 1]++;
+      for (uint32_t u = 0; u < V; u++) rowptr[u + 1] += rowptr[u];
+      std::vector<uint32_t> pos(rowptr.begin(), rowptr.end() - 1), auv2(E2);
+      std::vector<uint64_t> al2(E2);
+      std::vector<float> ap2(E2);
+      for (uint32_t e = 0; e < E2; e++) {
+        const uint32_t k = pos[auv[e] & 0xFFFFu]++;
+        auv2[k] = auv[e];
+        al2[k] = al[e];
+        ap2[k] = ap[e];
+      }
+      auv.swap(auv2);
+      al.swap(al2);
+      ap.swap(ap2);
+    }
     std::vector<uint64_t> sl(U);
     std::vector<float> sp(U);
     for (uint32_t i = 0; i < U; i++) {
@@ -787,8 +862,9 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     const uint32_t cap = (uint32_t)std::min<size_t>(std::max<size_t>(4096, 4 * (size_t)Vp),
                                                     (160 * 1024 - lds - 16) / 8);
     const size_t lds2 = lds + (size_t)cap * 8 + 16;
-    DevBuf dD, deu, dev, del, dauv, dal, dap, dus, dL, dit, dsl, dsp, dres, drowres;
+    DevBuf dD, deu, dev, del, dauv, dal, dap, dus, dL, dit, dsl, dsp, dres, drowres, drp;
     int rc;
+    if (csr && (rc = upload(ctx, drp, rowptr.data(), V + 1))) return rc;
     if ((rc = upload(ctx, deu, es.data(), E)) || (rc = upload(ctx, dev, ed.data(), E)) ||
         (rc = upload(ctx, del, g->edge_latency_ns, E)) || (rc = upload(ctx, dauv, auv.data(), E2)) ||
         (rc = upload(ctx, dal, al.data(), E2)) || (rc = upload(ctx, dap, ap.data(), E2)) ||
@@ -837,7 +913,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       for (int k : {8, 4}) {
         const size_t b = (size_t)Vp * k * 4;
         if (b > 160 * 1024) continue;
-        const void* f = k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>;
+        const void* f = csr ? (k == 8 ? (const void*)loss_sweep_csr<8> : (const void*)loss_sweep_csr<4>)
+                            : (k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>);
         if (b <= 64 * 1024 ||
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
           kS = k;
@@ -960,7 +1037,13 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         const uint32_t* us = (const uint32_t*)dus.p + s0;
         uint32_t* tcs = (uint32_t*)dtc.p + s0;
         uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
-        if (kS == 8)
+        if (csr && kS == 8)
+          hipLaunchKernelGGL(loss_sweep_csr<8>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
+                             (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
+        else if (csr)
+          hipLaunchKernelGGL(loss_sweep_csr<4>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
+                             (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
+        else if (kS == 8)
           hipLaunchKernelGGL(loss_sweep<8>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns,
                              (const uint32_t*)dauv.p, a32, E2, capg, tcs, tls);
         else

@@ -159,41 +159,55 @@ enum : uint32_t {
 };
 
 // One host's state record (array of records, one per owned host, 512 B, 128-B aligned).
-// A round touches only the hosts with something due (~1 in 8 at the bench workload), so a
-// record per host turns each executed host's state into 3 contiguous cache lines; the hot
-// part (bytes 0..335) is what Host::execute reads and writes every time it runs.
+// A round touches only the hosts with something due (~1 in 8 at config C, every host at D).
+// Line 0 is the HOT line: what Host::execute reads and writes every time a host runs (RNG,
+// event-id counter, the app's timer, token buckets, digests, app counter, flags, CoDel page).
+// Lines 1-3 are COLD: the relays' pending tasks and cached packets, the CoDel and send queues'
+// bookkeeping, the route cache, CoDel's drop state, rare counters. PERIODIC hosts (configs B, D)
+// end nearly every round with both queues empty and both relays idle: their store() leaves the
+// cold lines alone (F_COLD clear: the cold state is the default of an idle host, whatever the
+// lines hold) and load() reads them only when F_COLD is set. TGEN / EXTERNAL hosts always use
+// them. The per-host totals are no-return atomic adds into dense arrays (DevSim::n_cnt, maxq)
+// and the constants (HostId, address, node, refill increments) a dense array of their own, so
+// an idle PERIODIC host-round moves one line each way plus 32 read bytes.
 constexpr uint32_t CQ_PAGE = 16;  // CoDel runs per pool page (cq_head = page * CQ_PAGE + offset)
 
 struct __attribute__((aligned(128))) HostRec {
+  // ---- line 0: hot ----
   uint64_t rng[4];           // Xoshiro256++ state (host/host.rs:234)
   uint64_t eid;              // next event id (host.rs:259,662-666)
-  uint64_t ri_eid;           // relay_inet_in cached packet: src event id
-  uint64_t slot_t[3];        // local event slots (relay out, relay in, app): time ...
-  uint64_t slot_e[3];        // ... and event id
+  uint64_t st2, se2;         // the app's local event slot: time, event id
   uint64_t tb_bal[2];        // token buckets (0 = inet_out, 1 = inet_in): balance ...
   uint64_t tb_last[2];       // ... last refill
-  uint64_t tb_inc[2];        // ... refill increment (constant)
-  uint64_t tb_cap[2];        // ... capacity (constant)
-  uint64_t cq_bytes;         // CoDel queued bytes
-  uint64_t rc_lat, rc_T;     // route cache: latency, integer loss threshold ...
   uint64_t dig[3];           // digests tx, rx, app
-  uint32_t flags, ro_dst, ro_pay, ro_tag;    // flag bits; relay_inet_out cached packet
-  uint32_t ri_src, ri_pay, ri_tag, cq_head;  // relay_inet_in cached packet; CoDel head run (pool index)
-  uint32_t cq_nr, cq_len, fq_head, fq_len;   // CoDel runs / packets; send queue
-  uint32_t rc_dst, ip, unode, max_codel;     // ... route cache peer; address; node; high mark
-  uint32_t gid, rc_sid;                      // this host's HostId; route cache peer's slot id
-  uint32_t cq_tp, cq_pad;                    // CoDel chain's tail page (cq_head: head run's pool index)
-  uint64_t n_sent, n_popped, n_delivered;    // per-host counters (read-modify-write)
+  uint64_t app_k;            // synthetic app counter
+  uint32_t flags, cq_head;   // flag bits; CoDel head run (pool index; an empty queue keeps its page)
+  // ---- lines 1-3: cold ----
+  uint64_t st0, se0, st1, se1;  // local event slots: relay out, relay in (time, event id)
+  uint64_t ri_eid;           // relay_inet_in cached packet: src event id
+  uint64_t cq_bytes;         // CoDel queued bytes
+  uint64_t rc_lat, rc_T;     // route cache: latency, integer loss threshold (TGEN, EXTERNAL)
   uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
-  uint64_t app_k;                            // synthetic app counter
-  // cold: rare paths only
+  uint32_t ro_dst, ro_pay, ro_tag;           // relay_inet_out cached packet
+  uint32_t ri_src, ri_pay, ri_tag;           // relay_inet_in cached packet
+  uint32_t cq_nr, cq_len, cq_tp;             // CoDel runs / packets / chain's tail page
+  uint32_t fq_head, fq_len;                  // send queue (an empty queue's head is 0)
+  uint32_t rc_dst, rc_sid, pad_c;            // route cache peer (NO_HOST: none) and its slot id
+  // rare paths only (never loaded with the state: traced runs, sgn_rng_*, no-return atomics)
   uint64_t tseq;                            // trace sequence
   uint64_t rng_pos;                         // RNG draws so far (kept while tracing, and by sgn_rng_*)
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
-  uint64_t pad[14];
+  uint64_t pad[23];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
-static_assert(offsetof(HostRec, app_k) + 8 <= 384, "hot part: three cache lines");
+static_assert(offsetof(HostRec, st0) == 128, "line 0: the hot line");
+// the constants of a host's slot, read with the hot line (32 B)
+struct __attribute__((aligned(32))) HostConst {
+  uint32_t gid, ip, unode, pad;  // HostId, address, used-node index
+  uint64_t tb_inc[2];            // token-bucket refill increments (capacity = increment + MTU)
+};
+static_assert(sizeof(HostConst) == 32, "");
+enum { N_SENT = 0, N_POPPED, N_DELIVERED, N_CNT };  // DevSim::n_cnt rows
 
 // per-wave counters (DevSim::w_cnt rows of G)
 enum { W_EXEC = 0, W_RUNS, W_SORTED, W_LOSS, W_LOCAL_EV, W_BYTES, W_MAXFILL, W_BIG, W_N };  // W_MAXFILL: max, not sum
@@ -212,6 +226,7 @@ enum : uint32_t {
   F_HAS_APP = 0x400u,        // host runs a synthetic app timer
   F_RO_CONT = 0x800u,        // inside relay_inet_out's forwarding task (never stored)
   F_FH_DIRTY = 0x1000u,      // the send queue's head exists only in LDS (never stored)
+  F_COLD = 0x2000u,          // the record's cold lines hold the host's state (else: idle defaults)
 };
 
 enum { SLOT_RO = 0, SLOT_RI = 1, SLOT_APP = 2, NSLOT = 3 };
@@ -297,6 +312,9 @@ struct DevSim {
   // host state: one record per owned host, and each host's next local event time (read
   // for all hosts at the start of a round: a dense array keeps that read coalesced)
   SGN_GLB HostRec* hrec;        // [nH]
+  SGN_GLB const HostConst* hconst;  // [nH]
+  SGN_GLB uint64_t* n_cnt;      // [N_CNT * nH] per-host totals (sent, popped, delivered)
+  SGN_GLB uint32_t* maxq;       // [nH] per-host largest CoDel queue length
   SGN_GLB uint64_t* nextloc;    // [nH]
   // PERIODIC traffic: the peer (HostId, NO_HOST for an unknown address) of each host's next
   // datagram, a hash of its app counter written when the host's record is stored, so the next
@@ -355,6 +373,7 @@ struct DevSim {
   uint32_t agg_bmin;      // the round kernels fold bucket minima in an LDS table (see engine.hip)
   uint64_t BW;
   UDiv64 bw_div;          // division by BW
+  UDiv64 div_n, div_1000, div_ns;  // by n_all, 1000, n_servers (the synthetic apps' hashes, exact)
   SGN_GLB uint64_t* stamps;     // diagnostics (nullptr unless SGN_STAMPS is set)
   SGN_GLB uint64_t* rdbg;       // ... per-round timeline of the persistent kernel
   uint32_t n_ranks;

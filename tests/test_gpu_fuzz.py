@@ -2,7 +2,8 @@
 that mix every option of the path at once — traffic kind (PERIODIC / TGEN), static and
 dynamic runahead with bootstrapping, per-host bandwidths, lossy random and Tor-like graphs,
 unknown destinations, send-queue and CoDel-pool sizes down to the blocking / page-reuse
-regime, the interface qdisc, hosts per wave, and the round kernel (persistent k_rounds or
+regime, the interface qdisc, hosts per wave, small calendar slabs (extensions and the
+big-slab path), and the round kernel (persistent k_rounds or
 per-round k_execute, traced or not). Pools grow instead of refusing a scenario
 (test_gpu_pools.py), so no case may be skipped. Bar: every counter, the final window and
 every host's order-sensitive digests (tx / rx / app / RNG state / next event id) identical;
@@ -45,6 +46,9 @@ def draw(i):
     env = {"SGN_HOSTS_PER_WAVE": str(int(r.choice([16, 32, 64]))),
            "SGN_PERSISTENT": str(int(r.random() < 0.7))}
     trace = bool(r.random() < 0.5)
+    if r.random() < 0.3:  # small slabs that stay small: spills, extensions and big-slab pieces
+        env["SGN_SLAB_CAP"] = "16"
+        env["SGN_SLAB_LIM"] = "32"
     return kw, env, trace
 
 
