@@ -33,6 +33,7 @@ import sgn  # noqa: E402
 
 METRIC = "simulated packet events/sec (whole node) at 100k hosts; APSP build time"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md L2 section: 4 MiB per XCD, ~34.5 TB/s aggregate
 
 
 def build_workload(n_hosts, V, seed=1):
@@ -347,6 +348,20 @@ def apsp_roofline(apsp, V, U):
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         out[name] = {"bound": "hbm", "alg_bytes": int(b), "ms": round(ms, 3), "achieved": round(gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5)}
+    # the loss phase against each level it reads: its compulsory HBM bytes — the
+    # arc list once (8 B per arc), the used sources' u32 distance rows, the tight lists written
+    # and read back (~one arc per node and source, 4 B each way), the f32 loss rows written — and
+    # the re-read model above, whose arc re-reads are served by the L2s (MI355X_MICROARCH.md:
+    # 4 MiB per XCD, ~34.5 TB/s aggregate), not by HBM
+    ms = apsp["loss_ms"]
+    if ms > 0:
+        hbm = 8.0 * E + 4.0 * U * V + 2 * 4.0 * U * V + 4.0 * U * V
+        out["loss_phase"]["hbm_bytes"] = int(hbm)
+        out["loss_phase"]["hbm_frac"] = round(hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        out["loss_phase"]["l2_bytes"] = int(b_loss)
+        out["loss_phase"]["l2_peak_GBps"] = L2_PEAK_GBS
+        out["loss_phase"]["l2_frac"] = round(b_loss / (ms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)
+        out["loss_phase"]["bound"] = "l2"
     out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
                    ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else "u32 min-plus squaring"),
                    "loss": f"{k}-source arc sweep + LDS fold" if k else "one-source arc sweep + LDS fold"}

@@ -269,12 +269,18 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       }
       if (int rc = exchange_import()) return rc;
     }
-    // a held round edge (the same on every shard) or a spill: the pools grow before the next
+    // a held round edge (the same on every shard) or a spill: the pools grow before the next.
+    // SGN_LOCAL_DEFER=1 (test hook): like the RCCL transport between its batch syncs, runs
+    // k_import spilled stay in the spill area until a round is held (the next round's gathers
+    // read them there)
+    const bool defer = getenv("SGN_LOCAL_DEFER") && atoi(getenv("SGN_LOCAL_DEFER")) == 1;
+    bool held = false;
     for (uint32_t i = 0; i < n; i++) {
-      int rc = ctrl_sync(ctxs[i]);
-      if (!rc) rc = resolve_pools(ctxs[i]);
-      if (rc) return rc;
+      if (int rc = ctrl_sync(ctxs[i])) return rc;
+      held = held || ctxs[i]->h_ctrl->hold;
     }
+    for (uint32_t i = 0; i < n && (held || !defer); i++)
+      if (int rc = resolve_pools(ctxs[i])) return rc;
   }
   if (rounds_done) *rounds_done = done;
   return 0;

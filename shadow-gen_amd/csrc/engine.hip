@@ -362,10 +362,15 @@ __host__ __device__ __forceinline__ size_t exec_lds_runs_bytes(uint32_t cap) {
 // the record at once.
 // Its size is per kernel: 40 records for TGEN (config C: ~100 of 1563 server groups send more
 // than 24 records a round, up to ~90; same-box A/B 24 -> 40: -0.5 % per launch, and 40 still
-// leaves C at 7 workgroups per CU), 24 for the others (config D's PERIODIC kernel is at 8
-// workgroups per CU with 512 B of LDS to spare).
+// leaves C at 7 workgroups per CU), 32 for PERIODIC (config D: all 64 lanes send every round,
+// those past the outbox each pay a returning slab atomic in the sending lane's chain; D's
+// kernel must keep 8 workgroups per CU WITH its bucket-minimum table (256 buckets): 32 records
+// need 20356 of 20480 B; at 48 the table no longer fit and D ran 3.4x slower), 24 for EXTERNAL.
 template <uint32_t kApp>
-constexpr uint32_t kObox = kApp == SGN_TRAFFIC_TGEN ? 40 : 24;
+#ifndef SGN_OBOX_PERIODIC
+#define SGN_OBOX_PERIODIC 32
+#endif
+constexpr uint32_t kObox = kApp == SGN_TRAFFIC_TGEN ? 40 : kApp == SGN_TRAFFIC_PERIODIC ? SGN_OBOX_PERIODIC : 24;
 struct OutboxHdr {
   uint32_t n;          // records appended (may exceed the outbox: those were placed directly)
   uint64_t xmin;       // earliest run exported to another shard this round (multi-shard)
@@ -2455,7 +2460,11 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       loaded = true;
     }
     // more runs than the LDS holds: the big-slab path (ordered and executed in pieces)
+#ifdef SGN_EXP_NOBIG  // cost experiment only (build_exp.sh): the big-slab path compiled out
+    const bool big = false;
+#else
     const bool big = nraw > S.CAP;
+#endif
     const uint32_t n = min(nraw, S.CAP);
     uint32_t N = 0;
     if (!big) {
@@ -3660,9 +3669,11 @@ int relayout_calendar(sgn_ctx* ctx) {
       hot_old.push_back(i);
       max_oecap = std::max(max_oecap, oecap(i));
     }
-    const uint64_t need = std::max<uint64_t>(fill[i], had);
+    // (a slab that fits the slab capacity or what it had keeps that; one that outgrew both gets
+    // 1.5x its fill — growth follows the fill, not the number of re-layouts)
+    const uint64_t need = fill[i] <= std::max<uint64_t>(had, cap) ? had : fill[i] + fill[i] / 2;
     if (need <= cap) continue;
-    const uint64_t e = ((need + need / 2 - cap) + 63) / 64 * 64;
+    const uint64_t e = ((need - cap) + 63) / 64 * 64;
     if (e >= (1ULL << 24))
       return set_error(ctx, SGN_EOVERFLOW, "a calendar slab above 2^24 runs (slab " + std::to_string(i) + ", fill " +
                                                std::to_string(fill[i]) + ", had " + std::to_string(had) + ", cap " +

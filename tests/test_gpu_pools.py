@@ -184,12 +184,16 @@ def test_hot_slab_beyond_lds(ctxf, oracle):
     assert_same_run(o, c, n, trace=False)
 
 
-def test_hot_slab_two_shards(ctxf, oracle, monkeypatch):
+@pytest.mark.parametrize("defer", ["0", "1"])
+def test_hot_slab_two_shards(ctxf, oracle, monkeypatch, defer):
     """The multi-shard device path with hot slabs: servers in shard 0, clients in both, so the
     requests of shard 1's clients reach the servers' slabs through k_import (local shard-group
-    transport); identical to one unsharded shard."""
+    transport); identical to one unsharded shard. defer = 1: runs k_import spilled past a slab
+    stay in the spill area until a round is held, as between the RCCL transport's batch syncs,
+    so the next round's gathers read them there (the big-slab path's spill scan)."""
     monkeypatch.setenv("SGN_SLAB_CAP", "16")
     monkeypatch.setenv("SGN_SLAB_LIM", "32")
+    monkeypatch.setenv("SGN_LOCAL_DEFER", defer)
     n = 1200
     args = _hot_args(n)
     g, used, hosts, cfg, tr = args

@@ -86,3 +86,17 @@ def test_round_kernel_lds_budget():
         if "k_rounds" in name:
             total = m["group_segment_fixed_size"] + 64 * 32 + 2 * 64 * 2
             assert -(-total // 512) * 512 * 7 <= 160 * 1024, (name, m, total)
+
+
+@pytest.mark.skipif(not pathlib.Path("/opt/rocm/lib/llvm/bin/clang-offload-bundler").exists(),
+                    reason="ROCm LLVM tools absent")
+def test_periodic_round_kernel_lds_budget():
+    # config D's persistent grid needs 8 workgroups per CU WITH the LDS bucket-minimum table
+    # (256 buckets, 128-run slabs): without the table its ~1 M sends a round serialise on a few
+    # bucket words (round 4: a 48-record outbox pushed the table out and D ran 3.4x slower)
+    meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
+    for name, m in meta.items():
+        if "k_roundsILj1E" in name:  # SGN_TRAFFIC_PERIODIC
+            runs = 128 * 32 + 2 * 128 * 2
+            total = m["group_segment_fixed_size"] + max(runs, 1024) + 257 * 4
+            assert -(-total // 512) * 512 * 8 <= 160 * 1024, (name, m, total)
