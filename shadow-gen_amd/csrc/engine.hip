@@ -362,13 +362,12 @@ __host__ __device__ __forceinline__ size_t exec_lds_runs_bytes(uint32_t cap) {
 // the record at once.
 // Its size is per kernel: 40 records for TGEN (config C: ~100 of 1563 server groups send more
 // than 24 records a round, up to ~90; same-box A/B 24 -> 40: -0.5 % per launch, and 40 still
-// leaves C at 7 workgroups per CU), 32 for PERIODIC (config D: all 64 lanes send every round,
-// those past the outbox each pay a returning slab atomic in the sending lane's chain; D's
-// kernel must keep 8 workgroups per CU WITH its bucket-minimum table (256 buckets): 32 records
-// need 20356 of 20480 B; at 48 the table no longer fit and D ran 3.4x slower), 24 for EXTERNAL.
+// leaves C at 7 workgroups per CU), 24 for the others (config D's PERIODIC kernel must keep 8
+// workgroups per CU WITH its bucket-minimum table of 256 buckets: at 48 records the table no
+// longer fit and D ran 3.4x slower; 32 measured the same as 24, round 4).
 template <uint32_t kApp>
 #ifndef SGN_OBOX_PERIODIC
-#define SGN_OBOX_PERIODIC 32
+#define SGN_OBOX_PERIODIC 24
 #endif
 constexpr uint32_t kObox = kApp == SGN_TRAFFIC_TGEN ? 40 : kApp == SGN_TRAFFIC_PERIODIC ? SGN_OBOX_PERIODIC : 24;
 struct OutboxHdr {
@@ -475,6 +474,20 @@ struct LaneLDS : std::conditional_t<kApp == SGN_TRAFFIC_PERIODIC, LaneNoCq, Lane
   uint32_t rn[3];    // ... and their counts
 };
 
+// A slab with more due runs than the LDS holds (a hot spot: thousands of sources sending to one
+// host group within a bucket width) is ordered and executed in pieces of at most CAP runs in
+// Shadow's key order: piece k holds the runs with keys in (bound k-1, bound k]. The piece state
+// lives in LDS across the pieces' event loops (registers are the round kernel's scarce resource:
+// nothing of it is live in registers across HostExec::run, which reads the piece's tail time
+// and flush flag from here — INVALID and 1 outside the big-slab path).
+struct BigLDS {
+  uint64_t tmin, range;  // earliest due run's time, latest - earliest
+  uint64_t kp[3];        // the last piece's upper bound (BigKey)
+  uint64_t ib;           // the slab
+  uint64_t tail;         // run(): a host's next packet time after its runs of this piece
+  uint32_t ndue, done, have_prev, nraw, flush, pad;
+};
+
 // kTrace: the per-packet trace can be on (k_execute). The persistent k_rounds is built
 // without it (its registers are fully used; a traced run executes round by round).
 // kApp: the traffic kind (SGN_TRAFFIC_*), fixed per instantiation so that each kernel
@@ -520,26 +533,35 @@ struct HostExec {
   SGN_GLB HostRec* R;     // this host's record (set by load())
   const uint16_t* bslab;  // LDS copy of the bucket -> slab table (when NB <= LDS_BSLAB)
   Outbox<kApp>* ob;       // the wave's outbox (LDS)
+  const BigLDS* bg;       // the big-slab piece state (LDS)
 #ifdef SGN_DIAG
   uint32_t dgt[DGT_N];
   uint32_t wk[5];
 #endif
 
   __device__ HostExec(const DevSim& s, uint32_t hh, uint64_t w, uint32_t bucket1, uint32_t ks,
-                      LaneLDS<kApp>* l, const uint16_t* bs, Outbox<kApp>* o)
-      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o) {}
+                      LaneLDS<kApp>* l, const uint16_t* bs, Outbox<kApp>* o, const BigLDS* b)
+      : S(s), C(s.ctrl), h(hh), now(0), we(w), b1(bucket1), keep_slab(ks), L(l), bslab(bs), ob(o), bg(b) {}
 
   // the host's state into registers (once per round, only for hosts with something due);
   // fresh = false: a reload after park() (the pending digest runs in LDS continue)
   __device__ __forceinline__ void load(bool fresh = true) {
     R = S.hrec + h;
     const HostRec& r = *R;
-    const HostConst& k = S.hconst[h];
-    gid = k.gid;
-    my_ip = k.ip;
-    my_unode = k.unode;
-    lr().tbc[0] = k.tb_inc[0];
-    lr().tbc[1] = k.tb_inc[1];
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+      const HostConst& k = S.hconst[h];
+      gid = k.gid;
+      my_ip = k.ip;
+      my_unode = k.unode;
+      lr().tbc[0] = k.tb_inc[0];
+      lr().tbc[1] = k.tb_inc[1];
+    } else {  // (in the cold lines these kinds read anyway)
+      gid = r.k_gid;
+      my_ip = r.k_ip;
+      my_unode = r.k_unode;
+      lr().tbc[0] = r.k_tbinc[0];
+      lr().tbc[1] = r.k_tbinc[1];
+    }
     // the hot line
     r0 = r.rng[0];
     r1 = r.rng[1];
@@ -602,7 +624,7 @@ struct HostExec {
     }
     c_sent = c_loss = c_popped = c_deliv = c_localev = c_bytes = 0;
     c_runs = 0;
-    c_maxcodel = 0;
+    c_maxcodel = kApp == SGN_TRAFFIC_PERIODIC ? 0u : r.max_codel;
     hd_valid = tl_open = false;
     if (cq_nr > 0) {
       L->hd = ld_dev_cq(cq_head_slot());
@@ -714,13 +736,21 @@ struct HostExec {
         r.cq_prev = L->cq[3];
       }
     }
-    // the per-host totals: no-return adds (no load of the old value)
-    const size_t nH = S.nH;
-    if (c_sent) cnt_add(&S.n_cnt[N_SENT * nH + h], c_sent);
-    if (c_popped) cnt_add(&S.n_cnt[N_POPPED * nH + h], c_popped);
-    if (c_deliv) cnt_add(&S.n_cnt[N_DELIVERED * nH + h], c_deliv);
-    if (c_maxcodel)
-      (void)__hip_atomic_fetch_max(&S.maxq[h], c_maxcodel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the per-host totals: PERIODIC no-return adds into dense arrays (no load of the old
+    // value, no cold line); the other kinds in their cold lines
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+      const size_t nH = S.nH;
+      if (c_sent) cnt_add(&S.n_cnt[N_SENT * nH + h], c_sent);
+      if (c_popped) cnt_add(&S.n_cnt[N_POPPED * nH + h], c_popped);
+      if (c_deliv) cnt_add(&S.n_cnt[N_DELIVERED * nH + h], c_deliv);
+      if (c_maxcodel)
+        (void)__hip_atomic_fetch_max(&S.maxq[h], c_maxcodel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      r.max_codel = c_maxcodel;
+      r.n_sent += c_sent;
+      r.n_popped += c_popped;
+      r.n_delivered += c_deliv;
+    }
     S.nextloc[h] = next_local_time();
     if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
     if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
@@ -1812,14 +1842,14 @@ struct HostExec {
   // time < until. A window is executed as consecutive sub-windows (one per calendar
   // bucket): nothing created inside a window is due in it (packet deliveries are >= the
   // window end, worker.rs:386-390), so this is the same sequence of events.
-  // tail: the time of the host's next packet run after ev[ord[s1 - 1]] (INVALID: none) — a
+  // bg->tail: the time of the host's next packet run after ev[ord[s1 - 1]] (INVALID: none) — a
   // slab ordered in pieces (exec_group's big-slab path) runs a host's runs over several calls,
-  // each up to the next piece's first time; flush: close the digests' pending runs (the last
+  // each up to the next piece's bound; bg->flush: close the digests' pending runs (the last
   // piece of the sub-window only, so the digest steps are those of one call over all runs)
   __device__ __forceinline__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
-                      uint64_t until, uint64_t tail, bool flush) {
+                      uint64_t until) {
     uint32_t pi = s0;
-    uint64_t pt = pi < s1 ? ev[ord[pi]].time : tail;  // next due packet run's time
+    uint64_t pt = pi < s1 ? ev[ord[pi]].time : bg->tail;  // next due packet run's time
 #ifdef SGN_DIAG
 #endif
     while (true) {
@@ -1856,7 +1886,7 @@ struct HostExec {
         if (pi < s1 && pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           const EvRec& e = ev[ord[pi]];
           pi++;
-          pt = pi < s1 ? ev[ord[pi]].time : tail;  // the next run's time, ahead of need
+          pt = pi < s1 ? ev[ord[pi]].time : bg->tail;  // the next run's time, ahead of need
           now = e.time;
           if (external() && e.src == gid) {  // a CPU application's datagram (sgn_submit)
             app_submit(e);
@@ -1912,7 +1942,7 @@ struct HostExec {
       forward_out_step();
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
-    if (flush) flush_digests();
+    if (bg->flush) flush_digests();
   }
   __device__ __forceinline__ void flush_digests() {
     dr_flush_same<0>();
@@ -2092,15 +2122,7 @@ struct ExecLDS {
   uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
   struct BigLDS* big; // a big slab's piece state (exec_group)
 };
-// A slab with more due runs than the LDS holds (a hot spot: thousands of sources sending to one
-// host group within a bucket width) is ordered and executed in pieces of at most CAP runs in
-// Shadow's key order: piece k holds the runs with keys in (bound k-1, bound k]. The piece state
-// lives in LDS across the pieces' event loops (registers are the round kernel's scarce resource).
-struct BigLDS {
-  uint64_t tmin, range;  // earliest due run's time, latest - earliest
-  uint64_t kp[3];        // the last piece's upper bound (BigKey)
-  uint32_t ndue, done, have_prev, pad;
-};
+
 
 // One group (2^gsh consecutive hosts, one per lane) through the window [ws, we):
 //  1. gather: the group's slabs of the window's buckets are read; runs due in the window go
@@ -2114,7 +2136,7 @@ struct BigLDS {
 // at_end(kmin, next) runs once the group's cross-workgroup data (calendar records, slab
 // fills, minima) is issued and before the host records are written back: the round's
 // arrival goes there, so its wait covers only what other workgroups read.
-template <bool kTrace, uint32_t kApp, typename AtEnd>
+template <bool kTrace, uint32_t kApp, bool kBig, typename AtEnd>
 __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
                            const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out,
                            AtEnd&& at_end) {
@@ -2155,7 +2177,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     ob->hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
   }
   __syncthreads();
-  HostExec<kTrace, kApp> ex(S, h, we, be, ks, lslot + lane, lbs, ob);
+  HostExec<kTrace, kApp> ex(S, h, we, be, ks, lslot + lane, lbs, ob, X.big);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -2283,7 +2305,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   };
   // first pass: the later runs of the window's last bucket move to the spare slab set; the due
   // runs' count and time range go to the piece state
-  auto big_prepare = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, bool last) {
+  auto big_prepare = [&](size_t ib, uint32_t nraw, bool last) {
+    SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
     uint64_t tmin = INVALID, tmax = 0;
     uint32_t nd = 0;
     big_scan(ib, pb, nraw, [&](const EvRec& r, bool ok, uint64_t) {
@@ -2303,6 +2326,9 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       X.big->ndue = nd;
       X.big->done = 0;
       X.big->have_prev = 0;
+      X.big->ib = ib;
+      X.big->nraw = nraw;
+      X.big->pad = last ? 1u : 0u;  // (the window's last bucket)
     }
     __syncthreads();
   };
@@ -2312,9 +2338,12 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   // holding at most CAP of the remaining keys, taken at the first digit where it holds at least
   // half of what is still wanted. Returns true for the last piece; else *bound_t = the bound's
   // time part: the piece's runs are at or before it, every later run at or after it.
-  auto big_piece = [&](size_t ib, SGN_GLB const EvRec* pb, uint32_t nraw, bool last, uint32_t& N,
-                       uint64_t* bound_t) -> bool {
+  auto big_piece = [&](uint32_t& N) -> bool {
     BigLDS& B = *X.big;
+    const size_t ib = uni64(B.ib);
+    const uint32_t nraw = uni32(B.nraw);
+    const bool last = uni32(B.pad) != 0;
+    SGN_GLB const EvRec* pb = S.pool + ib * S.CAP;
     const uint64_t tmin = uni64(B.tmin);
     const bool have = uni32(B.have_prev) != 0;
     const BigKey kp = {uni64(B.kp[0]), uni64(B.kp[1]), uni64(B.kp[2])};
@@ -2384,30 +2413,32 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       if (sel && N + lanes_below(m) < S.CAP) lev[N + lanes_below(m)] = r;
       N += (uint32_t)__popcll(m);
     });
+    bool bad = false;
     if (N > S.CAP || (!fin && N == 0)) {  // (cannot happen: the select bounds every piece by
       // CAP and takes at least one run) never silent, and the pieces end
       if (lane == 0 && (atomicOr(&C->overflow, OVF_SEG) & OVF_SEG) == 0) C->overflow_info = gbase;
       N = min(N, S.CAP);
-      B.done = B.ndue;
-      return true;
+      bad = true;
     }
-    if (fin) {
+    if (fin || bad) {
       // runs taken from the spill area are tagged done (the re-layout must not file them again)
       big_scan(ib, pb, nraw, [&](const EvRec&, bool ok, uint64_t si) {
         if (ok && si != ~0ULL) st_dev(&S.spill_idx[si], SPILL_DEAD);
       });
-    } else {
-      *bound_t = uni64(kt.hi > EMU_MAX - tmin ? EMU_MAX : tmin + kt.hi);
     }
     __syncthreads();
     if (lane == 0) {
-      B.done += N;
+      B.done = bad ? B.ndue : B.done + N;
       B.have_prev = 1;
       B.kp[0] = kt.hi;
       B.kp[1] = kt.mid;
       B.kp[2] = kt.lo;
+      // the host's runs of this piece end at the bound's time T: every later run is at or after it
+      B.tail = fin || bad ? INVALID : (kt.hi > EMU_MAX - tmin ? EMU_MAX : tmin + kt.hi);
+      B.flush = fin || bad ? 1u : 0u;
     }
-    return fin;
+    __syncthreads();
+    return fin || bad;
   };
   auto slab_done = [&](size_t ib, uint32_t n) {
     if (lane == 0) {
@@ -2448,8 +2479,8 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       r0 = ld_dev_rec(pb + lane);
       if (pair) r1 = ld_dev_rec(pb1 + lane);
     }
-    const uint32_t nraw = uni32(ld_dev(&S.slab_n[ib]));
-    const uint32_t n1raw = pair ? uni32(ld_dev(&S.slab_n[ib1])) : 0u;
+    const uint32_t nraw_v = ld_dev(&S.slab_n[ib]);
+    const uint32_t n1raw_v = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
     // PERIODIC traffic (configs B and D: most executed hosts have their app timer due): the
     // host record of a lane whose local event is due in the window loads in the same round trip
     // as the gather, and the app's next route is prefetched behind the sort
@@ -2459,12 +2490,14 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       ex.prefetch_peer(np);
       loaded = true;
     }
-    // more runs than the LDS holds: the big-slab path (ordered and executed in pieces)
-#ifdef SGN_EXP_NOBIG  // cost experiment only (build_exp.sh): the big-slab path compiled out
-    const bool big = false;
-#else
-    const bool big = nraw > S.CAP;
-#endif
+    // (scalar copies after the host record's loads are issued: a readfirstlane waits for its load)
+    const uint32_t nraw = uni32(nraw_v), n1raw = uni32(n1raw_v);
+    // more runs than the LDS holds: the big-slab path (ordered and executed in pieces). The
+    // kernels without it (kBig false: no slab extension exists, so a run past CAP went to the
+    // spill area and the round edge held for the re-layout before the slab could be due) never
+    // see one; if one did, it is an overflow, not a silent truncation.
+    const bool big = kBig && nraw > S.CAP;
+    if (!kBig && nraw > S.CAP && lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_BUCKET);
     const uint32_t n = min(nraw, S.CAP);
     uint32_t N = 0;
     if (!big) {
@@ -2480,19 +2513,23 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
         last = true;
         sub_end = we;
       }
+      if (lane == 0) {  // one pass: no later packet run, digests close with it
+        X.big->tail = INVALID;
+        X.big->flush = 1;
+      }
+    } else {
+      park();
+      big_prepare(ib, nraw, last);
+      slab_done(ib, nraw);
     }
     for (bool first = true;; first = false) {  // pieces (one unless big)
-      uint64_t until = sub_end, tail = INVALID;
+      uint64_t until = sub_end;
       bool fin = true;
       if (big) {
-        park();
-        if (first) {
-          big_prepare(ib, pb, nraw, last);
-          slab_done(ib, nraw);
-        }
+        if (!first) park();
         lcnt[lane] = 0;
-        fin = big_piece(ib, pb, nraw, last, N, &tail);
-        if (!fin) until = tail;
+        fin = big_piece(N);
+        if (!fin) until = uni64(X.big->tail);
         n_pieces++;
         if (loaded) ex.load(false);
       }
@@ -2545,7 +2582,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       loaded = true;
     }
     const uint64_t tb = __builtin_amdgcn_s_memtime();
-    if (go) ex.run(lev, lc, start, start + cnt, until, tail, fin);
+    if (go) ex.run(lev, lc, start, start + cnt, until);
     const uint64_t tc = __builtin_amdgcn_s_memtime();
     w_load += tb - ta;
     w_run += tc - tb;
@@ -2556,7 +2593,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
         ex.load();
         loaded = true;
       }
-      ex.run(lev, lc, start, start + cnt, until, tail, fin);
+      ex.run(lev, lc, start, start + cnt, until);
     }
 #endif
     // a big slab's host that ran in an earlier piece closes its digest runs with the last one
@@ -2771,7 +2808,7 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
   __syncthreads();
   uint64_t kmin, m;
   bool last = false;
-  exec_group<kTrace, kApp>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
+  exec_group<kTrace, kApp, true>(S, blockIdx.x, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
     flush_bmin<kApp>(S, X);
     last = arrive(S, blockIdx.x, gridDim.x, k, n, od);
   });
@@ -2918,7 +2955,9 @@ __device__ __forceinline__ void rb_bookkeep(const DevSim& S, uint64_t ws, uint64
 // with one CU). Data another workgroup wrote in this launch is read with device-scope loads
 // (event records, slab fills, bucket minima, the round buffers); the rest (host records,
 // queues) belongs to this workgroup's groups.
-template <uint32_t kApp>
+// kBig: compiled with the big-slab path (launched while some slab has an extension; without
+// one, the path's code cost config C 2.6 % per launch in same-box A/B, round 4)
+template <uint32_t kApp, bool kBig>
 __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds) {
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
@@ -3033,7 +3072,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     for (uint32_t g = w; g < S.G; g += P) {
       uint64_t kmin, m;
       const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
-      exec_group<false, kApp>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
+      exec_group<false, kApp, kBig>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
         oall += od;
@@ -3463,11 +3502,15 @@ const void* execute_fn_t(uint32_t kind) {
 const void* execute_fn(uint32_t kind, bool trace) {
   return trace ? execute_fn_t<true>(kind) : execute_fn_t<false>(kind);
 }
-const void* rounds_fn(uint32_t kind) {
-  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_rounds<SGN_TRAFFIC_TGEN>;
-  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_rounds<SGN_TRAFFIC_EXTERNAL>;
-  return (const void*)k_rounds<SGN_TRAFFIC_PERIODIC>;
+template <bool kBig>
+const void* rounds_fn_t(uint32_t kind) {
+  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_rounds<SGN_TRAFFIC_TGEN, kBig>;
+  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_rounds<SGN_TRAFFIC_EXTERNAL, kBig>;
+  return (const void*)k_rounds<SGN_TRAFFIC_PERIODIC, kBig>;
 }
+// the persistent kernel with the big-slab path only while a slab can hold more than CAP runs
+bool rounds_big(const sgn_ctx* ctx) { return ctx->ext_slabs > 0; }
+const void* rounds_fn(uint32_t kind, bool big) { return big ? rounds_fn_t<true>(kind) : rounds_fn_t<false>(kind); }
 template <bool kTrace>
 void launch_k_execute_t(sgn_ctx* ctx, hipStream_t st) {
   const uint32_t k = ctx->S.tkind;
@@ -3487,17 +3530,24 @@ void launch_k_execute(sgn_ctx* ctx, hipStream_t st) {
   else
     launch_k_execute_t<false>(ctx, st);
 }
-void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
+template <bool kBig>
+void launch_k_rounds_t(sgn_ctx* ctx, uint32_t n) {
   const uint32_t k = ctx->S.tkind;
   const dim3 grid(ctx->persist_grid), block(64);
   const size_t lds = exec_lds_bytes(ctx->S.CAP, ctx->S.agg_bmin ? ctx->S.NB : 0);
   const DevSim* d = (const DevSim*)ctx->d_S;
   if (k == SGN_TRAFFIC_TGEN)
-    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_TGEN>, grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_TGEN, kBig>), grid, block, lds, ctx->stream, d, n);
   else if (k == SGN_TRAFFIC_EXTERNAL)
-    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_EXTERNAL>, grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_EXTERNAL, kBig>), grid, block, lds, ctx->stream, d, n);
   else
-    hipLaunchKernelGGL(k_rounds<SGN_TRAFFIC_PERIODIC>, grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_PERIODIC, kBig>), grid, block, lds, ctx->stream, d, n);
+}
+void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
+  if (rounds_big(ctx))
+    launch_k_rounds_t<true>(ctx, n);
+  else
+    launch_k_rounds_t<false>(ctx, n);
 }
 
 int launch_round(sgn_ctx* ctx) {
@@ -3549,7 +3599,7 @@ uint32_t max_slab_capacity(sgn_ctx* ctx, const DevSim& S) {
       per_block <= 0)
     per_block = 64 * 1024;
   size_t st = 0;
-  for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind, S.trace_on)}) {
+  for (const void* fn : {rounds_fn(S.tkind, false), rounds_fn(S.tkind, true), execute_fn(S.tkind, S.trace_on)}) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, fn) == hipSuccess) st = std::max<size_t>(st, fa.sharedSizeBytes);
   }
@@ -3572,7 +3622,7 @@ uint32_t max_slab_capacity(sgn_ctx* ctx, const DevSim& S) {
 void size_round_kernels(sgn_ctx* ctx, DevSim& S) {
   const uint64_t G = S.G, NB = S.NB;
   bool agg = S.tkind == SGN_TRAFFIC_PERIODIC;  // the kernels fold in LDS for PERIODIC traffic (kAggBmin)
-  for (const void* fn : {rounds_fn(S.tkind), execute_fn(S.tkind, S.trace_on)}) {
+  for (const void* fn : {rounds_fn(S.tkind, false), rounds_fn(S.tkind, true), execute_fn(S.tkind, S.trace_on)}) {
     const uint64_t r0 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP)), r1 = resident_wg(ctx, fn, exec_lds_bytes(S.CAP, S.NB));
     if (!r0 || std::min<uint64_t>(G, r1) < std::min<uint64_t>(G, r0)) agg = false;
   }
@@ -3582,7 +3632,9 @@ void size_round_kernels(sgn_ctx* ctx, DevSim& S) {
   ctx->persist_grid = 0;
   if (ctx->nranks == 1 && NB <= LDS_BSLAB && !S.trace_on && !ctx->persist_off &&
       !(getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0)) {
-    const uint64_t res = resident_wg(ctx, rounds_fn(S.tkind), exec_lds_bytes(S.CAP, S.agg_bmin ? S.NB : 0));
+    // (resident for either variant: a re-layout that adds slab extensions switches to kBig)
+    const size_t lds = exec_lds_bytes(S.CAP, S.agg_bmin ? S.NB : 0);
+    const uint64_t res = std::min(resident_wg(ctx, rounds_fn(S.tkind, false), lds), resident_wg(ctx, rounds_fn(S.tkind, true), lds));
     if (res) {
       ctx->persist_grid = (uint32_t)std::min<uint64_t>(G, res);
       // test hook: a smaller grid makes every workgroup serve several groups per round
@@ -4156,9 +4208,9 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     const uint32_t g = ctx->host_of[h];
     HostRec& r = recs[h];
     HostConst& k = hk[h];
-    k.gid = g;
-    k.ip = ctx->ip[g];
-    k.unode = ctx->unode[g];
+    k.gid = r.k_gid = g;
+    k.ip = r.k_ip = ctx->ip[g];
+    k.unode = r.k_unode = ctx->unode[g];
     // Xoshiro256PlusPlus::seed_from_u64 (SplitMix64 fill), host.rs:234
     uint64_t sm = ctx->seed[g];
     for (int i = 0; i < 4; i++) r.rng[i] = host_splitmix(sm);
@@ -4167,7 +4219,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     for (int w = 0; w < 2; w++) {
       const uint64_t bps = (w == 0 ? ctx->bw_up[g] : ctx->bw_down[g]) / 8;
       const uint64_t inc = std::max<uint64_t>(1, bps / 1000);
-      k.tb_inc[w] = inc;  // (capacity = inc + MTU, the bucket starts full)
+      k.tb_inc[w] = r.k_tbinc[w] = inc;  // (capacity = inc + MTU, the bucket starts full)
       r.tb_bal[w] = inc + SGN_CONFIG_MTU;
       r.tb_last[w] = SIM_START;
     }
@@ -4574,6 +4626,17 @@ int read_counts(sgn_ctx* ctx, uint32_t off, uint32_t n, std::vector<uint64_t>* c
   cnt->assign((size_t)N_CNT * n, 0);
   if (mq) mq->assign(n, 0);
   if (!n) return 0;
+  if (ctx->S.tkind != SGN_TRAFFIC_PERIODIC) {  // (these kinds keep them in the cold lines)
+    std::vector<HostRec> recs;
+    if (int e = read_recs(ctx, off, n, &recs)) return e;
+    for (uint32_t i = 0; i < n; i++) {
+      (*cnt)[(size_t)N_SENT * n + i] = recs[i].n_sent;
+      (*cnt)[(size_t)N_POPPED * n + i] = recs[i].n_popped;
+      (*cnt)[(size_t)N_DELIVERED * n + i] = recs[i].n_delivered;
+      if (mq) (*mq)[i] = recs[i].max_codel;
+    }
+    return 0;
+  }
   for (int k = 0; k < N_CNT; k++)
     SGN_HIP(ctx, hipMemcpy(cnt->data() + (size_t)k * n, (const void*)(ctx->S.n_cnt + k * nH + off), (size_t)n * 8,
                            hipMemcpyDeviceToHost));

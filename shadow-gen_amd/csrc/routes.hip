@@ -272,6 +272,165 @@ __global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_
   if (__ballot(ch) && (threadIdx.x & 63) == 0) flag[it] = 1;
 }
 
+// sq_init + sq_edges for a graph whose arcs are in tail order (CSR): one workgroup per row u
+// builds d[u][.] in LDS (the diagonal 0, each arc's latency by LDS atomic min: parallel
+// arcs keep the shortest) and writes it whole — no global atomics, one coalesced row write.
+__global__ __launch_bounds__(256) void sq_rows(uint32_t* D, uint32_t Vp, uint32_t V, const uint32_t* rowptr,
+                                               const uint32_t* auv, const uint64_t* al) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* row = (uint32_t*)smem;
+  const uint32_t u = blockIdx.x;
+  for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) row[v] = v == u ? 0u : SQ_INF;
+  __syncthreads();
+  if (u < V)
+    for (uint32_t e = rowptr[u] + threadIdx.x; e < rowptr[u + 1]; e += blockDim.x)
+      atomicMin(&row[auv[e] >> 16], (uint32_t)al[e]);  // (< 2^32 - 1: the fast form's bound)
+  __syncthreads();
+  for (uint32_t v = 4 * threadIdx.x; v < Vp; v += 4 * blockDim.x)
+    *(uint4*)&D[(uint64_t)u * Vp + v] = *(const uint4*)&row[v];
+}
+
+// All squaring passes in ONE launch (one shard): a 1024-thread workgroup per 64 x 64 output tile
+// (looping over tiles when they outnumber the CUs) whose four 256-thread slices each take a
+// quarter of K (16 waves per CU: sq_pass's 256 tiles left one wave per SIMD and ran at ~1/3 of
+// the VALU rate), the slices' minima folded in LDS; each slice's next K step is loaded into
+// registers while the current one is computed. A pass ends at a grid barrier (every workgroup
+// resident: the grid is at most one workgroup per CU; stores drained, agent release, counter,
+// agent acquire), and the launch ends after the first pass that changed nothing — a graph whose
+// edges already are its shortest paths (config C's Tor graph) pays one pass and one barrier
+// instead of ceil(log2 V) + 1 launches. *err: a barrier timed out (the host redoes the phase
+// with sq_pass).
+constexpr int SQR_SL = 4;                                   // K slices per workgroup
+constexpr size_t SQR_LDS = 2ull * SQR_SL * SQ_K * (SQ_T + 4) * 4;  // As + Bs per slice
+__global__ __launch_bounds__(1024) void sq_run(uint32_t* D, uint32_t Vp, uint32_t* flag, uint32_t max_pass,
+                                               uint32_t* err, uint32_t* bar) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef uint32_t Tile[SQ_K][SQ_T + 4];
+  Tile* As = (Tile*)smem;
+  Tile* Bs = As + SQR_SL;
+  uint32_t* red = (uint32_t*)smem;  // [64][64] after a tile's K loop (As[0..1] are free then)
+  __shared__ uint32_t go;
+  const uint32_t sl = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int tx = t & 15, ty = t >> 4;
+  const uint32_t nt = Vp / SQ_T, ntiles = nt * nt;
+  const uint32_t nsteps = Vp / SQ_K, per = (nsteps + SQR_SL - 1) / SQR_SL;
+  const uint32_t s_first = sl * per;
+  for (uint32_t it = 0; it < max_pass; it++) {
+    bool ch = false;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      const uint64_t r0 = (uint64_t)(tile / nt) * SQ_T, c0 = (uint64_t)(tile % nt) * SQ_T;
+      uint32_t acc[4][4], orig[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = orig[i][j] = SQ_INF;
+      if (sl == 0)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint4 v = *(const uint4*)&D[(r0 + ty * 4 + i) * Vp + c0 + tx * 4];
+          acc[i][0] = orig[i][0] = v.x;
+          acc[i][1] = orig[i][1] = v.y;
+          acc[i][2] = orig[i][2] = v.z;
+          acc[i][3] = orig[i][3] = v.w;
+        }
+      // step s's operands, thread t's share: A = D[r0 .. +64][k0 .. +32] (rows t / 8 and
+      // t / 8 + 32), B = D[k0 .. +32][c0 .. +64] (rows t / 16 and t / 16 + 16)
+      const uint32_t* pa = D + (r0 + (t >> 3)) * Vp + (t & 7) * 4;
+      const uint32_t* pb = D + (uint64_t)(t >> 4) * Vp + c0 + (t & 15) * 4;
+      const uint64_t a2 = 32ull * Vp, b2 = 16ull * Vp;
+      uint4 ra0 = {}, ra1 = {}, rb0 = {}, rb1 = {};
+#define SQR_LOAD(s)                                               \
+  do {                                                            \
+    const uint64_t k0_ = (uint64_t)(s) * SQ_K;                    \
+    ra0 = *(const uint4*)(pa + k0_);                              \
+    ra1 = *(const uint4*)(pa + a2 + k0_);                         \
+    rb0 = *(const uint4*)(pb + k0_ * Vp);                         \
+    rb1 = *(const uint4*)(pb + b2 + k0_ * Vp);                    \
+  } while (0)
+      if (s_first < nsteps) SQR_LOAD(s_first);
+      for (uint32_t s = 0; s < per; s++) {  // (every slice takes the same number of barriers)
+        const bool have = s_first + s < nsteps;
+        __syncthreads();  // the previous step's LDS reads (or the last tile's fold) are done
+        if (have) {
+          const int m = t >> 3, kq = (t & 7) * 4;
+          As[sl][kq][m] = ra0.x;
+          As[sl][kq + 1][m] = ra0.y;
+          As[sl][kq + 2][m] = ra0.z;
+          As[sl][kq + 3][m] = ra0.w;
+          As[sl][kq][m + 32] = ra1.x;
+          As[sl][kq + 1][m + 32] = ra1.y;
+          As[sl][kq + 2][m + 32] = ra1.z;
+          As[sl][kq + 3][m + 32] = ra1.w;
+          *(uint4*)&Bs[sl][t >> 4][(t & 15) * 4] = rb0;
+          *(uint4*)&Bs[sl][(t >> 4) + 16][(t & 15) * 4] = rb1;
+        }
+        __syncthreads();
+        if (have && s + 1 < per && s_first + s + 1 < nsteps) SQR_LOAD(s_first + s + 1);
+        if (have) {
+#pragma unroll 8
+          for (int k = 0; k < SQ_K; k++) {
+            const uint4 a = *(const uint4*)&As[sl][k][ty * 4];
+            const uint4 b = *(const uint4*)&Bs[sl][k][tx * 4];
+            const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const uint32_t s2 = __builtin_elementwise_add_sat(av[i], bv[j]);
+                acc[i][j] = s2 < acc[i][j] ? s2 : acc[i][j];
+              }
+          }
+        }
+      }
+#undef SQR_LOAD
+      // fold the slices: slice 0 (which started from the tile's entries) writes, the rest min in
+      __syncthreads();
+      if (sl == 0)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          *(uint4*)&red[(ty * 4 + i) * SQ_T + tx * 4] = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+      __syncthreads();
+      if (sl != 0)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (acc[i][j] < SQ_INF) atomicMin(&red[(ty * 4 + i) * SQ_T + tx * 4 + j], acc[i][j]);
+      __syncthreads();
+      if (sl == 0)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint4 r = *(const uint4*)&red[(ty * 4 + i) * SQ_T + tx * 4];
+          if (r.x != orig[i][0] || r.y != orig[i][1] || r.z != orig[i][2] || r.w != orig[i][3]) {
+            *(uint4*)&D[(r0 + ty * 4 + i) * Vp + c0 + tx * 4] = r;
+            ch = true;
+          }
+        }
+    }
+    // the pass's barrier: every storing wave drains, one lane releases and arrives
+    if (__ballot(ch) && (threadIdx.x & 63) == 0)
+      __hip_atomic_store(&flag[it], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t target = (it + 1) * gridDim.x;
+      uint32_t sp = 0;
+      while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++sp < (1u << 24))
+        __builtin_amdgcn_s_sleep(2);
+      if (sp >= (1u << 24)) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      go = __hip_atomic_load(&flag[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 &&
+           __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    }
+    __syncthreads();
+    if (!go) break;
+  }
+}
+
 // Latency phase for sparse graphs: one workgroup per used source relaxes the arc list over
 // its distance row in LDS (u64, 64-bit LDS atomic min) until a sweep changes nothing —
 // Bellman-Ford, exact (integer latencies, all positive), a few sweeps of a short list instead
@@ -318,6 +477,14 @@ __global__ void sq_widen(const uint32_t* D32, uint64_t* D, uint64_t n) {
 // two 4S-byte reads; arcs are 8 bytes: u | v << 16 and the u32 latency) and sweeps one P-th of the arc list; each arc load now serves S sources
 // instead of one (the single-source sweep re-read the whole arc list once per source, from
 // L2 / MALL). Tight arcs go to a per-source list in global memory (arc indices).
+// b + nl + nd as one v_add3_u32 (nd a scalar register: gfx950 VOP3 reads one SGPR); written
+// out because the compiler re-associates the sum into an add and a sub
+__device__ __forceinline__ uint32_t add3_vvs(uint32_t b, uint32_t nl, uint32_t nd) {
+  uint32_t r;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(nl), "s"(nd));
+  return r;
+}
+
 template <int S>
 __device__ __forceinline__ void sweep_arc(const uint32_t* row, uint32_t g0, uint32_t uv, uint32_t l, uint32_t e,
                                           uint32_t capg, uint32_t* tcnt, uint32_t* tlist) {
@@ -393,39 +560,70 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
                                                       uint32_t* tcnt, uint32_t* tlist) {
   static_assert(S % 4 == 0, "rows are read 4 sources at a time");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* row = (uint32_t*)smem;  // [Vp][S]
+  // S/4 planes of [Vp][4]: a lane's 16-byte read of 4 sources' d[.][v] sits at a 16-byte
+  // stride from its neighbour's (conflict-free; one [Vp][S] row put the lanes 4S bytes apart)
+  uint32_t* row = (uint32_t*)smem;
   const uint32_t g0 = blockIdx.x * S;
-  for (uint32_t i = threadIdx.x; i < Vp * S; i += blockDim.x) {
-    const uint32_t u = i / S, k = i % S;
-    row[i] = g0 + k < U ? D32[(uint64_t)usrc[g0 + k] * Vp + u] : SQ_INF;
+#pragma unroll
+  for (int k = 0; k < S; k++) {
+    const uint32_t* src = g0 + k < U ? D32 + (uint64_t)usrc[g0 + k] * Vp : nullptr;
+    for (uint32_t u = threadIdx.x; u < Vp; u += blockDim.x) row[(k >> 2) * Vp * 4 + u * 4 + (k & 3)] = src ? src[u] : SQ_INF;
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint32_t u0 = (uint32_t)((uint64_t)V * blockIdx.y / gridDim.y);
   const uint32_t u1 = (uint32_t)((uint64_t)V * (blockIdx.y + 1) / gridDim.y);
   for (uint32_t u = u0 + wave; u < u1; u += nw) {
-    uint32_t du[S];
+    uint32_t du[S], ndu[S];  // wave-uniform (u is): scalar operands of the filter below
 #pragma unroll
     for (int k = 0; k < S; k += 4) {
-      const uint4 x = *(const uint4*)(row + u * S + k);
-      du[k] = x.x;
-      du[k + 1] = x.y;
-      du[k + 2] = x.z;
-      du[k + 3] = x.w;
+      const uint4 x = *(const uint4*)(row + (k >> 2) * Vp * 4 + u * 4);
+      du[k] = __builtin_amdgcn_readfirstlane(x.x);
+      du[k + 1] = __builtin_amdgcn_readfirstlane(x.y);
+      du[k + 2] = __builtin_amdgcn_readfirstlane(x.z);
+      du[k + 3] = __builtin_amdgcn_readfirstlane(x.w);
     }
+#pragma unroll
+    for (int k = 0; k < S; k++) ndu[k] = 0u - du[k];
+    // four arcs per lane in flight (e, e + 64, e + 128, e + 192): the sweep waits on the arc
+    // loads (PMC, round 4: 84 % of its wave cycles waiting with one arc per lane)
     const uint32_t e1 = rowptr[u + 1];
-    for (uint32_t e = rowptr[u] + lane; e < e1; e += 64) {
-      const uint32_t l = al32[e];
-      if (l == SQ_INF) continue;
-      const uint32_t* dv = row + (auv[e] >> 16) * S;
+    for (uint32_t e0 = rowptr[u] + lane; e0 < e1; e0 += 256) {
+      uint32_t uv[4], l[4];
 #pragma unroll
-      for (int k = 0; k < S; k += 4) {
-        const uint4 y = *(const uint4*)(dv + k);
-        const uint32_t b[4] = {y.x, y.y, y.z, y.w};
+      for (int q = 0; q < 4; q++) {  // (clamped, unconditional loads: all eight in flight at once;
+        // 32-bit byte offsets from the scalar bases)
+        const uint32_t off = min(e0 + 64 * q, e1 - 1) * 4u;
+        uv[q] = *(const uint32_t*)((const char*)auv + off);
+        l[q] = *(const uint32_t*)((const char*)al32 + off);
+      }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          if (b[j] < du[k + j] || b[j] - du[k + j] != l) continue;
-          const uint32_t src = g0 + k + j;
+      for (int q = 0; q < 4; q++) {
+        const uint32_t v = uv[q] >> 16;
+        uint32_t b[S];
+#pragma unroll
+        for (int k = 0; k < S; k += 4) {
+          const uint4 y = *(const uint4*)(row + (k >> 2) * Vp * 4 + v * 4);
+          b[k] = y.x;
+          b[k + 1] = y.y;
+          b[k + 2] = y.z;
+          b[k + 3] = y.w;
+        }
+        // branch-free filter: b - l - du (one v_add3 with -l and the scalar -du) is 0 for every
+        // tight (source, arc) pair (and, rarely, for a wrapped one); about one pair in a thousand
+        // is tight, so the exact test below runs on a filter hit only (it also drops the clamped
+        // lanes past the tail's last arc, and arcs of 2^32 - 1 ns or more)
+        const uint32_t nl = 0u - l[q];
+        uint32_t acc = add3_vvs(b[0], nl, ndu[0]);
+#pragma unroll
+        for (int k = 1; k < S; k++) acc = min(acc, add3_vvs(b[k], nl, ndu[k]));
+        if (acc != 0) continue;
+        const uint32_t e = e0 + 64 * q;
+        if (e >= e1 || l[q] == SQ_INF) continue;
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+          if (du[k] == SQ_INF || b[k] < du[k] || b[k] - du[k] != l[q]) continue;
+          const uint32_t src = g0 + k;
           const uint32_t pos = atomicAdd(&tcnt[src], 1u);
           if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
         }
@@ -900,7 +1098,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     const uint32_t max_pass = 34;
     if (fast) {
       SGN_HIP(ctx, hipMalloc(&dD32.p, (size_t)Vp * Vp * 4));
-      SGN_HIP(ctx, hipMalloc(&dflag.p, max_pass * 4));
+      SGN_HIP(ctx, hipMalloc(&dflag.p, (max_pass + 2) * 4));  // + sq_run's timeout word and barrier counter
     }
     // the loss phase's form and buffers (allocated here, outside the timed build)
     const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
@@ -910,10 +1108,15 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     int lform = fast && !getenv("SGN_APSP_LOSS1") && lds_fold <= 160 * 1024 && E2 >= 32ull * Vp ? 1 : 0;
     int kS = 0;  // sources per sweep workgroup: the largest whose rows fit its LDS
     if (lform == 1) {
-      for (int k : {8, 4}) {
+      // (16 sources per workgroup in tail order share each arc's loads and addressing over twice
+      // the sources, but measured slower at config C's V = 1000: 179 vs 132 us, its 64 KB of rows
+      // leave 2 workgroups per CU; SGN_APSP_SWEEP_S=16 selects it, A/B)
+      const int smax = getenv("SGN_APSP_SWEEP_S") ? atoi(getenv("SGN_APSP_SWEEP_S")) : 8;
+      for (int k : {16, 8, 4}) {
         const size_t b = (size_t)Vp * k * 4;
-        if (b > 160 * 1024) continue;
-        const void* f = csr ? (k == 8 ? (const void*)loss_sweep_csr<8> : (const void*)loss_sweep_csr<4>)
+        if (b > 160 * 1024 || k > smax || (k == 16 && !csr)) continue;
+        const void* f = csr ? (k == 16 ? (const void*)loss_sweep_csr<16>
+                               : k == 8 ? (const void*)loss_sweep_csr<8> : (const void*)loss_sweep_csr<4>)
                             : (k == 8 ? (const void*)loss_sweep<8> : (const void*)loss_sweep<4>);
         if (b <= 64 * 1024 ||
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess) {
@@ -967,6 +1170,20 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     tm.shards = nsh;
     tm.shard_sources = (uint32_t)(soff[sh_last] - soff[sh_first]);
+    // one shard: all squaring passes in one launch (sq_run), unless its barrier ever timed out
+    // (the grid not resident: another context holds CUs) or SGN_APSP_SQ_PASSES=1 (A/B)
+    bool sq_one = nsh == 1 && !getenv("SGN_APSP_SQ_PASSES");
+    uint32_t n_cu = 0;
+    {
+      int c = 0;
+      if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || c <= 0) c = 0;
+      n_cu = (uint32_t)c;
+      if (!n_cu || hipFuncSetAttribute((const void*)sq_run, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)SQR_LDS) != hipSuccess) {
+        (void)hipGetLastError();
+        sq_one = false;
+      }
+    }
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
     if (bf) {  // per source: a shard's block needs no exchange until the table
@@ -979,16 +1196,24 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
     } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
-      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, max_pass * 4, st));
-      hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
-      hipLaunchKernelGGL(sq_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0,
-                         st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
-                         (int)g->directed);
+      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 2) * 4, st));
+      if (csr) {
+        hipLaunchKernelGGL(sq_rows, dim3(Vp), dim3(256), (size_t)Vp * 4, st, D32, Vp, V, (const uint32_t*)drp.p,
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p);
+      } else {
+        hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
+        hipLaunchKernelGGL(sq_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0,
+                           st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
+                           (int)g->directed);
+      }
       // ceil(log2 Vp) passes cover every simple path; one more confirms the fixed point
       uint32_t passes = 1;
       while ((1u << (passes - 1)) < Vp) passes++;
       passes = std::min(passes + 1, max_pass);
-      for (uint32_t it = 0; it < passes; it++) {
+      if (sq_one)
+        hipLaunchKernelGGL(sq_run, dim3(std::min<uint32_t>(nb * nb, n_cu)), dim3(1024), SQR_LDS, st, D32, Vp,
+                           (uint32_t*)dflag.p, passes, (uint32_t*)dflag.p + max_pass, (uint32_t*)dflag.p + max_pass + 1);
+      for (uint32_t it = 0; it < passes && !sq_one; it++) {
         for (uint32_t r = sh_first; r < sh_last; r++) {
           const uint32_t t0 = (uint32_t)toff[r], nt = (uint32_t)(toff[r + 1] - t0);
           if (nt)
@@ -1024,6 +1249,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     // graphs), then a per-source fold in LDS. Sparse graphs, the u64 form, a list overflow, or
     // SGN_APSP_LOSS1 take the one-source kernel.
     int form = lform;
+  loss_phase:
     if (form) {
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
       for (uint32_t r = sh_first; r < sh_last; r++) {
@@ -1037,7 +1263,10 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         const uint32_t* us = (const uint32_t*)dus.p + s0;
         uint32_t* tcs = (uint32_t*)dtc.p + s0;
         uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
-        if (csr && kS == 8)
+        if (csr && kS == 16)
+          hipLaunchKernelGGL(loss_sweep_csr<16>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
+                             (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
+        else if (csr && kS == 8)
           hipLaunchKernelGGL(loss_sweep_csr<8>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
                              (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
         else if (csr)
@@ -1055,15 +1284,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
-      // a source with more tight pairs than its list holds: redo the phase the one-source way
-      std::vector<uint32_t> tc(U);
-      SGN_HIP(ctx, hipMemcpyAsync(tc.data(), dtc.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
-      SGN_HIP(ctx, hipStreamSynchronize(st));
-      for (uint32_t x : tc)
-        if (x > capg) form = 0;
-    }
-    tm.loss_multi = form ? (uint32_t)kS : 0u;
-    if (!form) {
+    } else {
       for (uint32_t r = sh_first; r < sh_last; r++) {
         const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
         if (ns)
@@ -1073,6 +1294,24 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
       SGN_HIP(ctx, hipGetLastError());
       SGN_HIP(ctx, hipEventRecord(e2, st));
+    }
+    // a source with more tight pairs than its list holds: the phase is redone the one-source
+    // way. One shard checks after the extraction (no host round trip inside the timed build:
+    // ~40 us at config C); sharded builds check first, so every shard enters the table's
+    // exchange below exactly once.
+    std::vector<uint32_t> tc(form ? U : 0);
+    auto tight_over = [&]() {
+      for (uint32_t x : tc)
+        if (x > capg) return true;
+      return false;
+    };
+    if (form && rccl) {
+      SGN_HIP(ctx, hipMemcpyAsync(tc.data(), dtc.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
+      SGN_HIP(ctx, hipStreamSynchronize(st));
+      if (tight_over()) {
+        form = 0;
+        goto loss_phase;
+      }
     }
     for (uint32_t r = sh_first; r < sh_last; r++)
       if (soff[r + 1] > soff[r]) {
@@ -1092,9 +1331,16 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     unsigned long long res[3];
     SGN_HIP(ctx, hipMemcpyAsync(res, dres.p, sizeof(res), hipMemcpyDeviceToHost, st));
     SGN_HIP(ctx, hipEventRecord(e3, st));
+    if (form && !rccl) SGN_HIP(ctx, hipMemcpyAsync(tc.data(), dtc.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> its(U);
     SGN_HIP(ctx, hipMemcpyAsync(its.data(), dit.p, (size_t)U * 4, hipMemcpyDeviceToHost, st));
     SGN_HIP(ctx, hipStreamSynchronize(st));
+    if (form && !rccl && tight_over()) {
+      form = 0;
+      SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
+      goto loss_phase;
+    }
+    tm.loss_multi = form ? (uint32_t)kS : 0u;
     float ms_fw = 0, ms_loss = 0, ms_total = 0;
     hipEventElapsedTime(&ms_fw, e0, e1);
     hipEventElapsedTime(&ms_loss, e1, e2);
@@ -1114,8 +1360,14 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
               n_global, cap);
     uint32_t sq_passes = 0;
     if (fast) {
-      std::vector<uint32_t> fl(max_pass);
-      SGN_HIP(ctx, hipMemcpy(fl.data(), dflag.p, max_pass * 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> fl(max_pass + 1);
+      SGN_HIP(ctx, hipMemcpy(fl.data(), dflag.p, (max_pass + 1) * 4, hipMemcpyDeviceToHost));
+      if (sq_one && fl[max_pass]) {  // sq_run's grid barrier timed out: redo with sq_pass launches
+        fprintf(stderr, "libsgn: APSP squaring grid not resident; one launch per pass\n");
+        sq_one = false;
+        SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
+        goto latency_phase;
+      }
       while (sq_passes < max_pass && fl[sq_passes]) sq_passes++;
       sq_passes++;  // the pass that found the fixed point
     }

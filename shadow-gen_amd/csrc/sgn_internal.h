@@ -193,11 +193,17 @@ struct __attribute__((aligned(128))) HostRec {
   uint32_t cq_nr, cq_len, cq_tp;             // CoDel runs / packets / chain's tail page
   uint32_t fq_head, fq_len;                  // send queue (an empty queue's head is 0)
   uint32_t rc_dst, rc_sid, pad_c;            // route cache peer (NO_HOST: none) and its slot id
+  // TGEN / EXTERNAL (their cold lines are read and written with the hot one anyway): the
+  // constants and the per-host totals here, in the lines they already move (PERIODIC: the
+  // dense HostConst array and no-return adds into DevSim::n_cnt / maxq)
+  uint64_t k_tbinc[2];                       // = HostConst::tb_inc
+  uint32_t k_gid, k_ip, k_unode, max_codel;  // = HostConst; the largest CoDel queue length
+  uint64_t n_sent, n_popped, n_delivered;
   // rare paths only (never loaded with the state: traced runs, sgn_rng_*, no-return atomics)
   uint64_t tseq;                            // trace sequence
   uint64_t rng_pos;                         // RNG draws so far (kept while tracing, and by sgn_rng_*)
   uint64_t n_codel, n_unknown, n_local_deliv, n_blocked;
-  uint64_t pad[23];
+  uint64_t pad[16];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
 static_assert(offsetof(HostRec, st0) == 128, "line 0: the hot line");

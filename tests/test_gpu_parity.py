@@ -106,6 +106,43 @@ def test_apsp_paths_beyond_u32_fall_back(ctxf, oracle, monkeypatch):
     assert t["latency_u64"] == 0 and 1 <= t["latency_passes"] <= 8 and t["latency_bf"] == 0
 
 
+def test_apsp_squaring_one_launch_many_passes(ctxf, oracle, monkeypatch):
+    """sq_run (every squaring pass in one launch, grid barrier between passes, K split over four
+    slices per workgroup) on graphs whose direct edges are NOT their shortest paths, so several
+    passes change entries across many tiles (cross-XCD hand-offs between passes): a complete graph
+    with random latencies (CSR row build, sq_rows) and a sparse graph forced onto the squaring
+    form (V = 1000: 256 tiles, ~10 passes); against the oracle and against one launch per pass
+    (SGN_APSP_SQ_PASSES)."""
+    V = 700
+    rng = np.random.default_rng(11)
+    iu, ju = np.triu_indices(V, 1)
+    lat = rng.integers(1_000, 100_000, len(iu)).astype(np.uint64) * 1000
+    loss = np.round(rng.uniform(0, 0.01, len(iu)), 6).astype(np.float32)
+    dense = sgn.GraphArrays(np.arange(V), np.concatenate([iu, np.arange(V)]), np.concatenate([ju, np.arange(V)]),
+                            np.concatenate([lat, np.full(V, 1_000_000, np.uint64)]),
+                            np.concatenate([loss, np.zeros(V, np.float32)]), False)
+    cases = [(dense, {}), (sgn.random_graph(1000, seed=21, loss_frac=0.5), {"SGN_APSP_SQ": "1"})]
+    for k, (g, env) in enumerate(cases):
+        used = np.arange(len(g.node_id))
+        ol, op = oracle.routes(g, used)
+        passes = []
+        for one in (True, False):
+            for key, val in env.items():
+                monkeypatch.setenv(key, val)
+            if not one:
+                monkeypatch.setenv("SGN_APSP_SQ_PASSES", "1")
+            c = ctxf()
+            c.routes_build(g, used)
+            t = c.routes_timing()
+            for key in list(env) + ([] if one else ["SGN_APSP_SQ_PASSES"]):
+                monkeypatch.delenv(key)
+            gl, gp = c.routes_copy()
+            assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), (k, one)
+            assert t["latency_bf"] == 0 and t["latency_u64"] == 0, (k, t)
+            passes.append(t["latency_passes"])
+        assert min(passes) >= 2, (k, passes)  # (in place, the two forms may converge a pass apart)
+
+
 def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
     """The loss phase's multi-source arc sweep (complete graphs; 48 KB of rows per workgroup
     at V = 1500) against the oracle and against the one-source kernel (SGN_APSP_LOSS1; sparse

@@ -64,8 +64,9 @@ def test_round_kernels_have_no_scratch():
     # the round kernels must keep every host's state in registers/LDS: a non-inlined helper
     # or a spill puts it in scratch memory and costs ~2x (seen when send_batch was outlined)
     meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
-    # one instantiation per traffic kind; k_execute also per trace mode (traced / lean)
-    for k, count in (("k_rounds", 3), ("k_execute", 6)):
+    # one instantiation per traffic kind; k_rounds also with / without the big-slab path,
+    # k_execute per trace mode (traced / lean)
+    for k, count in (("k_rounds", 6), ("k_execute", 6)):
         names = [n for n in meta if k in n]
         assert len(names) == count, names
         for name in names:
