@@ -34,6 +34,9 @@ import sgn  # noqa: E402
 METRIC = "simulated packet events/sec (whole node) at 100k hosts; APSP build time"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md L2 section: 4 MiB per XCD, ~34.5 TB/s aggregate
+# 32-bit integer VALU (min / add have no packed form): 256 CUs x 64 lanes per clock x 2.4 GHz
+# (MI355X_MICROARCH.md: the 157.3 TF f32 vector peak counts packed FMA, 2 lanes x 2 flops)
+VALU_PEAK_TOPS = 39.3
 
 
 def build_workload(n_hosts, V, seed=1):
@@ -362,11 +365,30 @@ def apsp_roofline(apsp, V, U):
         out["loss_phase"]["l2_peak_GBps"] = L2_PEAK_GBS
         out["loss_phase"]["l2_frac"] = round(b_loss / (ms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)
         out["loss_phase"]["bound"] = "l2"
+    # the bound these two forms actually meet: 32-bit integer VALU work. Squaring: per pass every
+    # (i, k, j) relaxation is one saturating add and half a v_min3 (1.5 lane-ops, V^3 per pass,
+    # the padded V); the multi-source sweep: every (source, arc) pair is one v_add3 and half a
+    # v_min3 (1.5 lane-ops, U x E pairs)
+    Vp = -(-V // 64) * 64
+    if not apsp.get("latency_bf") and not apsp.get("latency_u64", 1) and apsp["latency_ms"] > 0:
+        ops = 1.5 * Vp ** 3 * max(1, apsp["latency_passes"])
+        out["latency_phase"]["valu"] = {"lane_ops": int(ops), "achieved_Tops": round(ops / (apsp["latency_ms"] * 1e-3) / 1e12, 2),
+                                        "peak_Tops": VALU_PEAK_TOPS,
+                                        "frac": round(ops / (apsp["latency_ms"] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+        out["latency_phase"]["bound"] = "valu"
+    if k and ms > 0:
+        ops = 1.5 * U * E
+        out["loss_phase"]["valu"] = {"lane_ops": int(ops), "achieved_Tops": round(ops / (ms * 1e-3) / 1e12, 2),
+                                     "peak_Tops": VALU_PEAK_TOPS, "frac": round(ops / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+        out["loss_phase"]["bound"] = "valu"
     out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
-                   ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else "u32 min-plus squaring"),
-                   "loss": f"{k}-source arc sweep + LDS fold" if k else "one-source arc sweep + LDS fold"}
-    out["note"] = ("the min-plus passes are VALU-bound (add-with-clamp + min per relaxation); the arc "
-                   "sweeps re-read the arc list from L2 / MALL, so their bytes exceed HBM traffic")
+                   ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else
+                    "u32 min-plus squaring, all passes in one launch (sq_run)"),
+                   "loss": f"{k}-source sweep (tail-ordered arcs, branch-free add3/min3 filter) + LDS fold" if k
+                   else "one-source arc sweep + LDS fold"}
+    out["note"] = ("the squaring passes and the multi-source sweep are bound by 32-bit integer VALU issue "
+                   "(valu: lane-ops over the phase's time, each phase timed whole including its launches "
+                   "and barrier); HBM and L2 bytes are reported beside it")
     return out
 
 

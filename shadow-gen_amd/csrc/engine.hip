@@ -185,6 +185,9 @@ __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
 // freed, so its entries are written through and read from memory like other cross-workgroup
 // data (a dirty L2 line of the previous owner must never overwrite the new owner's runs)
 __device__ __forceinline__ CodelEnt ld_dev_cq(SGN_GLB const CodelEnt* p) {
+#ifdef SGN_EXP_PLAINCQ  // cost experiment only (build_exp.sh): what device scope costs config C
+  return *p;
+#endif
   SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
   CodelEnt e;
   e.enqueue_ts = ld_dev(q);
@@ -197,6 +200,10 @@ __device__ __forceinline__ CodelEnt ld_dev_cq(SGN_GLB const CodelEnt* p) {
   return e;
 }
 __device__ __forceinline__ void st_dev_cq(SGN_GLB CodelEnt* p, const CodelEnt& e) {
+#ifdef SGN_EXP_PLAINCQ
+  *p = e;
+  return;
+#endif
   SGN_GLB char* q = (SGN_GLB char*)p;
   st_wt16(q, e.enqueue_ts, e.eid);
   st_wt16(q + 16, (uint64_t)e.src | ((uint64_t)e.payload << 32), (uint64_t)e.tag | ((uint64_t)e.count << 32));
@@ -681,7 +688,10 @@ struct HostExec {
     lr().rc_T = re.T;
   }
 
-  __device__ __forceinline__ void store() {
+  // old_next / old_peer: this host's S.nextloc / S.npeer as the round read them (a value that did
+  // not change is not stored again: a host-round that only took deliveries writes neither,
+  // and at config B's 16-host waves each was a partial-line write of its own)
+  __device__ __forceinline__ void store(uint64_t old_next, uint32_t old_peer) {
     HostRec& r = *R;
     r.rng[0] = r0;
     r.rng[1] = r1;
@@ -739,20 +749,28 @@ struct HostExec {
     // the per-host totals: PERIODIC no-return adds into dense arrays (no load of the old
     // value, no cold line); the other kinds in their cold lines
     if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+#ifndef SGN_EXP_NOCNT  // (cost experiments only, build_exp.sh: the traffic of each per-host stream)
       const size_t nH = S.nH;
       if (c_sent) cnt_add(&S.n_cnt[N_SENT * nH + h], c_sent);
       if (c_popped) cnt_add(&S.n_cnt[N_POPPED * nH + h], c_popped);
       if (c_deliv) cnt_add(&S.n_cnt[N_DELIVERED * nH + h], c_deliv);
       if (c_maxcodel)
         (void)__hip_atomic_fetch_max(&S.maxq[h], c_maxcodel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     } else {
       r.max_codel = c_maxcodel;
       r.n_sent += c_sent;
       r.n_popped += c_popped;
       r.n_delivered += c_deliv;
     }
-    S.nextloc[h] = next_local_time();
-    if (kApp == SGN_TRAFFIC_PERIODIC) S.npeer[h] = next_peer();
+#ifndef SGN_EXP_NONEXT
+    const uint64_t nl = next_local_time();
+    if (nl != old_next) S.nextloc[h] = nl;
+    if (kApp == SGN_TRAFFIC_PERIODIC) {
+      const uint32_t p = next_peer();
+      if (p != old_peer) S.npeer[h] = p;
+    }
+#endif
     if (hd_valid) st_dev_cq(cq_head_slot(), L->hd);
     if (tl_open) st_dev_cq(cq_tail_slot(), L->tl);
   }
@@ -2121,6 +2139,8 @@ struct ExecLDS {
   OutboxHdr* ob;      // the wave's outbox (an Outbox<kApp>)
   uint32_t* bmin;     // per-bucket minima of the workgroup's sends this round (S.agg_bmin) or null
   struct BigLDS* big; // a big slab's piece state (exec_group)
+  uint64_t* wacc;     // k_rounds: the workgroup's w_cnt sums (max for W_MAXFILL) over its whole
+                      // launch, flushed once at its end; null: exec_group adds to w_cnt itself
 };
 
 
@@ -2192,7 +2212,9 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint64_t pk_bytes = 0;
   auto park = [&]() {
     if (loaded) {
-      ex.store();
+      ex.store(lmin, np);
+      lmin = ex.next_local_time();  // (what memory holds now)
+      if (kApp == SGN_TRAFFIC_PERIODIC) np = ex.next_peer();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (its write-through stores are asm)
       pk_runs += ex.c_runs;
       pk_loss += ex.c_loss;
@@ -2443,8 +2465,11 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   auto slab_done = [&](size_t ib, uint32_t n) {
     if (lane == 0) {
       st_dev(&S.slab_n[ib], 0u);  // consumed (or moved); nobody appends to it this round
-      if (n) __hip_atomic_fetch_max(&S.w_cnt[W_MAXFILL * S.G + g], (uint64_t)n, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
+      if (n && X.wacc)
+        X.wacc[W_MAXFILL] = max(X.wacc[W_MAXFILL], (uint64_t)n);
+      else if (n)
+        __hip_atomic_fetch_max(&S.w_cnt[W_MAXFILL * S.G + g], (uint64_t)n, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
     }
   };
   for (uint32_t bi = 0; bi < nbk; bi++) {
@@ -2637,7 +2662,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   const uint64_t td = __builtin_amdgcn_s_memtime();
 #endif
   if (loaded) {
-    ex.store();
+    ex.store(lmin, np);
     n_ev = ex.c_popped + ex.c_sent + ex.c_loss + ex.c_deliv + ex.c_localev;
   }
 #ifdef SGN_DIAG
@@ -2692,7 +2717,16 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   uint64_t w_bytes = (loaded ? ex.c_bytes : 0) + pk_bytes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) w_bytes += shfl_xor64(w_bytes, off);
-  if (lane == 0) {
+  if (lane == 0 && X.wacc) {  // (persistent launches: per-round statistics stay in LDS; at config
+    // B these ~8 small atomics per group and round were ~70 % of the round kernel's PMC writes)
+    X.wacc[W_EXEC] += (uint64_t)__popcll(ex_mask);
+    X.wacc[W_RUNS] += N_all;
+    X.wacc[W_SORTED] += n_sorted;
+    X.wacc[W_LOSS] += w_loss;
+    X.wacc[W_LOCAL_EV] += w_lev;
+    X.wacc[W_BYTES] += w_bytes;
+    X.wacc[W_BIG] += n_pieces;
+  } else if (lane == 0) {
     const size_t G = S.G;
     if (ex_mask) cnt_add(&S.w_cnt[W_EXEC * G + g], (uint64_t)__popcll(ex_mask));
     if (N_all) cnt_add(&S.w_cnt[W_RUNS * G + g], N_all);
@@ -2722,6 +2756,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.lbs = lbs_;                                                                      \
   X.ob = &ob_;                                                                       \
   X.big = &big_;                                                                     \
+  X.wacc = nullptr;                                                                  \
   if (threadIdx.x == 0) ob_.bmin = X.bmin;
 
 // The workgroup's LDS table of bucket minima (S.agg_bmin): its sends of the round fold their
@@ -2962,6 +2997,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
   SGN_EXEC_LDS(X)
+  __shared__ uint64_t wacc_[W_N];
+  X.wacc = wacc_;
+  if (threadIdx.x < W_N) wacc_[threadIdx.x] = 0;
   const uint32_t w = blockIdx.x, P = gridDim.x;
   // Residency census before any simulation state is touched: the grid barrier below needs
   // every workgroup on the chip at once. Each workgroup counts itself in and waits (bounded)
@@ -3160,6 +3198,15 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       }
     }
     __syncthreads();
+  }
+  // the launch's per-wave statistics, in this workgroup's slot (the host sums the slots)
+  __syncthreads();
+  if (threadIdx.x < W_N && wacc_[threadIdx.x]) {
+    const uint32_t k = threadIdx.x;
+    if (k == W_MAXFILL)
+      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + w], wacc_[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      cnt_add(&S.w_cnt[k * S.G + w], wacc_[k]);
   }
   // the last round's bookkeeping and the host-visible control block
   if (w == wbk) {

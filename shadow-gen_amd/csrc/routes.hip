@@ -553,6 +553,7 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
 // broadcast read kept in registers, and the lanes' heads v are consecutive (conflict-free
 // reads of d[s][v]); a workgroup sweeps a range of tails. The test is d[s][v] - d[s][u] == l
 // with d[s][v] >= d[s][u] (u32; an arc of 2^32 - 1 ns or more is never tight).
+constexpr uint32_t SWEEP_HCAP = 256;  // filter hits one wave lists per 256-arc step (at most 256)
 template <int S>
 __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
                                                       uint32_t U, uint32_t V, const uint32_t* rowptr,
@@ -564,13 +565,25 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
   // stride from its neighbour's (conflict-free; one [Vp][S] row put the lanes 4S bytes apart)
   uint32_t* row = (uint32_t*)smem;
   const uint32_t g0 = blockIdx.x * S;
+  // (all S loads of a column in flight, then one 16-byte LDS write per plane; a source past U
+  // reads source 0's row and keeps INF)
+  const uint32_t* src[S];
 #pragma unroll
-  for (int k = 0; k < S; k++) {
-    const uint32_t* src = g0 + k < U ? D32 + (uint64_t)usrc[g0 + k] * Vp : nullptr;
-    for (uint32_t u = threadIdx.x; u < Vp; u += blockDim.x) row[(k >> 2) * Vp * 4 + u * 4 + (k & 3)] = src ? src[u] : SQ_INF;
+  for (int k = 0; k < S; k++) src[k] = D32 + (uint64_t)usrc[g0 + k < U ? g0 + k : 0] * Vp;
+  for (uint32_t u = threadIdx.x; u < Vp; u += blockDim.x) {
+    uint32_t x[S];
+#pragma unroll
+    for (int k = 0; k < S; k++) x[k] = src[k][u];
+#pragma unroll
+    for (int k = 0; k < S; k += 4)
+      *(uint4*)(row + (k >> 2) * Vp * 4 + u * 4) =
+          make_uint4(g0 + k < U ? x[k] : SQ_INF, g0 + k + 1 < U ? x[k + 1] : SQ_INF,
+                     g0 + k + 2 < U ? x[k + 2] : SQ_INF, g0 + k + 3 < U ? x[k + 3] : SQ_INF);
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // a wave's filter hits of one 256-arc step, checked exactly after the step (after the rows)
+  uint32_t* hits = (uint32_t*)smem + (size_t)Vp * S + wave * SWEEP_HCAP;
   const uint32_t u0 = (uint32_t)((uint64_t)V * blockIdx.y / gridDim.y);
   const uint32_t u1 = (uint32_t)((uint64_t)V * (blockIdx.y + 1) / gridDim.y);
   for (uint32_t u = u0 + wave; u < u1; u += nw) {
@@ -587,8 +600,8 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
     for (int k = 0; k < S; k++) ndu[k] = 0u - du[k];
     // four arcs per lane in flight (e, e + 64, e + 128, e + 192): the sweep waits on the arc
     // loads (PMC, round 4: 84 % of its wave cycles waiting with one arc per lane)
-    const uint32_t e1 = rowptr[u + 1];
-    for (uint32_t e0 = rowptr[u] + lane; e0 < e1; e0 += 256) {
+    const uint32_t e_beg = rowptr[u], e1 = rowptr[u + 1];
+    for (uint32_t e0 = e_beg + lane; e0 - lane < e1; e0 += 256) {
       uint32_t uv[4], l[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {  // (clamped, unconditional loads: all eight in flight at once;
@@ -597,6 +610,7 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
         uv[q] = *(const uint32_t*)((const char*)auv + off);
         l[q] = *(const uint32_t*)((const char*)al32 + off);
       }
+      uint32_t nh = 0;  // (wave-uniform)
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const uint32_t v = uv[q] >> 16;
@@ -610,22 +624,36 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
           b[k + 3] = y.w;
         }
         // branch-free filter: b - l - du (one v_add3 with -l and the scalar -du) is 0 for every
-        // tight (source, arc) pair (and, rarely, for a wrapped one); about one pair in a thousand
-        // is tight, so the exact test below runs on a filter hit only (it also drops the clamped
-        // lanes past the tail's last arc, and arcs of 2^32 - 1 ns or more)
+        // tight (source, arc) pair (and, rarely, for a wrapped one). About one pair in a
+        // thousand is tight, yet ~40 % of wave steps hold a hit in some lane: hits are listed
+        // (ballot + mbcnt, no divergence) and checked exactly after the step, lane-parallel
         const uint32_t nl = 0u - l[q];
         uint32_t acc = add3_vvs(b[0], nl, ndu[0]);
 #pragma unroll
         for (int k = 1; k < S; k++) acc = min(acc, add3_vvs(b[k], nl, ndu[k]));
-        if (acc != 0) continue;
-        const uint32_t e = e0 + 64 * q;
-        if (e >= e1 || l[q] == SQ_INF) continue;
+        const uint64_t m = __ballot(acc == 0);
+        if (m) {
+          if (acc == 0) hits[nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = e0 + 64 * q;
+          nh += (uint32_t)__popcll(m);
+        }
+      }
+      if (nh) {
+        // the exact test (it also drops the clamped lanes past the tail's last arc, and arcs of
+        // 2^32 - 1 ns or more)
+        for (uint32_t h = lane; h < nh; h += 64) {
+          const uint32_t e = hits[h];
+          if (e >= e1) continue;
+          const uint32_t lq = al32[e];
+          if (lq == SQ_INF) continue;
+          const uint32_t v = auv[e] >> 16;
 #pragma unroll
-        for (int k = 0; k < S; k++) {
-          if (du[k] == SQ_INF || b[k] < du[k] || b[k] - du[k] != l[q]) continue;
-          const uint32_t src = g0 + k;
-          const uint32_t pos = atomicAdd(&tcnt[src], 1u);
-          if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+          for (int k = 0; k < S; k++) {
+            const uint32_t bk = row[(k >> 2) * Vp * 4 + v * 4 + (k & 3)];
+            if (du[k] == SQ_INF || bk < du[k] || bk - du[k] != lq) continue;
+            const uint32_t src = g0 + k;
+            const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+            if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+          }
         }
       }
     }
@@ -1113,7 +1141,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       // leave 2 workgroups per CU; SGN_APSP_SWEEP_S=16 selects it, A/B)
       const int smax = getenv("SGN_APSP_SWEEP_S") ? atoi(getenv("SGN_APSP_SWEEP_S")) : 8;
       for (int k : {16, 8, 4}) {
-        const size_t b = (size_t)Vp * k * 4;
+        const size_t b = (size_t)Vp * k * 4 + (csr ? 8 * SWEEP_HCAP * 4 : 0);  // rows (+ hit lists)
         if (b > 160 * 1024 || k > smax || (k == 16 && !csr)) continue;
         const void* f = csr ? (k == 16 ? (const void*)loss_sweep_csr<16>
                                : k == 8 ? (const void*)loss_sweep_csr<8> : (const void*)loss_sweep_csr<4>)
@@ -1127,7 +1155,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
       if (!kS) lform = 0;
     }
-    const size_t lds_sw = (size_t)Vp * kS * 4;
+    const size_t lds_sw = (size_t)Vp * kS * 4 + (csr ? 8 * SWEEP_HCAP * 4 : 0);
     DevBuf dtc, dtl, dal32;
     if (lform) {
       SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
