@@ -1867,7 +1867,10 @@ struct HostExec {
   __device__ __forceinline__ void run(const EvRec* ev, const uint16_t* ord, uint32_t s0, uint32_t s1,
                       uint64_t until) {
     uint32_t pi = s0;
-    uint64_t pt = pi < s1 ? ev[ord[pi]].time : bg->tail;  // next due packet run's time
+    // (bg null: kernels without the big-slab path — no later piece, digests close here; the
+    // tail is re-read from LDS where it is needed: a register across the loop spilled the
+    // PERIODIC big-slab kernel)
+    uint64_t pt = pi < s1 ? ev[ord[pi]].time : bg ? bg->tail : INVALID;  // next due packet run's time
 #ifdef SGN_DIAG
 #endif
     while (true) {
@@ -1904,7 +1907,7 @@ struct HostExec {
         if (pi < s1 && pt <= lt) {  // Packet < Local at equal times (event.rs:102-110)
           const EvRec& e = ev[ord[pi]];
           pi++;
-          pt = pi < s1 ? ev[ord[pi]].time : bg->tail;  // the next run's time, ahead of need
+          pt = pi < s1 ? ev[ord[pi]].time : bg ? bg->tail : INVALID;  // the next run's time, ahead of need
           now = e.time;
           if (external() && e.src == gid) {  // a CPU application's datagram (sgn_submit)
             app_submit(e);
@@ -1960,7 +1963,7 @@ struct HostExec {
       forward_out_step();
     }
     // the sub-window is done: close the digests' pending runs (sgn_workload.h)
-    if (bg->flush) flush_digests();
+    if (!bg || bg->flush) flush_digests();
   }
   __device__ __forceinline__ void flush_digests() {
     dr_flush_same<0>();
@@ -2128,6 +2131,14 @@ __device__ void finalize_fused(const DevSim& S, uint32_t lane, uint32_t nch, uin
 //     segment and local slots, emitting new runs into the calendar / exchange slots;
 //  4. the wave's minimum next local event time goes to Ctrl::round_min.
 // LDS of the round kernels (one wave per workgroup)
+// no-return LDS atomics on a workgroup's statistics (ds_add_u64 / ds_max_u64: the wave does not
+// wait for them)
+__device__ __forceinline__ void wacc_add(uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wacc_max(uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 struct ExecLDS {
   EvRec* lev;         // due runs of one bucket (dynamic LDS, CAP entries)
   uint16_t* lb;       // grouped by destination lane (unordered)
@@ -2197,7 +2208,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     ob->hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
   }
   __syncthreads();
-  HostExec<kTrace, kApp> ex(S, h, we, be, ks, lslot + lane, lbs, ob, X.big);
+  HostExec<kTrace, kApp> ex(S, h, we, be, ks, lslot + lane, lbs, ob, kBig ? X.big : nullptr);
   bool loaded = false;
   uint32_t N_all = 0, sorted = 0;
   uint64_t kmin = INVALID;
@@ -2466,7 +2477,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     if (lane == 0) {
       st_dev(&S.slab_n[ib], 0u);  // consumed (or moved); nobody appends to it this round
       if (n && X.wacc)
-        X.wacc[W_MAXFILL] = max(X.wacc[W_MAXFILL], (uint64_t)n);
+        wacc_max(&X.wacc[W_MAXFILL], n);
       else if (n)
         __hip_atomic_fetch_max(&S.w_cnt[W_MAXFILL * S.G + g], (uint64_t)n, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
@@ -2538,7 +2549,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
         last = true;
         sub_end = we;
       }
-      if (lane == 0) {  // one pass: no later packet run, digests close with it
+      if (kBig && lane == 0) {  // one pass: no later packet run, digests close with it
         X.big->tail = INVALID;
         X.big->flush = 1;
       }
@@ -2718,14 +2729,15 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) w_bytes += shfl_xor64(w_bytes, off);
   if (lane == 0 && X.wacc) {  // (persistent launches: per-round statistics stay in LDS; at config
-    // B these ~8 small atomics per group and round were ~70 % of the round kernel's PMC writes)
-    X.wacc[W_EXEC] += (uint64_t)__popcll(ex_mask);
-    X.wacc[W_RUNS] += N_all;
-    X.wacc[W_SORTED] += n_sorted;
-    X.wacc[W_LOSS] += w_loss;
-    X.wacc[W_LOCAL_EV] += w_lev;
-    X.wacc[W_BYTES] += w_bytes;
-    X.wacc[W_BIG] += n_pieces;
+    // B these ~8 small atomics per group and round were ~70 % of the round kernel's PMC writes;
+    // no-return LDS atomics: this runs after the round's arrival, on the next round's path)
+    wacc_add(&X.wacc[W_EXEC], (uint64_t)__popcll(ex_mask));
+    wacc_add(&X.wacc[W_RUNS], N_all);
+    wacc_add(&X.wacc[W_SORTED], n_sorted);
+    wacc_add(&X.wacc[W_LOSS], w_loss);
+    wacc_add(&X.wacc[W_LOCAL_EV], w_lev);
+    wacc_add(&X.wacc[W_BYTES], w_bytes);
+    if (n_pieces) wacc_add(&X.wacc[W_BIG], n_pieces);
   } else if (lane == 0) {
     const size_t G = S.G;
     if (ex_mask) cnt_add(&S.w_cnt[W_EXEC * G + g], (uint64_t)__popcll(ex_mask));
@@ -2997,9 +3009,14 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
   SGN_EXEC_LDS(X)
-  __shared__ uint64_t wacc_[W_N];
-  X.wacc = wacc_;
-  if (threadIdx.x < W_N) wacc_[threadIdx.x] = 0;
+  // PERIODIC (configs B, D): the per-wave statistics in LDS for the launch (B: ~70 % of the
+  // PMC writes were their per-round atomics); TGEN keeps the per-round no-return adds (config
+  // C: 0.45 % faster per launch without the LDS accumulator, same-box A/B)
+  if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+    __shared__ uint64_t wacc_[W_N];
+    X.wacc = wacc_;
+    if (threadIdx.x < W_N) wacc_[threadIdx.x] = 0;
+  }
   const uint32_t w = blockIdx.x, P = gridDim.x;
   // Residency census before any simulation state is touched: the grid barrier below needs
   // every workgroup on the chip at once. Each workgroup counts itself in and waits (bounded)
@@ -3201,12 +3218,12 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   }
   // the launch's per-wave statistics, in this workgroup's slot (the host sums the slots)
   __syncthreads();
-  if (threadIdx.x < W_N && wacc_[threadIdx.x]) {
+  if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x]) {
     const uint32_t k = threadIdx.x;
     if (k == W_MAXFILL)
-      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + w], wacc_[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + w], X.wacc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
-      cnt_add(&S.w_cnt[k * S.G + w], wacc_[k]);
+      cnt_add(&S.w_cnt[k * S.G + w], X.wacc[k]);
   }
   // the last round's bookkeeping and the host-visible control block
   if (w == wbk) {

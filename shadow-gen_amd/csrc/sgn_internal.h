@@ -183,6 +183,12 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t app_k;            // synthetic app counter
   uint32_t flags, cq_head;   // flag bits; CoDel head run (pool index; an empty queue keeps its page)
   // ---- lines 1-3: cold ----
+  // (first: the queue fields that the next loads depend on — the CoDel head run and the send
+  // queue's head entry are loaded from them in load(); from the third line they cost config C
+  // 1 % per launch, same-box A/B of this order against the previous one, round 4)
+  uint32_t cq_nr, cq_len, cq_tp;             // CoDel runs / packets / chain's tail page
+  uint32_t fq_head, fq_len;                  // send queue (an empty queue's head is 0)
+  uint32_t rc_dst, rc_sid, pad_c;            // route cache peer (NO_HOST: none) and its slot id
   uint64_t st0, se0, st1, se1;  // local event slots: relay out, relay in (time, event id)
   uint64_t ri_eid;           // relay_inet_in cached packet: src event id
   uint64_t cq_bytes;         // CoDel queued bytes
@@ -190,9 +196,6 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t cq_ie, cq_dn, cq_cur, cq_prev;    // CoDel interval end / drop next / counts
   uint32_t ro_dst, ro_pay, ro_tag;           // relay_inet_out cached packet
   uint32_t ri_src, ri_pay, ri_tag;           // relay_inet_in cached packet
-  uint32_t cq_nr, cq_len, cq_tp;             // CoDel runs / packets / chain's tail page
-  uint32_t fq_head, fq_len;                  // send queue (an empty queue's head is 0)
-  uint32_t rc_dst, rc_sid, pad_c;            // route cache peer (NO_HOST: none) and its slot id
   // TGEN / EXTERNAL (their cold lines are read and written with the hot one anyway): the
   // constants and the per-host totals here, in the lines they already move (PERIODIC: the
   // dense HostConst array and no-return adds into DevSim::n_cnt / maxq)
@@ -206,7 +209,7 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t pad[16];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
-static_assert(offsetof(HostRec, st0) == 128, "line 0: the hot line");
+static_assert(offsetof(HostRec, cq_nr) == 128, "line 0: the hot line");
 // the constants of a host's slot, read with the hot line (32 B)
 struct __attribute__((aligned(32))) HostConst {
   uint32_t gid, ip, unode, pad;  // HostId, address, used-node index
