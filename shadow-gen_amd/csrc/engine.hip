@@ -3018,6 +3018,23 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     if (threadIdx.x < W_N) wacc_[threadIdx.x] = 0;
   }
   const uint32_t w = blockIdx.x, P = gridDim.x;
+  // The workgroup's groups: [gq0, gq1) in steps of gqs. TGEN: w, w + P, ... (config C's server
+  // groups come first in slot order and set the round's chain: dealt over every XCD). PERIODIC:
+  // XCD-aware — workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8; observed, used
+  // for speed only), so the ones sharing blockIdx % 8 take one contiguous eighth of the groups.
+  // Slots are ordered by graph node (sim_init), so an XCD's hosts cover an eighth of the nodes
+  // and their sends read an eighth of the route table's rows (config D: 2 of 16 MB, L2-resident).
+  // Any fixed bijection works: a group's records belong to its workgroup for the launch.
+  uint32_t gq0 = w, gq1 = S.G, gqs = P;
+  if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+    const uint32_t x = w & 7u, cx = (P - x + 7u) >> 3;  // this class's workgroups
+    uint32_t before = 0;                                 // workgroups of the classes below x
+    for (uint32_t y = 0; y < x; y++) before += (P - y + 7u) >> 3;
+    const uint32_t s0 = (uint32_t)((uint64_t)S.G * before / P), s1 = (uint32_t)((uint64_t)S.G * (before + cx) / P);
+    gq0 = s0 + (w >> 3);
+    gq1 = s1;
+    gqs = cx;
+  }
   // Residency census before any simulation state is touched: the grid barrier below needs
   // every workgroup on the chip at once. Each workgroup counts itself in and waits (bounded)
   // for the rest; the first to see the whole grid, or to give up, sets the verdict with a
@@ -3124,9 +3141,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     }
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
-    for (uint32_t g = w; g < S.G; g += P) {
+    for (uint32_t g = gq0; g < gq1; g += gqs) {
       uint64_t kmin, m;
-      const bool lastg = g + P >= S.G;  // the workgroup's last group arrives
+      const bool lastg = g + gqs >= gq1;  // the workgroup's last group arrives
       exec_group<false, kApp, kBig>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
@@ -4238,7 +4255,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   }
 
   // ---- host slots: every shard's HostId range, permuted so that hosts of one kind share
-  // waves (TGEN: servers by uplink, then clients by downlink; otherwise by bandwidth). The
+  // waves (TGEN: servers by uplink, then clients by downlink; otherwise by bandwidth, then by
+  // graph node: a wave's sends then read one row of the route table, and an XCD's workgroups
+  // a few hundred rows instead of all of them — config D's ~1 k hosts per node fill whole
+  // waves, so its random-peer route lookups become L2 hits). The
   // permutation only places hosts on lanes; semantics follow HostIds. SGN_HOST_ORDER=id keeps
   // HostId order (test hook). Every shard computes every shard's permutation (same inputs).
   {
@@ -4253,8 +4273,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
       if (!by_id) {
         auto key = [&](uint32_t i) {
           if (tr->kind == SGN_TRAFFIC_TGEN)
-            return std::make_tuple(is_server[i] ? 0u : 1u, is_server[i] ? ctx->bw_up[i] : ctx->bw_down[i], i);
-          return std::make_tuple(0u, ctx->bw_up[i] ^ (ctx->bw_down[i] << 1), i);
+            return std::make_tuple(is_server[i] ? 0u : 1u, is_server[i] ? ctx->bw_up[i] : ctx->bw_down[i], (uint64_t)i);
+          return std::make_tuple(0u, ctx->bw_up[i] ^ (ctx->bw_down[i] << 1), (uint64_t)ctx->unode[i] << 32 | i);
         };
         std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
       }
