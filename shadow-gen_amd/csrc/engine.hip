@@ -658,9 +658,18 @@ struct HostExec {
   // peer), so a hint that is not the next peer costs a miss, never a different result.
   uint32_t pf_peer;
   uint64_t pf_pi;
+  // a peer's slot id | used-node index << 32: from the 4-byte table when sim_init built one
+  // (half the bytes of the 8-byte one: config D's 1 M-host table is 4 MB, about an XCD's L2)
+  __device__ __forceinline__ uint64_t peer_info(uint32_t dst) const {
+    if (S.peer32) {
+      const uint32_t v = S.peer32[dst];
+      return (v & ((1u << S.peer_sb) - 1u)) | ((uint64_t)(v >> S.peer_sb) << 32);
+    }
+    return S.peer[dst];
+  }
   __device__ __forceinline__ void prefetch_peer(uint32_t np) {
     pf_peer = np;
-    pf_pi = np != NO_HOST ? S.peer[np] : 0;
+    pf_pi = np != NO_HOST ? peer_info(np) : 0;
   }
   __device__ __forceinline__ uint32_t next_peer() const {
     uint32_t peer = NO_HOST, uip = 0;
@@ -1467,7 +1476,7 @@ struct HostExec {
       // reliability = (f64)(1.0f - loss) is 0 or >= 2^-24, so reliability * 2^53 is an exact
       // integer T (precomputed per route, sim_init) and the test is (x >> 11) >= T, bit for
       // bit the same decision
-      const uint64_t pi = S.peer[dst];
+      const uint64_t pi = peer_info(dst);
       dsid = (uint32_t)pi;
       const RouteEnt re = S.route[(size_t)my_unode * S.U + (uint32_t)(pi >> 32)];
       delay = re.lat;
@@ -4342,6 +4351,17 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     std::vector<uint64_t> pe(N);
     for (uint32_t i = 0; i < N; i++) pe[i] = (uint64_t)ctx->sid_of[i] | ((uint64_t)ctx->unode[i] << 32);
     if ((rc = up64(pe, &S.peer))) return rc;
+    // the 4-byte form when slot ids and node indices fit together (sid < N, node < U)
+    uint32_t sb = 1, ub = 1;
+    while (sb < 32 && (1ull << sb) < N) sb++;
+    while (ub < 32 && (1ull << ub) < ctx->U) ub++;
+    S.peer32 = nullptr;
+    S.peer_sb = sb;
+    if (sb + ub <= 32 && !getenv("SGN_PEER64")) {
+      std::vector<uint32_t> p32(N);
+      for (uint32_t i = 0; i < N; i++) p32[i] = ctx->sid_of[i] | (ctx->unode[i] << sb);
+      if ((rc = up32(p32, &S.peer32))) return rc;
+    }
     if ((rc = ensure_host_routes(ctx))) return rc;
     const size_t UU = (size_t)ctx->U * ctx->U;
     std::vector<RouteEnt> re(UU);

@@ -312,6 +312,8 @@ struct DevSim {
   // A slot id (sid) is lo + slot; event records carry the destination's sid.
   SGN_GLB const uint32_t* sid_of;   // [n_all] HostId -> sid (every shard's permutation)
   SGN_GLB const uint64_t* peer;     // [n_all] HostId -> sid | used-node index << 32 (one load per peer)
+  SGN_GLB const uint32_t* peer32;   // the same packed in 4 bytes (sid | node << peer_sb) when it fits, else null
+  uint32_t peer_sb;                 // sid bits of peer32
   SGN_GLB const RouteEnt* route;    // [U x U] {latency, loss threshold} (routing table, packet-path form)
   SGN_GLB const uint32_t* host_of;  // [nH] slot -> HostId of this shard
   SGN_GLB const uint32_t* dns_key;
