@@ -101,3 +101,29 @@ def test_periodic_round_kernel_lds_budget():
             runs = 128 * 32 + 2 * 128 * 2
             total = m["group_segment_fixed_size"] + max(runs, 1024) + 257 * 4
             assert -(-total // 512) * 512 * 8 <= 160 * 1024, (name, m, total)
+
+
+def _periodic_groups(w, P, G):
+    """The PERIODIC persistent kernel's group list for workgroup w of P (k_rounds, engine.hip):
+    the workgroups sharing w % 8 take one contiguous eighth of the G groups."""
+    x = w & 7
+    cx = (P - x + 7) >> 3
+    before = sum((P - y + 7) >> 3 for y in range(x))
+    s0, s1 = G * before // P, G * (before + cx) // P
+    return list(range(s0 + (w >> 3), s1, cx))
+
+
+@pytest.mark.parametrize("P,G", [(1, 1), (2, 5), (7, 7), (9, 100), (625, 625), (2048, 15625),
+                                 (1792, 15625), (2040, 15625), (300, 200)])
+def test_periodic_xcd_group_mapping_is_a_bijection(P, G):
+    # every group exactly once per round, each workgroup's groups inside its XCD class's
+    # contiguous range (P > G: the oversized-grid test hook leaves some workgroups idle)
+    seen = []
+    for w in range(P):
+        gs = _periodic_groups(w, P, G)
+        assert all(0 <= g < G for g in gs)
+        seen += gs
+    assert sorted(seen) == list(range(G))
+    for x in range(min(8, P)):  # one contiguous range per class
+        cls = sorted(g for w in range(x, P, 8) for g in _periodic_groups(w, P, G))
+        assert cls == list(range(cls[0], cls[-1] + 1)) if cls else True
