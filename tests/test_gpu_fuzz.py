@@ -3,8 +3,8 @@ that mix every option of the path at once — traffic kind (PERIODIC / TGEN), st
 dynamic runahead with bootstrapping, per-host bandwidths, lossy random and Tor-like graphs,
 unknown destinations, send-queue and CoDel-pool sizes down to the blocking / page-reuse
 regime, the interface qdisc, hosts per wave, small calendar slabs (extensions and the
-big-slab path), and the round kernel (persistent k_rounds or
-per-round k_execute, traced or not). Pools grow instead of refusing a scenario
+big-slab path), host slot order, the peer table's form, and the round kernel (persistent
+k_rounds or per-round k_execute, traced or not). Pools grow instead of refusing a scenario
 (test_gpu_pools.py), so no case may be skipped. Bar: every counter, the final window and
 every host's order-sensitive digests (tx / rx / app / RNG state / next event id) identical;
 with the trace on, every per-packet record (IF_POP, SEND with drop decision and delivery
@@ -49,6 +49,12 @@ def draw(i):
     if r.random() < 0.3:  # small slabs that stay small: spills, extensions and big-slab pieces
         env["SGN_SLAB_CAP"] = "16"
         env["SGN_SLAB_LIM"] = "32"
+    # (drawn after the fields above, so earlier cases keep their parameters) host slots in
+    # HostId order instead of kind / bandwidth / node order, and the 8-byte peer table
+    if r.random() < 0.2:
+        env["SGN_HOST_ORDER"] = "id"
+    if r.random() < 0.2:
+        env["SGN_PEER64"] = "1"
     return kw, env, trace
 
 
