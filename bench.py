@@ -346,49 +346,67 @@ def apsp_roofline(apsp, V, U):
         b_lat = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
     k = apsp.get("loss_multi", 0)
     b_loss = 8.0 * E * -(-U // k) + 4.0 * U * V if k else 12.0 * U * E
+    # Each phase's `frac` is the fraction of the bound it meets (`bound`): 32-bit integer VALU
+    # issue for the squaring passes and the multi-source sweep, HBM for the other forms. The
+    # HBM fraction is always given as `hbm_frac` (against HBM_PEAK_GBS) and the loss phase's
+    # L2 traffic as `l2_frac` (against L2_PEAK_GBS): L2 bytes are never quoted against the HBM
+    # peak.
     out = {}
     for name, b, ms in (("latency_phase", b_lat, apsp["latency_ms"]), ("loss_phase", b_loss, apsp["loss_ms"])):
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         out[name] = {"bound": "hbm", "alg_bytes": int(b), "ms": round(ms, 3), "achieved": round(gbs, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5)}
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+                     "hbm_frac": round(gbs / HBM_PEAK_GBS, 5)}
     # the loss phase against each level it reads: its compulsory HBM bytes — the
     # arc list once (8 B per arc), the used sources' u32 distance rows, the tight lists written
     # and read back (~one arc per node and source, 4 B each way), the f32 loss rows written — and
     # the re-read model above, whose arc re-reads are served by the L2s (MI355X_MICROARCH.md:
     # 4 MiB per XCD, ~34.5 TB/s aggregate), not by HBM
     ms = apsp["loss_ms"]
-    if ms > 0:
+    if ms > 0 and k:
         hbm = 8.0 * E + 4.0 * U * V + 2 * 4.0 * U * V + 4.0 * U * V
-        out["loss_phase"]["hbm_bytes"] = int(hbm)
-        out["loss_phase"]["hbm_frac"] = round(hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-        out["loss_phase"]["l2_bytes"] = int(b_loss)
-        out["loss_phase"]["l2_peak_GBps"] = L2_PEAK_GBS
-        out["loss_phase"]["l2_frac"] = round(b_loss / (ms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)
-        out["loss_phase"]["bound"] = "l2"
+        lp = out["loss_phase"]
+        lp["hbm_bytes"] = int(hbm)
+        lp["hbm_GBps"] = round(hbm / (ms * 1e-3) / 1e9, 2)
+        lp["hbm_frac"] = round(hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        lp["l2_bytes"] = int(b_loss)
+        lp["l2_GBps"] = round(b_loss / (ms * 1e-3) / 1e9, 2)
+        lp["l2_peak_GBps"] = L2_PEAK_GBS
+        lp["l2_frac"] = round(b_loss / (ms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)
+        # (alg_bytes / achieved above are the L2-served re-read model; the HBM figure is hbm_GBps)
     # the bound these two forms actually meet: 32-bit integer VALU work. Squaring: per pass every
     # (i, k, j) relaxation is one saturating add and half a v_min3 (1.5 lane-ops, V^3 per pass,
     # the padded V); the multi-source sweep: every (source, arc) pair is one v_add3 and half a
     # v_min3 (1.5 lane-ops, U x E pairs)
     Vp = -(-V // 64) * 64
+
+    def valu_bound(ph, ops, ms_):
+        tops = ops / (ms_ * 1e-3) / 1e12
+        ph["valu"] = {"lane_ops": int(ops), "achieved_Tops": round(tops, 2), "peak_Tops": VALU_PEAK_TOPS,
+                      "frac": round(tops / VALU_PEAK_TOPS, 4)}
+        ph.update({"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tops (int32 lane-ops)",
+                   "frac": round(tops / VALU_PEAK_TOPS, 4)})
+
     if not apsp.get("latency_bf") and not apsp.get("latency_u64", 1) and apsp["latency_ms"] > 0:
-        ops = 1.5 * Vp ** 3 * max(1, apsp["latency_passes"])
-        out["latency_phase"]["valu"] = {"lane_ops": int(ops), "achieved_Tops": round(ops / (apsp["latency_ms"] * 1e-3) / 1e12, 2),
-                                        "peak_Tops": VALU_PEAK_TOPS,
-                                        "frac": round(ops / (apsp["latency_ms"] * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
-        out["latency_phase"]["bound"] = "valu"
+        lp, lms = out["latency_phase"], apsp["latency_ms"]
+        # compulsory HBM bytes: the u32 matrix read and written once per pass; the panel re-reads
+        # of the model above (alg_bytes) are L2-served
+        hbm = 8.0 * V * V * max(1, apsp["latency_passes"])
+        lp.update({"hbm_bytes": int(hbm), "hbm_GBps": round(hbm / (lms * 1e-3) / 1e9, 2),
+                   "hbm_frac": round(hbm / (lms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "l2_bytes": int(b_lat),
+                   "l2_frac": round(b_lat / (lms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)})
+        valu_bound(lp, 1.5 * Vp ** 3 * max(1, apsp["latency_passes"]), lms)
     if k and ms > 0:
-        ops = 1.5 * U * E
-        out["loss_phase"]["valu"] = {"lane_ops": int(ops), "achieved_Tops": round(ops / (ms * 1e-3) / 1e12, 2),
-                                     "peak_Tops": VALU_PEAK_TOPS, "frac": round(ops / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
-        out["loss_phase"]["bound"] = "valu"
+        valu_bound(out["loss_phase"], 1.5 * U * E, ms)
     out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
                    ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else
                     "u32 min-plus squaring, all passes in one launch (sq_run)"),
                    "loss": f"{k}-source sweep (tail-ordered arcs, branch-free add3/min3 filter) + LDS fold" if k
                    else "one-source arc sweep + LDS fold"}
-    out["note"] = ("the squaring passes and the multi-source sweep are bound by 32-bit integer VALU issue "
-                   "(valu: lane-ops over the phase's time, each phase timed whole including its launches "
-                   "and barrier); HBM and L2 bytes are reported beside it")
+    out["note"] = ("frac is the fraction of each phase's bound: the squaring passes and the multi-source "
+                   "sweep are bound by 32-bit integer VALU issue (lane-ops over the phase's time, each "
+                   "phase timed whole including its launches and barrier); hbm_frac (HBM bytes / 8 TB/s) "
+                   "and l2_frac (L2-served bytes / 34.5 TB/s) are reported beside it")
     return out
 
 

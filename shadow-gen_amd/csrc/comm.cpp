@@ -218,6 +218,11 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       return ctxs[i] ? set_error(ctxs[i], SGN_ESTATE, "not a local shard group") : SGN_EINVAL;
   for (uint32_t i = 0; i < n; i++)
     if (int rc = rng_release(ctxs[i])) return rc;
+  // SGN_LOCAL_DEFER=1 (test hook): like the RCCL transport between its batch syncs, runs
+  // k_import spilled stay in the spill area until a round is held (the next round's gathers
+  // read them there)
+  const char* dv = getenv("SGN_LOCAL_DEFER");
+  const bool defer = dv && atoi(dv) == 1;
   uint64_t done = 0;
   for (; done < max_rounds; done++) {
     Ctrl h{};
@@ -269,11 +274,7 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       }
       if (int rc = exchange_import()) return rc;
     }
-    // a held round edge (the same on every shard) or a spill: the pools grow before the next.
-    // SGN_LOCAL_DEFER=1 (test hook): like the RCCL transport between its batch syncs, runs
-    // k_import spilled stay in the spill area until a round is held (the next round's gathers
-    // read them there)
-    const bool defer = getenv("SGN_LOCAL_DEFER") && atoi(getenv("SGN_LOCAL_DEFER")) == 1;
+    // a held round edge (the same on every shard) or a spill: the pools grow before the next
     bool held = false;
     for (uint32_t i = 0; i < n; i++) {
       if (int rc = ctrl_sync(ctxs[i])) return rc;
@@ -282,6 +283,14 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
     for (uint32_t i = 0; i < n && (held || !defer); i++)
       if (int rc = resolve_pools(ctxs[i])) return rc;
   }
+  // (deferred spills: every run is back in its slab before the caller can ask for next-event
+  // times — k_next_packet scans the pool and the extensions, not the spill area)
+  if (defer)
+    for (uint32_t i = 0; i < n; i++) {
+      if (int rc = ctrl_sync(ctxs[i])) return rc;
+      if (ctxs[i]->h_ctrl->spill_n || ctxs[i]->h_ctrl->hold)
+        if (int rc = resolve_pools(ctxs[i])) return rc;
+    }
   if (rounds_done) *rounds_done = done;
   return 0;
 }

@@ -3242,14 +3242,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     }
     __syncthreads();
   }
-  // the launch's per-wave statistics, in this workgroup's slot (the host sums the slots)
+  // the launch's per-wave statistics, in the slot of this workgroup's first group (the host sums
+  // the slots; the mapping is a bijection, so gq0 < G is this workgroup's alone — a forced grid
+  // larger than G has workgroups w >= G; one without groups has nothing to flush)
   __syncthreads();
-  if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x]) {
+  if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x] && gq0 < gq1) {
     const uint32_t k = threadIdx.x;
     if (k == W_MAXFILL)
-      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + w], X.wacc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + gq0], X.wacc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
-      cnt_add(&S.w_cnt[k * S.G + w], X.wacc[k]);
+      cnt_add(&S.w_cnt[k * S.G + gq0], X.wacc[k]);
   }
   // the last round's bookkeeping and the host-visible control block
   if (w == wbk) {
@@ -3458,14 +3460,18 @@ __global__ void k_relayout_ext(const uint64_t* __restrict__ hot, uint64_t n_hot,
 }
 __global__ void k_respill(const EvRec* __restrict__ spill, const uint32_t* __restrict__ spill_idx, uint64_t n,
                           EvRec* pool, uint32_t cap, const uint64_t* __restrict__ ext, EvRec* ext_pool,
-                          uint32_t* cursor) {
+                          uint32_t* cursor, uint32_t* lost) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t idx = spill_idx[i];
   if (idx & SPILL_PEER) return;  // a run for another shard (grow_exchange_slot), or one a gather took
   const uint32_t pos = atomicAdd(&cursor[idx], 1u);
   const uint32_t room = cap + (ext ? (uint32_t)(ext[idx] >> 40) : 0u);
-  if (pos < room) *relayout_dst(pool, cap, ext, ext_pool, idx, pos) = spill[i];
+  if (pos < room)
+    *relayout_dst(pool, cap, ext, ext_pool, idx, pos) = spill[i];
+  else  // the host sized every slab for its fill (room >= fill): a violation is an error, never
+        // a silent loss (relayout_calendar reads this count)
+    atomicAdd(lost, 1u);
 }
 
 // sgn_rng_*: draws of host Xoshiro256++ streams (the state stays on the device). One thread
@@ -3830,13 +3836,13 @@ int relayout_calendar(sgn_ctx* ctx) {
     EvRec* np = cap != S.CAP ? (EvRec*)dev_alloc(ctx, n_slabs * cap * sizeof(EvRec), false) : (EvRec*)S.pool;
     EvRec* nep = etot ? (EvRec*)dev_alloc(ctx, etot * sizeof(EvRec), false) : nullptr;
     uint64_t* nxt = etot ? (uint64_t*)dev_alloc(ctx, n_slabs * 8, false) : nullptr;
-    uint32_t* cur = (uint32_t*)dev_alloc(ctx, n_slabs * 4, false);
+    uint32_t* cur = (uint32_t*)dev_alloc(ctx, (n_slabs + 1) * 4, false);  // + k_respill's lost-run count
     uint64_t* dhot = hot_old.empty() ? nullptr : (uint64_t*)dev_alloc(ctx, hot_old.size() * 8, false);
     auto undo = [&]() {
       if (np && np != (EvRec*)S.pool) dev_free(ctx, np, n_slabs * cap * sizeof(EvRec));
       if (nep) dev_free(ctx, nep, etot * sizeof(EvRec));
       if (nxt) dev_free(ctx, nxt, n_slabs * 8);
-      if (cur) dev_free(ctx, cur, n_slabs * 4);
+      if (cur) dev_free(ctx, cur, (n_slabs + 1) * 4);
       if (dhot) dev_free(ctx, dhot, hot_old.size() * 8);
     };
     if (!np || (etot && (!nep || !nxt)) || !cur || (!hot_old.empty() && !dhot)) {
@@ -3845,6 +3851,7 @@ int relayout_calendar(sgn_ctx* ctx) {
     }
     if (nxt) SGN_HIP(ctx, hipMemcpy(nxt, next.data(), n_slabs * 8, hipMemcpyHostToDevice));
     if (dhot) SGN_HIP(ctx, hipMemcpy(dhot, hot_old.data(), hot_old.size() * 8, hipMemcpyHostToDevice));
+    SGN_HIP(ctx, hipMemsetAsync(cur + n_slabs, 0, 4, ctx->stream));
     // the pool part moves only when the slabs grow (in place it stays where it is)
     const uint64_t nt = n_slabs * S.CAP;
     if (np != (EvRec*)S.pool) {
@@ -3866,13 +3873,19 @@ int relayout_calendar(sgn_ctx* ctx) {
     if (nsp)
       hipLaunchKernelGGL(k_respill, dim3((uint32_t)((nsp + 255) / 256)), dim3(256), 0, ctx->stream,
                          (const EvRec*)S.spill, (const uint32_t*)S.spill_idx, nsp, np, cap, (const uint64_t*)nxt,
-                         nep, cur);
+                         nep, cur, cur + n_slabs);
     SGN_HIP(ctx, hipGetLastError());
     SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t lost = 0;
+    SGN_HIP(ctx, hipMemcpy(&lost, cur + n_slabs, 4, hipMemcpyDeviceToHost));
+    if (lost) {
+      ctx->failed = "calendar re-layout lost " + std::to_string(lost) + " spilled runs (slab sizing)";
+      return set_error(ctx, SGN_EOVERFLOW, ctx->failed);
+    }
     if (np != (EvRec*)S.pool) dev_free(ctx, (void*)S.pool, n_slabs * S.CAP * sizeof(EvRec));
     if (S.ext_pool) dev_free(ctx, (void*)S.ext_pool, S.ext_total * sizeof(EvRec));
     if (S.ext) dev_free(ctx, (void*)S.ext, n_slabs * 8);
-    dev_free(ctx, cur, n_slabs * 4);
+    dev_free(ctx, cur, (n_slabs + 1) * 4);
     if (dhot) dev_free(ctx, dhot, hot_old.size() * 8);
     if (cap != S.CAP) ctx->cal_grows++;
     S.pool = (decltype(S.pool))np;
