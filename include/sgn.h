@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 8
+#define SGN_ABI_VERSION 9
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -455,6 +455,19 @@ typedef struct sgn_engine_info {
   uint64_t big_slab_pieces;      /* pieces run by the big-slab path since sim_init */
   uint64_t spill_area_runs;      /* the spill area's capacity */
   uint64_t spill_area_grows;     /* spill area enlargements */
+  /* ABI 9: persistent multi-shard rounds. With N > 1 shards the rounds run in one persistent
+   * launch per GPU (or, for a local group on one GPU, one launch whose workgroup ranges are the
+   * shards): runs for another shard go straight into that shard's inbox (peer-mapped memory),
+   * and every shard computes the next window from the N round-edge messages in its inbox
+   * (core/manager.rs:568-628, core/controller.rs:88-112). */
+  uint64_t exchange_mode;        /* 0: one shard; 1: per-round launches + RCCL send/recv (or the
+                                    local group's copies); 2: persistent rounds, peer inboxes */
+  uint64_t inbox_slot_runs;      /* runs per sender and round parity in each inbox */
+  uint64_t inbox_grows;          /* inbox enlargements (a round used more than half a slot) */
+  uint64_t inbox_overflow_rounds;/* rounds whose runs past a slot the host moved */
+  uint64_t inbox_moved_runs;     /* ... runs moved that way (into this shard) */
+  uint64_t persistent_x_launches;/* persistent multi-shard launches */
+  uint64_t persistent_x_grid;    /* this shard's workgroups in the last one */
 } sgn_engine_info;
 int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out);
 

@@ -176,6 +176,130 @@ int comm_allreduce_minmax(sgn_ctx* ctx, uint64_t* p, size_t n_min, size_t n_max)
   return 0;
 }
 
+// ---- persistent multi-shard rounds, one shard per GPU: the peers' inboxes in this process ----
+// Every shard exports its inbox (uncached device memory) as an IPC handle; one RCCL all-gather
+// gives every shard every handle, and each opens its peers' (xGMI peer access). A shard that
+// cannot export or open one tells the others through a max all-reduce, and then every shard
+// keeps the per-round RCCL path (the same decision everywhere: the rounds stay in lockstep).
+int comm_xpeer_map(sgn_ctx* ctx) {
+  ncclComm_t comm = (ncclComm_t)ctx->comm;
+  const uint32_t R = ctx->nranks;
+  ctx->x_mapped = false;
+  for (void* p : ctx->x_opened)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  ctx->x_opened.clear();
+  static_assert(sizeof(hipIpcMemHandle_t) <= 128, "IPC handle size");
+  constexpr size_t HB = 128;
+  std::vector<uint8_t> mine(HB, 0), all((size_t)R * HB, 0);
+  uint64_t bad = 0;
+  hipIpcMemHandle_t h;
+  if (!ctx->xin_mem || hipIpcGetMemHandle(&h, ctx->xin_mem) != hipSuccess)
+    bad = 1;
+  else
+    std::memcpy(mine.data(), &h, sizeof(h));
+  void* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, (R + 1) * HB));
+  hipError_t e = hipMemcpy(d, mine.data(), HB, hipMemcpyHostToDevice);
+  ncclResult_t r = e == hipSuccess ? ncclAllGather(d, (char*)d + HB, HB, ncclUint8, comm, ctx->stream) : ncclInternalError;
+  if (r == ncclSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (r == ncclSuccess && e == hipSuccess) e = hipMemcpy(all.data(), (char*)d + HB, (size_t)R * HB, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-gather (inbox handles): ") + ncclGetErrorString(r));
+  if (e != hipSuccess) return hip_fail(ctx, e, "inbox handle exchange");
+  std::vector<char*> base(R, nullptr);
+  base[ctx->rank] = (char*)ctx->xin_mem;
+  for (uint32_t q = 0; q < R && !bad; q++) {
+    if (q == ctx->rank) continue;
+    hipIpcMemHandle_t hq;
+    std::memcpy(&hq, all.data() + (size_t)q * HB, sizeof(hq));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !p) {
+      bad = 1;
+      (void)hipGetLastError();
+      break;
+    }
+    ctx->x_opened.push_back(p);
+    base[q] = (char*)p;
+  }
+  if (int rc = comm_allreduce_max_u64(ctx, &bad, 1)) return rc;
+  if (bad) {  // some shard cannot map every inbox: all shards keep the per-round path
+    for (void* p : ctx->x_opened)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    ctx->x_opened.clear();
+    ctx->x_off = true;
+    return 0;
+  }
+  ctx->x_base = base;
+  if (int rc = xpeer_upload(ctx)) return rc;
+  ctx->x_mapped = true;
+  return 0;
+}
+
+// Runs some shard sent past a peer's inbox slot (out[q]: this shard's for shard q) to their
+// shards at a held round edge: the counts by one all-gather, the runs by one grouped send/recv.
+int comm_xmove_spills(sgn_ctx* ctx, const std::vector<std::vector<EvRec>>& out, std::vector<EvRec>* in) {
+  ncclComm_t comm = (ncclComm_t)ctx->comm;
+  const uint32_t R = ctx->nranks, me = ctx->rank;
+  std::vector<uint64_t> cnt(R, 0), all((size_t)R * R, 0);
+  for (uint32_t q = 0; q < R; q++) cnt[q] = q < out.size() ? out[q].size() : 0;
+  void* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, (size_t)(R + R * R) * 8));
+  SGN_HIP(ctx, hipMemcpy(d, cnt.data(), R * 8, hipMemcpyHostToDevice));
+  ncclResult_t r = ncclAllGather(d, (uint64_t*)d + R, R, ncclUint64, comm, ctx->stream);
+  if (r == ncclSuccess) SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (r == ncclSuccess) SGN_HIP(ctx, hipMemcpy(all.data(), (uint64_t*)d + R, (size_t)R * R * 8, hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-gather (spill counts): ") + ncclGetErrorString(r));
+  // all[q * R + p]: runs shard q holds for shard p
+  uint64_t nout = 0, nin = 0;
+  std::vector<uint64_t> ooff(R + 1, 0), ioff(R + 1, 0);
+  for (uint32_t q = 0; q < R; q++) {
+    ooff[q + 1] = ooff[q] + (q == me ? 0 : cnt[q]);
+    ioff[q + 1] = ioff[q] + (q == me ? 0 : all[(size_t)q * R + me]);
+  }
+  nout = ooff[R];
+  nin = ioff[R];
+  in->assign(nin, EvRec{});
+  if (nout == 0 && nin == 0) return 0;
+  EvRec *ds = nullptr, *dr = nullptr;
+  SGN_HIP(ctx, hipMalloc((void**)&ds, std::max<uint64_t>(1, nout) * sizeof(EvRec)));
+  SGN_HIP(ctx, hipMalloc((void**)&dr, std::max<uint64_t>(1, nin) * sizeof(EvRec)));
+  for (uint32_t q = 0; q < R; q++)
+    if (q != me && cnt[q]) SGN_HIP(ctx, hipMemcpy(ds + ooff[q], out[q].data(), cnt[q] * sizeof(EvRec), hipMemcpyHostToDevice));
+  r = ncclGroupStart();
+  for (uint32_t q = 0; q < R && r == ncclSuccess; q++) {
+    if (q == me) continue;
+    if (ooff[q + 1] > ooff[q]) r = ncclSend(ds + ooff[q], (ooff[q + 1] - ooff[q]) * sizeof(EvRec), ncclUint8, (int)q, comm, ctx->stream);
+    if (r == ncclSuccess && ioff[q + 1] > ioff[q])
+      r = ncclRecv(dr + ioff[q], (ioff[q + 1] - ioff[q]) * sizeof(EvRec), ncclUint8, (int)q, comm, ctx->stream);
+  }
+  ncclResult_t r2 = ncclGroupEnd();
+  hipError_t e = hipSuccess;
+  if (r == ncclSuccess && r2 == ncclSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (r == ncclSuccess && r2 == ncclSuccess && e == hipSuccess && nin)
+    e = hipMemcpy(in->data(), dr, nin * sizeof(EvRec), hipMemcpyDeviceToHost);
+  (void)hipFree(ds);
+  (void)hipFree(dr);
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return set_error(ctx, SGN_EDEVICE, std::string("RCCL send/recv (spilled runs): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  if (e != hipSuccess) return hip_fail(ctx, e, "spilled runs exchange");
+  return 0;
+}
+
+// max all-reduce of n host u64 values (through a device buffer)
+int comm_allreduce_max_u64(sgn_ctx* ctx, uint64_t* host_v, size_t n) {
+  void* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, n * 8));
+  hipError_t e = hipMemcpy(d, host_v, n * 8, hipMemcpyHostToDevice);
+  ncclResult_t r = e == hipSuccess ? ncclAllReduce(d, d, n, ncclUint64, ncclMax, (ncclComm_t)ctx->comm, ctx->stream) : ncclInternalError;
+  if (r == ncclSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (r == ncclSuccess && e == hipSuccess) e = hipMemcpy(host_v, d, n * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-reduce: ") + ncclGetErrorString(r));
+  if (e != hipSuccess) return hip_fail(ctx, e, "all-reduce");
+  return 0;
+}
+
 int comm_allreduce_max_u32(sgn_ctx* ctx, uint32_t* p, size_t n) {
   ncclResult_t r = ncclAllReduce(p, p, n, ncclUint32, ncclMax, (ncclComm_t)ctx->comm, ctx->stream);
   if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-reduce: ") + ncclGetErrorString(r));
@@ -218,6 +342,34 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       return ctxs[i] ? set_error(ctxs[i], SGN_ESTATE, "not a local shard group") : SGN_EINVAL;
   for (uint32_t i = 0; i < n; i++)
     if (int rc = rng_release(ctxs[i])) return rc;
+  // persistent rounds (k_rounds_x): every shard a range of workgroups of ONE launch on their GPU,
+  // the inboxes ordinary (uncached) device memory of that GPU — the device code of the N-GPU
+  // path, rehearsed on one GPU. SGN_LOCAL_PERSIST=0 keeps the per-round copies below.
+  uint64_t pre = 0;
+  {
+    const char* lp = getenv("SGN_LOCAL_PERSIST");
+    bool ok = !(lp && atoi(lp) == 0) && n <= XL_MAX;
+    for (uint32_t i = 0; i < n && ok; i++)
+      ok = ctxs[i]->device == ctxs[0]->device && xpersist_possible(ctxs[i]) && ctxs[i]->S.tkind == ctxs[0]->S.tkind;
+    if (ok) {
+      std::vector<sgn_ctx*> sh(ctxs, ctxs + n);
+      if (!ctxs[0]->x_mapped) {
+        std::vector<char*> base(n);
+        for (uint32_t i = 0; i < n; i++) base[i] = (char*)ctxs[i]->xin_mem;
+        for (uint32_t i = 0; i < n; i++) {
+          ctxs[i]->x_base = base;
+          if (int rc = xpeer_upload(ctxs[i])) return rc;
+          ctxs[i]->x_mapped = true;
+        }
+      }
+      if (int rc = run_xpersist(sh, false, max_rounds, &pre)) return rc;
+      if (!ctxs[0]->x_off || pre >= max_rounds) {
+        if (rounds_done) *rounds_done = pre;
+        return 0;
+      }
+    }
+  }
+  max_rounds -= pre;
   // SGN_LOCAL_DEFER=1 (test hook): like the RCCL transport between its batch syncs, runs
   // k_import spilled stay in the spill area until a round is held (the next round's gathers
   // read them there)
@@ -291,7 +443,7 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
       if (ctxs[i]->h_ctrl->spill_n || ctxs[i]->h_ctrl->hold)
         if (int rc = resolve_pools(ctxs[i])) return rc;
     }
-  if (rounds_done) *rounds_done = done;
+  if (rounds_done) *rounds_done = pre + done;
   return 0;
 }
 

@@ -181,6 +181,40 @@ __device__ __forceinline__ void st_dev_rec(SGN_GLB EvRec* p, const EvRec& r) {
   st_wt16(q + 16, (uint64_t)r.src | ((uint64_t)r.dst << 32), (uint64_t)r.pc | ((uint64_t)r.tag << 32));
 }
 
+// Multi-shard exchange data (a peer shard's inbox: another GPU's memory over xGMI, or the
+// RCCL transport's send block): written through to memory at system scope (sc0 sc1), so the
+// record is in the receiver's memory when the writing wave's s_waitcnt vmcnt(0) completes — the
+// sender publishes its round-edge message only after every such store has completed.
+__device__ __forceinline__ void st_sys16(SGN_GLB void* p, uint64_t lo, uint64_t hi) {
+  u64x2 v;
+  v.x = lo;
+  v.y = hi;
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"((uint64_t)p), "v"(v));
+}
+__device__ __forceinline__ void st_sys_rec(SGN_GLB EvRec* p, const EvRec& r) {
+  SGN_GLB char* q = (SGN_GLB char*)p;
+  st_sys16(q, r.time, r.eid);
+  st_sys16(q + 16, (uint64_t)r.src | ((uint64_t)r.dst << 32), (uint64_t)r.pc | ((uint64_t)r.tag << 32));
+}
+__device__ __forceinline__ void st_sys(SGN_GLB uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys(SGN_GLB uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ EvRec ld_sys_rec(SGN_GLB const EvRec* p) {
+  SGN_GLB uint64_t* q = (SGN_GLB uint64_t*)p;
+  EvRec r;
+  r.time = ld_sys(q);
+  r.eid = ld_sys(q + 1);
+  const uint64_t sd = ld_sys(q + 2), pt = ld_sys(q + 3);
+  r.src = (uint32_t)sd;
+  r.dst = (uint32_t)(sd >> 32);
+  r.pc = (uint32_t)pt;
+  r.tag = (uint32_t)(pt >> 32);
+  return r;
+}
+
 // CoDel pool entries: a page serves other hosts (other workgroups, other XCDs) after it is
 // freed, so its entries are written through and read from memory like other cross-workgroup
 // data (a dirty L2 line of the previous owner must never overwrite the new owner's runs)
@@ -388,6 +422,8 @@ struct OutboxHdr {
   SGN_GLB uint64_t* pg_freed; // ... and the round's freed-page counter
   SGN_GLB uint64_t* pg_allocd;// ... and allocated-page counter (the round edge's guard)
   SGN_GLB uint64_t* spilled;  // runs this round put in the calendar's spill area
+  SGN_GLB uint32_t* xn;       // multi-shard: this round's per-peer run counters
+  uint32_t xbuf;              // ... and the peer blocks they go to (XPeer::runs[xbuf])
 };
 template <uint32_t N>
 struct OutboxN : OutboxHdr {
@@ -492,6 +528,8 @@ struct BigLDS {
   uint64_t kp[3];        // the last piece's upper bound (BigKey)
   uint64_t ib;           // the slab
   uint64_t tail;         // run(): a host's next packet time after its runs of this piece
+  uint64_t spill_imp;    // spill-area entries that may hold imported runs (multi-shard): set by
+                         // the round kernels (k_import's count, or k_rounds_x's after its imports)
   uint32_t ndue, done, have_prev, nraw, flush, pad;
 };
 
@@ -1660,10 +1698,12 @@ struct HostExec {
         if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
       }
       atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
-      pos = atomicAdd(&S.xout_n[lo], nrec);
+      pos = atomicAdd(&ob->xn[lo], nrec);
       sidx = SPILL_PEER | lo;  // (runs beyond the peer's slot: the slot grows at a held round)
-      dstp = S.xout + (size_t)lo * (S.xslot + XHDR) + XHDR;  // (a peer's block starts with the message)
-      cap = S.xslot;
+      // the peer's block: the RCCL transport's send block (after its message records), or the
+      // peer's inbox slot for this shard and round parity (persistent rounds: peer-mapped memory)
+      dstp = S.xp[lo].runs[ob->xbuf];
+      cap = ob->xbuf == 2 ? S.xslot : S.xislot;
     }
     for (uint32_t m = 0; m < nrec; m++) {
       const uint32_t k = min(RUN_MAX, nsent - m * RUN_MAX);
@@ -1674,9 +1714,12 @@ struct HostExec {
       r.dst = dsid;
       r.pc = payload | (k << 16);
       r.tag = tag;
-      if (pos + m < cap)
-        st_dev_rec(dstp + pos + m, r);
-      else if (owned)  // the slab is full: its extension, or the spill area
+      if (pos + m < cap) {
+        if (owned)
+          st_dev_rec(dstp + pos + m, r);
+        else
+          st_sys_rec(dstp + pos + m, r);
+      } else if (owned)  // the slab is full: its extension, or the spill area
         place_overflow(S, ob, sidx, pos + m, r);
       else  // the peer's exchange slot is full
         spill_run(S, ob, sidx, r);
@@ -2303,7 +2346,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       f(r, j < ne, ~0ULL);
     }
     if (nraw - np > ecap) {
-      const uint64_t ns = min(ld_dev(&C->spill_imp), S.spill_cap);
+      const uint64_t ns = min(X.big->spill_imp, S.spill_cap);
       for (uint64_t i0 = 0; i0 < ns; i0 += 64) {
         const uint64_t i = i0 + lane;
         const bool mine = i < ns && ld_dev(&S.spill_idx[i]) == (uint32_t)ib;
@@ -2334,7 +2377,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       f(t, e, src, j < ne);
     }
     if (nraw - np > ecap) {
-      const uint64_t ns = min(ld_dev(&C->spill_imp), S.spill_cap);
+      const uint64_t ns = min(X.big->spill_imp, S.spill_cap);
       for (uint64_t i0 = 0; i0 < ns; i0 += 64) {
         const uint64_t i = i0 + lane;
         const bool mine = i < ns && ld_dev(&S.spill_idx[i]) == (uint32_t)ib;
@@ -2778,7 +2821,10 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.ob = &ob_;                                                                       \
   X.big = &big_;                                                                     \
   X.wacc = nullptr;                                                                  \
-  if (threadIdx.x == 0) ob_.bmin = X.bmin;
+  if (threadIdx.x == 0) {                                                            \
+    ob_.bmin = X.bmin;                                                               \
+    big_.spill_imp = ld_dev(&S.ctrl->spill_imp);                                     \
+  }
 
 // The workgroup's LDS table of bucket minima (S.agg_bmin): its sends of the round fold their
 // delivery times there with LDS atomics; before the round's arrival every lane publishes a
@@ -2859,6 +2905,8 @@ __global__ __launch_bounds__(64, 2) void k_execute(const DevSim* __restrict__ Sg
     X.ob->pg_freed = &C->pg_freed;
     X.ob->pg_allocd = &C->rnd_alloc;
     X.ob->spilled = &C->rnd_spill;
+    X.ob->xn = S.xout_n;
+    X.ob->xbuf = 2;  // (the RCCL send blocks)
   }
   init_bmin<kApp>(S, X);
   __syncthreads();
@@ -3264,6 +3312,442 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       st_dev(&C->rounds, rounds0 + r);
       st_dev(&C->pg_avail, rs.pg_avail);
       st_dev(&C->cal_occ, rs.occ);
+      if (rs.hold) {
+        st_dev(&C->hold, rs.hold);
+        st_dev(&C->hold_need, rs.hold_need);
+      }
+    }
+  }
+}
+
+// ---- persistent multi-shard rounds (k_rounds_x) ----
+// N shards, each on its own GPU (one launch per GPU) or, for the one-GPU rehearsal, on its own
+// range of workgroups of ONE launch. A round of shard s is the single-shard persistent round
+// (k_rounds) plus the exchange that replaces the RCCL send/recv and k_import:
+//  1. execute: runs for another shard's hosts go straight into that shard's inbox slot for this
+//     shard and round parity (peer-mapped memory, system-scope write-through stores), counted
+//     per peer in local counters (Worker::send_packet pushes into the destination host's queue
+//     from any thread: core/worker.rs:603-613);
+//  2. the local barrier (k_rounds' chunk counters) and the local round edge (rb_edge: this
+//     shard's minima, the runs it exported included);
+//  3. the shard's last workgroup writes one 128-B message per shard (its own included) into the
+//     receivers' inboxes — run count, min next event, min used latency, the pool figures every
+//     shard needs for the same hold decisions — and then, after every store has completed, the
+//     message's tag (the global round number);
+//  4. every workgroup waits for the N messages of its own inbox and computes the next window
+//     from them: the min over messages is the min over all pending events (each message counts
+//     its shard's, exported runs included), i.e. the RCCL min all-reduce of the north star and
+//     Controller::manager_finished_current_round (controller.rs:88-112) over the global min;
+//  5. the workgroups file the runs of their inbox into the local calendar (k_import's work) and
+//     meet at a second local barrier before the next round's gathers read the slabs.
+// Inbox slots alternate by round parity: a sender writes round r + 1's runs while the receiver
+// may still be filing round r's. Rounds that would need more than a slot, or a larger pool, or a
+// re-layout, are held on every shard alike (the same messages, the same decisions) and the host
+// completes them between launches.
+constexpr uint32_t XR_MAX = 8;  // shards of a persistent multi-shard run (one MI355X node)
+constexpr uint64_t kXWaitTicks = 2000000000ull;  // 20 s on the 100 MHz clock: a peer that never
+                                                 // answers is an error (OVF_TIMEOUT), not a hang
+
+template <uint32_t kApp>
+__device__ __forceinline__ bool rb_wait(SGN_GLB uint32_t* top, uint32_t nch) {
+  uint32_t spins = 0;
+  while (ld_dev(top) < nch) {
+    __builtin_amdgcn_s_sleep(kApp == SGN_TRAFFIC_TGEN ? 16 : kApp == SGN_TRAFFIC_PERIODIC ? 8 : 1);
+    if (++spins > (1u << 22)) return false;
+  }
+  return true;
+}
+
+// the second local barrier (after the imports): chunk counters, then the top counter
+template <uint32_t kApp>
+__device__ __forceinline__ void rb2_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw) {
+  if (threadIdx.x != 0) return;
+  using Y = RbLayout<kApp>;
+  const uint32_t ch = w >> 6;
+  const uint32_t csz = min(64u, nw - (ch << 6));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's imports are in place
+  SGN_GLB uint32_t* cnt = S.rb2_cnt + (size_t)p * Y::CB;
+  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <uint32_t kApp>
+__global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ L, uint32_t max_rounds) {
+  // this workgroup's shard and its place in the shard's range
+  const uint32_t nl = L->n_local;
+  uint32_t si = 0;
+  while (si + 1 < nl && blockIdx.x >= L->base[si + 1]) si++;
+  const DevSim& S = *L->S[si];
+  SGN_GLB Ctrl* C = S.ctrl;
+  const uint32_t w_i = blockIdx.x - L->base[si], P_i = L->base[si + 1] - L->base[si];
+  SGN_EXEC_LDS(X)
+  if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+    __shared__ uint64_t wacc_[W_N];
+    X.wacc = wacc_;
+    if (threadIdx.x < W_N) wacc_[threadIdx.x] = 0;
+  }
+  // the workgroup's groups, as in k_rounds
+  uint32_t gq0_i = w_i, gq1_i = S.G, gqs_i = P_i;
+  if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
+    const uint32_t x = w_i & 7u, cx = (P_i - x + 7u) >> 3;
+    uint32_t before = 0;
+    for (uint32_t y = 0; y < x; y++) before += (P_i - y + 7u) >> 3;
+    const uint32_t s0 = (uint32_t)((uint64_t)S.G * before / P_i), s1 = (uint32_t)((uint64_t)S.G * (before + cx) / P_i);
+    gq0_i = s0 + (w_i >> 3);
+    gq1_i = s1;
+    gqs_i = cx;
+  }
+  const uint32_t w = w_i, P = P_i, gq0 = gq0_i, gq1 = gq1_i, gqs = gqs_i;
+  const uint32_t R = S.n_ranks, me = S.rank;
+  const uint32_t nch = (P + 63) >> 6;
+  const uint32_t wbk = P - 1;  // this shard's bookkeeping workgroup (and its messages)
+  // residency census over the whole launch (the control block of its first shard), then, one
+  // shard per GPU, over the shards: every shard publishes its verdict to every inbox and waits for
+  // all of them — a grid that is not resident anywhere makes every shard fall back alike
+  {
+    __shared__ uint32_t verdict;
+    SGN_GLB Ctrl* C0 = L->S[0]->ctrl;
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(&C0->res_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t v = 0, spins = 0;
+      bool decided = false;
+      while ((v = ld_dev(&C0->res_verdict)) == 0) {
+        if (ld_dev(&C0->res_arrive) >= gridDim.x) {
+          v = 1;
+        } else if (++spins > (1u << 14)) {
+          v = 2;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        uint32_t expect = 0;
+        decided = __hip_atomic_compare_exchange_strong(&C0->res_verdict, &expect, v, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = ld_dev(&C0->res_verdict);
+        break;
+      }
+      if (L->peers_census) {
+        const uint64_t ep = L->epoch << 2;
+        if (decided)  // the deciding workgroup tells every shard (its own inbox too)
+          for (uint32_t q = 0; q < R; q++) st_sys(S.xp[q].cen, ep | v);
+        if (v == 1) {  // a peer that is not resident (or never answers) stops this shard too
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t q = 0; q < R && v == 1; q++) {
+            uint64_t c;
+            while (((c = ld_sys(&S.xin_cen[q])) >> 2) != L->epoch) {
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
+                c = ep | 2;
+                atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(8);
+            }
+            if ((c & 3) != 1) v = 3;
+          }
+        }
+      }
+      verdict = v;
+    }
+    __syncthreads();
+    if (verdict != 1) {
+      if (verdict == 3 && w == P - 1 && threadIdx.x == 0) st_dev(&C->res_verdict, 3u);
+      return;
+    }
+  }
+  struct RoundLDS {
+    uint64_t ws, we, pend_ws, pend_we, pend_nb1, pg_avail;
+    uint64_t pg_alloc, occ, hold_need;
+    uint32_t active, ks, pend, pend_new, ngap, hold;
+    uint32_t n_in, nin[XR_MAX];  // runs to file this round: in all, and from each shard
+  };
+  __shared__ RoundLDS rs;
+  if (threadIdx.x == 0) {
+    rs.pg_avail = ld_dev(&C->pg_avail);
+    rs.ws = ld_dev(&C->ws);
+    rs.we = ld_dev(&C->we);
+    rs.active = ld_dev(&C->active);
+    rs.ks = ld_dev(&C->keep_slab);
+    rs.pend = 0;
+    rs.ngap = 0;
+    rs.pg_alloc = ld_dev(&C->pg_alloc);
+    rs.occ = ld_dev(&C->cal_occ);
+    rs.hold = ld_dev(&C->hold);
+    rs.hold_need = ld_dev(&C->hold_need);
+  }
+  const uint64_t rounds0 = ld_dev(&C->rounds);
+  for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
+  init_bmin<kApp>(S, X);
+  __syncthreads();
+  uint32_t r = 0;
+  for (; r < max_rounds; r++) {
+    if (!__builtin_amdgcn_readfirstlane((int)rs.active) || __builtin_amdgcn_readfirstlane((int)rs.hold)) break;
+    const uint64_t ws = uni64(rs.ws), we = uni64(rs.we);
+    const uint32_t ks = (uint32_t)__builtin_amdgcn_readfirstlane((int)rs.ks);
+    const uint32_t p = r % 3;
+    if (w == wbk) {
+      if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
+      // reset buffer (r + 1) % 3 for the next round: minima, counters, both barriers, exports
+      const uint32_t q = (r + 1) % 3;
+      for (uint32_t i = threadIdx.x; i < nch; i += 64) {
+        st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS], (uint64_t)INVALID);
+        st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS + 1], (uint64_t)INVALID);
+        st_dev(&S.rb_occ[((size_t)q * RB_CH + i) * RbLayout<kApp>::OS], (uint64_t)0);
+      }
+      for (uint32_t i = threadIdx.x; i <= nch; i += 64) {
+        const size_t o = (size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS;
+        st_dev(&S.rb_cnt[o], 0u);
+        st_dev(&S.rb2_cnt[o], 0u);
+      }
+      for (uint32_t i = threadIdx.x; i < R; i += 64) st_dev(&S.xout_n[q * R + i], 0u);
+      if (threadIdx.x == 0) {
+        st_dev(&S.rb_keep[q], (uint64_t)INVALID);
+        st_dev(&S.rb_free[q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + q], (uint64_t)0);
+        st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + q], (uint64_t)0);
+      }
+    }
+    if (threadIdx.x == 0) {
+      X.ob->keepmin = &S.rb_keep[p];
+      X.ob->bbase = ws;
+      X.ob->pg_avail = rs.pg_avail;
+      X.ob->pg_freed = &S.rb_free[p];
+      X.ob->pg_allocd = &S.rb_occ[3 * RB_CH * RB_OS_MAX + p];
+      X.ob->spilled = &S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p];
+      X.ob->xn = S.xout_n + (size_t)p * R;
+      X.ob->xbuf = (uint32_t)((rounds0 + r + 1) & 1);
+    }
+    // ---- 1. execute this workgroup's groups ----
+    uint64_t kall = INVALID, mall = INVALID, oall = 0;
+    bool arrived = false;
+    for (uint32_t g = gq0; g < gq1; g += gqs) {
+      uint64_t kmin, m;
+      const bool lastg = g + gqs >= gq1;
+      exec_group<false, kApp, true>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
+        kall = k < kall ? k : kall;
+        mall = n < mall ? n : mall;
+        oall += od;
+        if (lastg) {
+          flush_bmin<kApp>(S, X);
+          rb_arrive<kApp>(S, p, w, P, kall, mall, oall);
+          arrived = true;
+        }
+      });
+      __syncthreads();
+    }
+    if (!arrived) rb_arrive<kApp>(S, p, w, P, INVALID, INVALID, 0);
+    // ---- 2. the local barrier and this shard's round edge ----
+    if (!rb_wait<kApp>(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
+      if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+      return;
+    }
+    asm volatile("" ::: "memory");
+    const uint64_t tag = rounds0 + r + 1;  // the global round number + 1 (the same on every shard)
+    const uint32_t buf = (uint32_t)(tag & 1);
+    const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
+    // (the lane index laundered every round: the compiler would otherwise hoist this section's
+    // lane-dependent values out of the round loop and keep them in registers through the
+    // execute phase, where the round kernels have none to spare)
+    uint32_t lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    // ---- 3. this shard's message to every shard ----
+    if (w == wbk) {
+      uint64_t cnt = 0;
+      if (lane < R && lane != me) cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
+      uint64_t xmax = cnt, xsum = cnt;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = shfl_xor64(xmax, off);
+        xmax = o > xmax ? o : xmax;
+        xsum += shfl_xor64(xsum, off);
+      }
+      const uint64_t spilled = ld_dev(&C->spill_n) != 0 ? 1u : 0u;
+      const uint64_t mu = ld_dev(&C->min_used);
+      if (lane < R) {
+        SGN_GLB uint64_t* h = S.xp[lane].hdr[buf];
+        st_sys(h + XH_CNT, cnt);
+        st_sys(h + XH_MIN, e.min_next);
+        st_sys(h + XH_MU, mu);
+        st_sys(h + XH_XMAX, xmax);
+        st_sys(h + XH_SPILL, spilled);
+        st_sys(h + XH_PFREE, pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc));
+        st_sys(h + XH_OCC, rs.occ + e.occd);
+        st_sys(h + XH_XSUM, xsum);
+        st_sys(h + XH_CAPB, (uint64_t)S.G * S.CAP + S.ext_total);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the message is in the receiver's memory
+        st_sys(h + XH_TAG, tag);
+      }
+    }
+    // ---- 4. every shard's message, then the next window (the same on every shard) ----
+    uint64_t mv[XH_CAPB + 1];
+    {
+      bool ok = true;
+      if (lane < R) {
+        SGN_GLB uint64_t* h = S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_sys(h + XH_TAG) != tag) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = ok ? ld_sys(h + k) : 0;
+      } else {
+#pragma unroll
+        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = 0;
+      }
+      if (__ballot(!ok)) {
+        if (lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+        return;
+      }
+    }
+    const bool sender = lane < R;
+    uint64_t gm = sender ? mv[XH_MIN] : INVALID, gmu = sender ? mv[XH_MU] : INVALID;
+    uint64_t xs = sender ? mv[XH_XSUM] : 0, xmax = sender ? mv[XH_XMAX] : 0;
+    uint32_t spill_any = sender && mv[XH_SPILL] ? 1u : 0u;
+    // runs this shard files from each sender (the slot holds at most xslot; the rest wait in the
+    // sender's spill area and the round edge holds for the host to move them)
+    const uint32_t nin_l = sender && lane != me ? (uint32_t)min(mv[XH_CNT], (uint64_t)S.xislot) : 0u;
+    gm = wave_min_u64(gm);
+    gmu = wave_min_u64(gmu);
+    xmax = wave_max_u64(xmax);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) xs += shfl_xor64(xs, off);
+    spill_any = __ballot(spill_any) ? 1u : 0u;
+    // Runahead::get (runahead.rs:44-57) over the global min used latency; the controller
+    // (controller.rs:88-112) over the global min next event
+    const uint64_t min_next = gm;  // (each message's minimum is already unwrapped: EMU_MAX = none)
+    uint64_t ra = (S.dynamic && gmu != INVALID) ? gmu : S.min_possible;
+    ra = ra > S.runahead_cfg ? ra : S.runahead_cfg;
+    uint64_t ne = min_next + ra;
+    if (ne < min_next || ne > EMU_MAX) ne = EMU_MAX;
+    ne = ne < S.end_time ? ne : S.end_time;
+    const uint32_t active = min_next < ne ? 1u : 0u;
+    // the next round's guards, evaluated for every shard from the messages alike (k_import's):
+    // CoDel pages for the next window's due runs (occupancy plus everything exported this round,
+    // a bound on what any shard receives), a re-layout after spills, the inbox slots
+    uint32_t hflags = 0;
+    uint64_t own_need = 0;
+    if (active) {
+      const uint32_t nbk = ((bucket_of(S, ne - 1) - bucket_of(S, min_next)) & (S.NB - 1)) + 1;
+      uint32_t hq = 0;
+      if (sender) {
+        const uint64_t occ = mv[XH_OCC] + xs, capb = (uint64_t)nbk * mv[XH_CAPB] + xs;
+        const uint64_t need = codel_pages_bound(occ < capb ? occ : capb, S.rank_lo[lane + 1] - S.rank_lo[lane]);
+        if (mv[XH_PFREE] < need) hq |= HOLD_CODEL;
+        if (lane == me) own_need = need;
+      }
+      hflags = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u64(hq));  // (one flag)
+      own_need = shfl64(own_need, (int)me);
+      if (spill_any) hflags |= HOLD_SPILL;
+      if (xmax > S.xislot) hflags |= HOLD_XSLOT;
+      else if (2 * xmax > S.xislot) hflags |= HOLD_XGROW;
+    }
+    uint32_t n_in = nin_l;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off, 64);
+    // the idle-gap case of k_rounds: the bookkeeping now, and a local barrier before any send of
+    // the next round can reach this round's bucket indices again
+    const uint64_t span = (uint64_t)S.NB * S.BW;
+    const uint64_t bstart = SIM_START + S.bw_div.div(ws - SIM_START) * S.BW;
+    const bool gap = active && (ne + S.max_lat >= bstart + span || ne + S.max_lat < ne);
+    if (gap) {
+      if (w == wbk) rb_bookkeep(S, ws, we, e.nb1, ks);
+      if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        SGN_GLB uint32_t* gc = S.rb_cnt + 3 * RB_CB_MAX;
+        const uint32_t target = (rs.ngap + 1) * P;
+        __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t sp = 0;
+        while (ld_dev(gc) < target && ++sp < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+        if (sp >= (1u << 24)) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+        rs.ngap++;
+      }
+    }
+    if (lane < XR_MAX) rs.nin[lane] = nin_l;  // (lanes >= R hold 0)
+    __syncthreads();
+    const uint32_t b1 = bucket_of(S, we - 1);
+    if (threadIdx.x == 0) {
+      // the spare slab set (survivors + this round's new runs for b1) becomes bucket b1
+      const uint32_t slab_b1 = X.lbs[b1];
+      X.lbs[b1] = (uint16_t)ks;
+      rs.pend = gap ? 0u : 1u;
+      rs.pend_ws = ws;
+      rs.pend_we = we;
+      rs.pend_nb1 = e.nb1;
+      rs.pend_new = ks;
+      rs.ks = slab_b1;
+      rs.ws = min_next;
+      rs.we = ne;
+      rs.active = active;
+      rs.pg_avail += e.nfree;
+      rs.pg_alloc += e.nalloc;
+      rs.occ += e.occd + n_in;
+      rs.n_in = n_in;
+      rs.hold = hflags;
+      rs.hold_need = own_need;
+      if (w == wbk) {
+        st_dev(&C->last_min_next, min_next);
+        st_dev(&C->prev_we, we);
+        if (gmu != INVALID) min_nr(&C->min_used, gmu);  // (the next rounds' messages carry it)
+        // the largest per-peer count any shard produced (the host sizes the inbox slots by it)
+        (void)__hip_atomic_fetch_max(&C->xhwm, xmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    // ---- 5. the runs other shards sent this shard into its calendar, then a local barrier ----
+    if (uni32(rs.n_in)) {
+      const uint64_t hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
+      for (uint32_t i = w * 64 + lane; i < rs.n_in; i += P * 64) {
+        uint32_t q = 0, off = i;
+        while (off >= rs.nin[q]) off -= rs.nin[q++];
+        const EvRec ev = ld_sys_rec(S.xin_runs + ((size_t)buf * R + q) * S.xislot + off);
+        if (ev.time >= hz) {
+          if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = ev.dst;
+          continue;
+        }
+        const uint32_t b = bucket_of(S, ev.time);
+        const size_t idx = (size_t)X.lbs[b] * S.G + ((ev.dst - S.lo) >> S.gsh);
+        const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+        // (bucket b1's minimum is not needed: a run there makes the next window start in b1,
+        // whose minimum no round edge reads while it is the window's first bucket)
+        if (b != b1) min_nr(&S.bucket_min[b], ev.time);
+        if (pos < S.CAP)
+          st_dev_rec(S.pool + idx * S.CAP + pos, ev);
+        else  // the extension, or the spill area: the next round's gathers read it there, and the
+              // spill flag holds the round after that on every shard for the re-layout
+          place_overflow(S, nullptr, (uint32_t)idx, pos, ev);
+      }
+      rb2_arrive<kApp>(S, p, w, P);
+      if (!rb_wait<kApp>(&S.rb2_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
+        if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+        return;
+      }
+      if (threadIdx.x == 0) X.big->spill_imp = ld_dev(&C->spill_n);  // (imports past their slab)
+      __syncthreads();
+    }
+  }
+  // the launch's per-wave statistics (k_rounds)
+  __syncthreads();
+  if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x] && gq0 < gq1) {
+    const uint32_t k = threadIdx.x;
+    if (k == W_MAXFILL)
+      __hip_atomic_fetch_max(&S.w_cnt[k * S.G + gq0], X.wacc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      cnt_add(&S.w_cnt[k * S.G + gq0], X.wacc[k]);
+  }
+  if (w == wbk) {
+    if (rs.pend) rb_bookkeep(S, rs.pend_ws, rs.pend_we, rs.pend_nb1, rs.pend_new);
+    if (threadIdx.x == 0) {
+      st_dev(&C->keep_slab, rs.ks);
+      st_dev(&C->ws, rs.ws);
+      st_dev(&C->we, rs.we);
+      st_dev(&C->active, rs.active);
+      st_dev(&C->rounds, rounds0 + r);
+      st_dev(&C->pg_avail, rs.pg_avail);
+      st_dev(&C->cal_occ, rs.occ);
+      st_dev(&C->spill_imp, X.big->spill_imp);
       if (rs.hold) {
         st_dev(&C->hold, rs.hold);
         st_dev(&C->hold_need, rs.hold_need);
@@ -4014,6 +4498,7 @@ int grow_exchange_slot_impl(sgn_ctx* ctx) {
   S.xslot = (uint32_t)ns;
   ctx->xslot = ns;
   ctx->xslot_grows++;
+  if (int rc = xpeer_upload(ctx)) return rc;  // (the send blocks moved)
   return upload_sim(ctx);
 }
 
@@ -4156,8 +4641,307 @@ void drop_graph(sgn_ctx* ctx) {
   ctx->graph_pending = false;
 }
 
+// ---- persistent multi-shard rounds (k_rounds_x): host side ----
+// Inbox layout (one uncached allocation per shard): headers [2][R][XH_WORDS], census words [R]
+// (padded to a line), runs [2][R][xislot].
+XLay xlay(uint32_t R, uint64_t xislot) {
+  XLay l;
+  l.hdr = 0;
+  l.cen = (size_t)2 * R * XH_WORDS * 8;
+  l.runs = l.cen + ((size_t)R * 8 + 127) / 128 * 128;
+  l.bytes = l.runs + (size_t)2 * R * xislot * sizeof(EvRec);
+  return l;
+}
+
+void xinbox_release(sgn_ctx* ctx) {
+  for (void* p : ctx->x_opened)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  ctx->x_opened.clear();
+  if (ctx->xin_mem) {
+    (void)hipFree(ctx->xin_mem);
+    ctx->sim_bytes -= std::min<uint64_t>(ctx->sim_bytes, ctx->xin_bytes);
+  }
+  ctx->xin_mem = nullptr;
+  ctx->xin_bytes = 0;
+  ctx->x_base.clear();
+  ctx->x_mapped = false;
+}
+
+// A (new) inbox of xislot runs per sender and round parity, zeroed (no tag matches a round).
+// Uncached device memory: peers' stores reach it over xGMI and no L2 — the writer's or this
+// GPU's — keeps a copy, so the tags polled and the runs read here are the memory's. The old
+// inbox and the peer mappings go (the caller maps the new ones).
+int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot) {
+  DevSim& S = ctx->S;
+  const XLay l = xlay(ctx->nranks, xislot);
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, l.bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return set_error(ctx, SGN_ENOMEM, std::string("inbox allocation: ") + hipGetErrorString(e));
+  if ((e = hipMemset(p, 0, l.bytes)) != hipSuccess) {
+    (void)hipFree(p);
+    return hip_fail(ctx, e, "hipMemset (inbox)");
+  }
+  xinbox_release(ctx);
+  ctx->xin_mem = p;
+  ctx->xin_bytes = l.bytes;
+  ctx->sim_bytes += l.bytes;
+  S.xin_hdr = (decltype(S.xin_hdr))((char*)p + l.hdr);
+  S.xin_cen = (decltype(S.xin_cen))((char*)p + l.cen);
+  S.xin_runs = (decltype(S.xin_runs))((char*)p + l.runs);
+  S.xislot = (uint32_t)xislot;
+  return 0;
+}
+
+// This shard's XPeer table: its slot, header and census word in every shard's inbox
+// (ctx->x_base, by rank; none before the mapping) and the RCCL transport's send blocks.
+int xpeer_upload(sgn_ctx* ctx) {
+  DevSim& S = ctx->S;
+  const uint32_t R = ctx->nranks, s = ctx->rank;
+  const XLay l = xlay(R, S.xislot);
+  std::vector<XPeer> xp(R);
+  std::memset(xp.data(), 0, R * sizeof(XPeer));
+  for (uint32_t q = 0; q < R; q++) {
+    XPeer& x = xp[q];
+    char* b = q < ctx->x_base.size() ? ctx->x_base[q] : nullptr;
+    if (b) {
+      for (uint32_t k = 0; k < 2; k++) {
+        x.runs[k] = (std::remove_reference_t<decltype(x.runs[k])>)((EvRec*)(b + l.runs) + ((size_t)k * R + s) * S.xislot);
+        x.hdr[k] = (std::remove_reference_t<decltype(x.hdr[k])>)((uint64_t*)(b + l.hdr) + ((size_t)k * R + s) * XH_WORDS);
+      }
+      x.cen = (decltype(x.cen))((uint64_t*)(b + l.cen) + s);
+    }
+    if (S.xout) x.runs[2] = (std::remove_reference_t<decltype(x.runs[2])>)((EvRec*)S.xout + (size_t)q * (S.xslot + XHDR) + XHDR);
+  }
+  SGN_HIP(ctx, hipMemcpy(ctx->d_xp, xp.data(), R * sizeof(XPeer), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// The persistent multi-shard path runs where the persistent kernel would (the bucket -> slab
+// table in LDS, no per-packet trace) unless refused before or switched off (SGN_XPERSIST=0 or
+// SGN_PERSISTENT=0: per-round launches and the RCCL / local-copy exchange).
+bool xpersist_possible(sgn_ctx* ctx) {
+  static const bool off = (getenv("SGN_XPERSIST") && atoi(getenv("SGN_XPERSIST")) == 0) ||
+                          (getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0);
+  return ctx->nranks > 1 && ctx->nranks <= XR_MAX && ctx->sim_ready && ctx->xin_mem && ctx->S.NB <= LDS_BSLAB &&
+         !ctx->S.trace_on &&
+         !ctx->x_off && !ctx->persist_off && !off;
+}
+
+// runs into this shard's calendar at a held round edge (k_inject: the bucket's current slab)
+int inject_runs(sgn_ctx* ctx, const std::vector<EvRec>& runs) {
+  if (runs.empty()) return 0;
+  void* d = nullptr;
+  SGN_HIP(ctx, hipMalloc(&d, runs.size() * sizeof(EvRec)));
+  hipError_t e = hipMemcpy(d, runs.data(), runs.size() * sizeof(EvRec), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_inject, dim3((uint32_t)((runs.size() + 255) / 256)), dim3(256), 0, ctx->stream,
+                       (const DevSim*)ctx->d_S, (const EvRec*)d, (uint32_t)runs.size());
+    e = hipStreamSynchronize(ctx->stream);
+  }
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "inject_runs");
+  return 0;
+}
+
+namespace {
+const void* rounds_x_fn(uint32_t kind) {
+  if (kind == SGN_TRAFFIC_TGEN) return (const void*)k_rounds_x<SGN_TRAFFIC_TGEN>;
+  if (kind == SGN_TRAFFIC_EXTERNAL) return (const void*)k_rounds_x<SGN_TRAFFIC_EXTERNAL>;
+  return (const void*)k_rounds_x<SGN_TRAFFIC_PERIODIC>;
+}
+
+// One k_rounds_x launch of up to n rounds over the shards sh (all on sh[0]'s GPU and stream).
+// Returns 1 when no resident grid can be sized (the caller falls back to per-round launches).
+int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
+  sgn_ctx* c0 = sh[0];
+  const uint32_t kind = c0->S.tkind;
+  size_t lds = 0;
+  uint64_t sumG = 0;
+  for (sgn_ctx* c : sh) {
+    lds = std::max(lds, exec_lds_bytes(c->S.CAP, c->S.agg_bmin ? c->S.NB : 0));
+    sumG += c->S.G;
+  }
+  const uint64_t res = resident_wg(c0, rounds_x_fn(kind), lds);
+  if (!res || res < sh.size()) return 1;
+  if (!c0->x_hxl) SGN_HIP(c0, hipHostMalloc(&c0->x_hxl, sizeof(XLaunch), 0));
+  XLaunch& xl = *(XLaunch*)c0->x_hxl;
+  std::memset(&xl, 0, sizeof(xl));
+  xl.n_local = (uint32_t)sh.size();
+  xl.peers_census = peers ? 1u : 0u;
+  xl.epoch = ++c0->x_epoch;
+  uint32_t b = 0;
+  const char* cap_env = getenv("SGN_PERSIST_GRID");
+  for (size_t i = 0; i < sh.size(); i++) {
+    sgn_ctx* c = sh[i];
+    uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(c->S.G, res * c->S.G / sumG));
+    if (cap_env) P = std::max<uint64_t>(1, std::min<uint64_t>(P, (uint64_t)atoi(cap_env)));
+    P = std::min<uint64_t>(P, 64 * RB_CH);
+    xl.base[i] = b;
+    xl.S[i] = (const DevSim*)c->d_S;
+    b += (uint32_t)P;
+    c->x_grid = (uint32_t)P;
+    const DevSim& S = c->S;
+    hipStream_t st = c0->stream;
+    SGN_HIP(c, hipMemsetAsync((void*)S.rb_min, 0xFF, (3 * RB_CH * RB_MS_MAX + 4) * 8, st));
+    SGN_HIP(c, hipMemsetAsync((void*)S.rb_cnt, 0, (3 * RB_CB_MAX + 1) * 4, st));
+    SGN_HIP(c, hipMemsetAsync((void*)S.rb2_cnt, 0, 3 * RB_CB_MAX * 4, st));
+    SGN_HIP(c, hipMemsetAsync((void*)S.rb_free, 0, 3 * 8, st));
+    SGN_HIP(c, hipMemsetAsync((void*)S.rb_occ, 0, (3 * RB_CH * RB_OS_MAX + 6) * 8, st));
+    SGN_HIP(c, hipMemsetAsync((void*)S.xout_n, 0, (3 * (size_t)c->nranks + 8) * 4, st));
+    SGN_HIP(c, hipMemsetAsync((char*)S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, st));
+  }
+  xl.base[sh.size()] = b;
+  SGN_HIP(c0, hipMemcpyAsync(c0->d_xl, &xl, sizeof(XLaunch), hipMemcpyHostToDevice, c0->stream));
+  time_begin(c0, K_EXECUTE);
+  const dim3 grid(b), block(64);
+  const XLaunch* d = (const XLaunch*)c0->d_xl;
+  if (kind == SGN_TRAFFIC_TGEN)
+    hipLaunchKernelGGL((k_rounds_x<SGN_TRAFFIC_TGEN>), grid, block, lds, c0->stream, d, n);
+  else if (kind == SGN_TRAFFIC_EXTERNAL)
+    hipLaunchKernelGGL((k_rounds_x<SGN_TRAFFIC_EXTERNAL>), grid, block, lds, c0->stream, d, n);
+  else
+    hipLaunchKernelGGL((k_rounds_x<SGN_TRAFFIC_PERIODIC>), grid, block, lds, c0->stream, d, n);
+  time_end(c0);
+  c0->kt[K_EXECUTE].total++;
+  SGN_HIP(c0, hipGetLastError());
+  for (sgn_ctx* c : sh) {
+    c->x_launches++;
+    c->x_mode = 2;
+  }
+  return 0;
+}
+
+// A round edge held by k_rounds_x (every shard the same flags): runs past an inbox slot go from
+// the senders' spill areas into their shards' calendars, and the inboxes grow; then each shard's
+// own pools (resolve_hold). sh: every shard of the group (local) or this GPU's one (peers).
+int x_resolve(const std::vector<sgn_ctx*>& sh, bool peers) {
+  uint32_t hold = 0;
+  uint64_t hwm = 0;
+  for (sgn_ctx* c : sh) {
+    hold |= c->h_ctrl->hold;
+    hwm = std::max<uint64_t>(hwm, c->h_ctrl->xhwm);
+  }
+  const uint32_t xf = HOLD_XSLOT | HOLD_XGROW;
+  if (!(hold & xf)) {
+    for (sgn_ctx* c : sh)
+      if (int rc = resolve_hold(c)) return rc;
+    return 0;
+  }
+  for (sgn_ctx* c : sh) {  // the inbox flags are this function's: cleared before any growth
+    c->h_ctrl->hold &= ~xf;
+    SGN_HIP(c, hipMemcpy((char*)c->S.ctrl + offsetof(Ctrl, hold), &c->h_ctrl->hold, 4, hipMemcpyHostToDevice));
+  }
+  if (hold & HOLD_XSLOT) {
+    // each sender's runs past a peer's slot (spill-area entries tagged SPILL_PEER | peer)
+    std::vector<std::vector<std::vector<EvRec>>> out(sh.size());
+    for (size_t i = 0; i < sh.size(); i++) {
+      sgn_ctx* c = sh[i];
+      const DevSim& S = c->S;
+      out[i].assign(c->nranks, {});
+      const uint64_t n = std::min<uint64_t>(c->h_ctrl->spill_n, S.spill_cap);
+      if (!n) continue;
+      std::vector<uint32_t> idx(n);
+      std::vector<EvRec> rec(n);
+      SGN_HIP(c, hipMemcpy(idx.data(), (const void*)S.spill_idx, n * 4, hipMemcpyDeviceToHost));
+      SGN_HIP(c, hipMemcpy(rec.data(), (const void*)S.spill, n * sizeof(EvRec), hipMemcpyDeviceToHost));
+      bool any = false;
+      for (uint64_t k = 0; k < n; k++)
+        if ((idx[k] & SPILL_PEER) && idx[k] != SPILL_DEAD) {
+          out[i][idx[k] & ~SPILL_PEER].push_back(rec[k]);
+          idx[k] = SPILL_DEAD;
+          any = true;
+        }
+      if (any) SGN_HIP(c, hipMemcpy((void*)S.spill_idx, idx.data(), n * 4, hipMemcpyHostToDevice));
+    }
+    if (!peers) {
+      for (size_t i = 0; i < sh.size(); i++)
+        for (uint32_t q = 0; q < sh[i]->nranks; q++) {
+          sh[q]->x_moved += out[i][q].size();
+          if (int rc = inject_runs(sh[q], out[i][q])) return rc;
+        }
+    } else {
+      std::vector<EvRec> in;
+      if (int rc = comm_xmove_spills(sh[0], out[0], &in)) return rc;
+      sh[0]->x_moved += in.size();
+      if (int rc = inject_runs(sh[0], in)) return rc;
+    }
+    for (sgn_ctx* c : sh) c->x_over_rounds++;
+  }
+  // larger inboxes: 4x the largest per-peer count any round produced (every shard sees the same
+  // maximum: the same size everywhere), at least twice the slot
+  uint64_t ns = sh[0]->S.xislot;
+  do ns *= 2;
+  while (ns < 4 * hwm);
+  if (ns > (1ULL << 26)) return set_error(sh[0], SGN_EOVERFLOW, "inbox slot above 2^26 runs per sender");
+  for (sgn_ctx* c : sh)
+    if (int rc = xinbox_alloc(c, ns)) return rc;
+  if (!peers) {
+    std::vector<char*> base(sh.size());
+    for (size_t i = 0; i < sh.size(); i++) base[sh[i]->rank] = (char*)sh[i]->xin_mem;
+    for (sgn_ctx* c : sh) {
+      c->x_base = base;
+      if (int rc = xpeer_upload(c)) return rc;
+      c->x_mapped = true;
+    }
+  } else {
+    if (int rc = comm_xpeer_map(sh[0])) return rc;
+    if (!sh[0]->x_mapped) return set_error(sh[0], SGN_EDEVICE, "inbox growth: the peers' new inboxes could not be mapped");
+  }
+  for (sgn_ctx* c : sh) {
+    c->x_grows++;
+    if (int rc = upload_sim(c)) return rc;
+    if (int rc = sync_ctrl(c)) return rc;  // (the injected runs' occupancy and spills)
+    if (int rc = resolve_hold(c)) return rc;
+  }
+  return 0;
+}
+}  // namespace
+
+// Rounds through k_rounds_x until max_rounds, the end, or a refused census (every shard's x_off
+// set: the caller goes on with per-round launches). sh: the shards of one launch — a local
+// group's (rank order) or this GPU's one (peers: the census and messages cross GPUs).
+int run_xpersist(const std::vector<sgn_ctx*>& sh, bool peers, uint64_t max_rounds, uint64_t* rounds_done) {
+  sgn_ctx* c0 = sh[0];
+  for (sgn_ctx* c : sh)
+    if (int rc = sync_ctrl(c)) return rc;
+  const uint64_t r_start = c0->h_ctrl->rounds;
+  uint64_t enq = 0;
+  int rc = 0;
+  // (a round still held from an earlier call: its pools first)
+  if (!rc) rc = x_resolve(sh, peers);
+  while (!rc && c0->h_ctrl->active && enq < max_rounds) {
+    const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
+    const int lr = x_launch(sh, peers, n);
+    if (lr < 0) return lr;
+    if (lr == 0) SGN_HIP(c0, hipStreamSynchronize(c0->stream));
+    for (sgn_ctx* c : sh)
+      if ((rc = sync_ctrl(c))) break;
+    if (rc) break;
+    if (lr == 1 || c0->h_ctrl->res_verdict != 1) {
+      // not resident (here or on a peer): nothing ran; per-round launches from now on
+      for (sgn_ctx* c : sh) {
+        c->x_off = true;
+        c->x_mode = 1;
+        c->persist_fallbacks++;
+      }
+      break;
+    }
+    rc = x_resolve(sh, peers);
+    enq = c0->h_ctrl->rounds - r_start;
+  }
+  for (sgn_ctx* c : sh)  // (the per-round path counts its sends in row 0 from zero)
+    if (c->S.xout_n) (void)hipMemsetAsync((void*)c->S.xout_n, 0, (3 * (size_t)c->nranks + 8) * 4, c->stream);
+  if (rounds_done) *rounds_done = c0->h_ctrl->rounds - r_start;
+  return rc;
+}
+
 void free_sim(sgn_ctx* ctx) {
   drop_graph(ctx);
+  xinbox_release(ctx);
+  if (ctx->x_hxl) (void)hipHostFree(ctx->x_hxl);
+  ctx->x_hxl = nullptr;
+  ctx->d_xp = ctx->d_xl = nullptr;  // (in allocs)
+  ctx->x_mapped = false;
   ctx->rng_held.clear();
   if (ctx->d_rng_stage) hipFree(ctx->d_rng_stage);
   ctx->d_rng_stage = nullptr;
@@ -4511,9 +5295,27 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     // per peer a block of 1 + xslot records: the 32-byte round-edge message, then the runs
     S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
     S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
-    S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
+    // (per-round launches count in row 0; k_rounds_x in row round % 3)
+    S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 3 + 8);
     S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
+    // persistent rounds: the second barrier's counters, the XPeer table, the launch descriptor
+    // and this shard's inbox (SGN_XISLOT: a smaller first slot, a test hook for the growth path)
+    S.rb2_cnt = (decltype(S.rb2_cnt))dalloc<uint32_t>(ctx, 3 * RB_CB_MAX);
+    ctx->d_xp = dalloc<XPeer>(ctx, ctx->nranks);
+    ctx->d_xl = dalloc<XLaunch>(ctx, 1);
+    if (!S.rb2_cnt || !ctx->d_xp || !ctx->d_xl) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
+    S.xp = (decltype(S.xp))ctx->d_xp;
+    uint64_t xis = ctx->xslot;
+    if (const char* e = getenv("SGN_XISLOT")) xis = std::max<uint64_t>(1, std::min<uint64_t>(xis, (uint64_t)atoll(e)));
+    ctx->S = S;  // (xinbox_alloc / xpeer_upload work on ctx->S)
+    if ((rc = xinbox_alloc(ctx, xis)) || (rc = xpeer_upload(ctx))) return rc;
+    S = ctx->S;
+    ctx->x_off = false;
+    ctx->x_mode = 1;
+    ctx->x_epoch = ctx->x_grows = ctx->x_over_rounds = ctx->x_moved = ctx->x_launches = 0;
+    for (sgn_ctx* g : ctx->group)  // (a local group maps every member's inbox at its next run)
+      if (g) g->x_mapped = false;
   }
   Ctrl c{};
   c.ws = SIM_START;  // initial window (manager.rs:506-509)
@@ -4675,9 +5477,23 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
     return 0;
   }
+  // multi-shard, one shard per GPU: persistent rounds with the peers' inboxes mapped into this
+  // process (k_rounds_x; mapped at the first run, a collective over RCCL), unless refused — then
+  // per-round launches with the RCCL send/recv for the rest
+  if (ctx->nranks > 1 && ctx->comm && xpersist_possible(ctx)) {
+    if (!ctx->x_mapped && (rc = comm_xpeer_map(ctx))) return rc;
+    if (ctx->x_mapped) {
+      uint64_t k = 0;
+      if ((rc = run_xpersist({ctx}, true, max_rounds, &k))) return rc;
+      if (!ctx->x_off || k >= max_rounds || !ctx->h_ctrl->active) {
+        if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
+        return 0;
+      }
+    }
+  }
   // rounds are counted as they complete: a multi-shard round held for a full-slot exchange
   // (comm_complete_spill) turns the rest of its batch into no-ops, which are not rounds
-  uint64_t done = 0;
+  uint64_t done = ctx->h_ctrl->rounds - r_start;
   static const bool dbg = getenv("SGN_DEBUG_RUN") != nullptr;
   while (ctx->h_ctrl->active && done < max_rounds) {
     const uint64_t n = std::min<uint64_t>(batch, max_rounds - done);
@@ -4957,6 +5773,13 @@ int sgn_engine_info_get(sgn_ctx* ctx, sgn_engine_info* out) {
   }
   out->spill_area_runs = ctx->S.spill_cap;
   out->spill_area_grows = ctx->spill_grows;
+  out->exchange_mode = ctx->nranks > 1 ? ctx->x_mode : 0;
+  out->inbox_slot_runs = ctx->nranks > 1 ? ctx->S.xislot : 0;
+  out->inbox_grows = ctx->x_grows;
+  out->inbox_overflow_rounds = ctx->x_over_rounds;
+  out->inbox_moved_runs = ctx->x_moved;
+  out->persistent_x_launches = ctx->x_launches;
+  out->persistent_x_grid = ctx->x_grid;
   return 0;
 }
 
@@ -4976,6 +5799,7 @@ int sgn_kernel_times_get(sgn_ctx* ctx, sgn_kernel_times* out) {
   }
   // the round kernel's slot: persistent launches (many rounds each) when enabled
   if (ctx->persist_grid) out->name[K_EXECUTE] = "k_rounds";
+  if (ctx->x_mode == 2) out->name[K_EXECUTE] = "k_rounds_x";
   return 0;
 }
 

@@ -144,6 +144,9 @@ static_assert(offsetof(Ctrl, min_used) == offsetof(Ctrl, round_min) + 8,
 enum : uint32_t {
   HOLD_CODEL = 1u,  // the next round could take more CoDel pages than the pool has free
   HOLD_SPILL = 2u,  // runs went to the calendar's spill area: the calendar is re-laid out
+  HOLD_XSLOT = 4u,  // persistent multi-shard: some shard sent a peer more runs than its inbox slot
+                    // holds (the rest wait in the sender's spill area: the host moves them)
+  HOLD_XGROW = 8u,  // persistent multi-shard: a round used more than half an inbox slot (grow)
 };
 
 enum : uint32_t {
@@ -407,6 +410,53 @@ struct DevSim {
   uint32_t xslot;    // run capacity per peer block
   uint32_t rank;
   SGN_GLB const uint32_t* rank_lo;  // [n_ranks + 1] host ranges
+  // persistent multi-shard rounds (k_rounds_x): this shard's view of every shard's inbox (xp[q],
+  // q = this shard: its own), its own inbox (headers [2][n_ranks][XH_WORDS], runs [2][n_ranks]
+  // [xslot], census words [n_ranks]), and the second barrier's counters (after the imports)
+  SGN_GLB const struct XPeer* xp;
+  SGN_GLB uint64_t* xin_hdr;
+  SGN_GLB EvRec* xin_runs;
+  SGN_GLB uint64_t* xin_cen;
+  SGN_GLB uint32_t* rb2_cnt;  // [3][RB_CB_MAX]
+  uint32_t xislot;            // inbox runs per sender and round parity
+  uint32_t pad_x;
+};
+
+// Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and
+// round parity a header line (the round-edge message, XH_WORDS u64, word 0 = the round tag,
+// stored last) and a slot of xslot runs — that the senders write directly (peer-mapped memory
+// across GPUs, ordinary device memory when the shards are workgroup ranges of one launch).
+// XPeer is one sender's view of one receiver's inbox: where its runs and its message go in each
+// round parity, and its census word. runs[2] is the RCCL transport's send block (per-round path).
+struct XPeer {
+  SGN_GLB EvRec* runs[3];
+  SGN_GLB uint64_t* hdr[2];
+  SGN_GLB uint64_t* cen;
+  uint64_t pad[2];
+};
+constexpr uint32_t XH_WORDS = 16;  // one 128-B line per message
+// message words (XH_*): what every shard needs to take the same round-edge decisions
+enum : uint32_t {
+  XH_TAG = 0,    // global round number + 1 (stored last, after the rest has completed)
+  XH_CNT,        // runs the sender put in this receiver's slot this round (may exceed the slot)
+  XH_MIN,        // the sender's min next event time, the runs it exported included (INVALID: none)
+  XH_MU,         // the sender's min used latency (dynamic runahead; INVALID: none)
+  XH_XMAX,       // the sender's largest per-peer run count this round
+  XH_SPILL,      // the sender's spill area holds runs (the calendar must be re-laid out)
+  XH_PFREE,      // the sender's free CoDel pages for the next round
+  XH_OCC,        // the sender's calendar occupancy (before this round's imports)
+  XH_XSUM,       // runs the sender exported this round (a bound on what any shard receives)
+  XH_CAPB,       // the sender's slab runs per bucket (extensions included)
+};
+// k_rounds_x launch descriptor (device memory): the shards this launch runs, each on a
+// contiguous range of workgroups (all shards of a local group on one GPU, or this GPU's one)
+constexpr uint32_t XL_MAX = 16;
+struct XLaunch {
+  uint32_t n_local;              // shards in this launch
+  uint32_t peers_census;         // 1: one shard per GPU: the census is exchanged with the peers
+  uint64_t epoch;                // launch number (census tags)
+  uint32_t base[XL_MAX + 1];     // workgroup range of local shard i: [base[i], base[i + 1])
+  const struct DevSim* S[XL_MAX];
 };
 
 constexpr uint32_t SPILL_PEER = 0x80000000u;  // spill area tag: a run for that peer shard's exchange slot
@@ -531,6 +581,21 @@ struct sgn_ctx {
   std::string failed;  // sticky: an operation left the device state unusable (every call fails)
   uint64_t codel_allocs_before = 0;  // page allocations before the last pool growth (its ring restarts)
   bool capturing = false;
+  // persistent multi-shard rounds (k_rounds_x): this shard's inbox (uncached device memory:
+  // peers write it over xGMI), its XPeer table, peer inboxes opened from IPC handles (one shard
+  // per GPU), the launch descriptor, and the mode the rounds run in
+  void* xin_mem = nullptr;
+  size_t xin_bytes = 0;
+  void* d_xp = nullptr;
+  void* d_xl = nullptr;
+  std::vector<void*> x_opened;
+  std::vector<char*> x_base;   // every shard's inbox as this process addresses it (by rank)
+  void* x_hxl = nullptr;       // pinned host copy of the launch descriptor
+  bool x_mapped = false;       // the XPeer table points at every shard's current inbox
+  bool x_off = false;          // the persistent path was refused (mapping / residency): per-round
+  uint32_t x_mode = 0;         // 0 one shard, 1 per-round launches + exchange, 2 persistent rounds
+  uint32_t x_grid = 0;         // this shard's workgroups in the last k_rounds_x launch
+  uint64_t x_epoch = 0, x_grows = 0, x_over_rounds = 0, x_moved = 0, x_launches = 0;
 
   ~sgn_ctx();
 };
@@ -559,6 +624,21 @@ int comm_round_exchange(sgn_ctx* ctx);
 int comm_bcast_blocks(sgn_ctx* ctx, void* base, size_t unit_bytes, const std::vector<uint64_t>& off);
 int comm_allreduce_minmax(sgn_ctx* ctx, uint64_t* p, size_t n_min, size_t n_max);
 int comm_allreduce_max_u32(sgn_ctx* ctx, uint32_t* p, size_t n);
+// persistent multi-shard rounds (engine.hip: the launches; comm.cpp: the IPC mapping over RCCL)
+struct XLay {
+  size_t hdr, cen, runs, bytes;
+};
+XLay xlay(uint32_t R, uint64_t xislot);
+int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot);
+void xinbox_release(sgn_ctx* ctx);
+int xpeer_upload(sgn_ctx* ctx);  // the XPeer table from ctx->x_base (and the RCCL send blocks)
+bool xpersist_possible(sgn_ctx* ctx);
+int run_xpersist(const std::vector<sgn_ctx*>& sh, bool peers, uint64_t max_rounds, uint64_t* rounds_done);
+int comm_xpeer_map(sgn_ctx* ctx);       // one shard per GPU: map every peer's inbox (collective)
+int comm_xmove_spills(sgn_ctx* ctx, const std::vector<std::vector<EvRec>>& out,
+                      std::vector<EvRec>* in);  // runs past an inbox slot, to their shards (collective)
+int comm_allreduce_max_u64(sgn_ctx* ctx, uint64_t* host_v, size_t n);  // (host values, collective)
+int inject_runs(sgn_ctx* ctx, const std::vector<EvRec>& runs);      // engine.hip: into the calendar
 }  // namespace sgn
 
 #define SGN_HIP(ctx, call)                                   \

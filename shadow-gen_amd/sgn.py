@@ -179,7 +179,9 @@ class EngineInfo(C.Structure):
         "codel_page_allocs", "codel_pages_free", "codel_pages_chained",
         "compute_units", "bucket_min_lds", "lds_per_cu", "codel_pool_grows", "calendar_grows",
         "calendar_spill_runs", "exchange_slot_grows", "rounds_held", "slab_extensions",
-        "slab_extension_runs", "big_slab_pieces", "spill_area_runs", "spill_area_grows")]
+        "slab_extension_runs", "big_slab_pieces", "spill_area_runs", "spill_area_grows",
+        "exchange_mode", "inbox_slot_runs", "inbox_grows", "inbox_overflow_rounds", "inbox_moved_runs",
+        "persistent_x_launches", "persistent_x_grid")]
 
 
 class KernelTimes(C.Structure):

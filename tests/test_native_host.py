@@ -66,13 +66,20 @@ def test_round_kernels_have_no_scratch():
     meta = _kernel_meta(ROOT / "shadow-gen_amd" / "libsgn.so")
     # one instantiation per traffic kind; k_rounds also with / without the big-slab path,
     # k_execute per trace mode (traced / lean)
-    for k, count in (("k_rounds", 6), ("k_execute", 6)):
+    for k, count in (("k_roundsI", 6), ("k_execute", 6)):
         names = [n for n in meta if k in n]
         assert len(names) == count, names
         for name in names:
             m = meta[name]
             assert m["private_segment_fixed_size"] == 0, (name, m)
             assert m["vgpr_spill_count"] == 0 and m["vgpr_count"] <= 256, (name, m)
+    # the persistent multi-shard kernel (one per traffic kind): its exchange state on top of the
+    # big-slab path leaves a few spill slots outside the event loop; bounded here
+    names = [n for n in meta if "k_rounds_x" in n]
+    assert len(names) == 3, names
+    for name in names:
+        m = meta[name]
+        assert m["vgpr_count"] <= 256 and m["private_segment_fixed_size"] <= 256, (name, m)
 
 
 @pytest.mark.skipif(not pathlib.Path("/opt/rocm/lib/llvm/bin/clang-offload-bundler").exists(),
