@@ -188,7 +188,10 @@ int comm_xpeer_map(sgn_ctx* ctx) {
   for (void* p : ctx->x_opened)
     if (p) (void)hipIpcCloseMemHandle(p);
   ctx->x_opened.clear();
-  static_assert(sizeof(hipIpcMemHandle_t) <= 128, "IPC handle size");
+  // per shard: its inbox handle and its GPU's PCI bus id (shards sharing one GPU — the one-GPU
+  // RCCL rehearsal — would need their persistent grids resident side by side: only with
+  // SGN_XPEER_SHARED=1, each grid sized for its share of the GPU; else the per-round path)
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
   constexpr size_t HB = 128;
   std::vector<uint8_t> mine(HB, 0), all((size_t)R * HB, 0);
   uint64_t bad = 0;
@@ -197,6 +200,7 @@ int comm_xpeer_map(sgn_ctx* ctx) {
     bad = 1;
   else
     std::memcpy(mine.data(), &h, sizeof(h));
+  if (hipDeviceGetPCIBusId((char*)mine.data() + 64, 63, ctx->device) != hipSuccess) bad = 1;
   void* d = nullptr;
   SGN_HIP(ctx, hipMalloc(&d, (R + 1) * HB));
   hipError_t e = hipMemcpy(d, mine.data(), HB, hipMemcpyHostToDevice);
@@ -206,6 +210,11 @@ int comm_xpeer_map(sgn_ctx* ctx) {
   (void)hipFree(d);
   if (r != ncclSuccess) return set_error(ctx, SGN_EDEVICE, std::string("RCCL all-gather (inbox handles): ") + ncclGetErrorString(r));
   if (e != hipSuccess) return hip_fail(ctx, e, "inbox handle exchange");
+  ctx->x_share = 0;
+  for (uint32_t q = 0; q < R; q++)
+    ctx->x_share += std::memcmp(all.data() + (size_t)q * HB + 64, mine.data() + 64, 64) == 0 ? 1u : 0u;
+  const char* sh = getenv("SGN_XPEER_SHARED");
+  if (ctx->x_share > 1 && !(sh && atoi(sh) == 1)) bad = 1;
   std::vector<char*> base(R, nullptr);
   base[ctx->rank] = (char*)ctx->xin_mem;
   for (uint32_t q = 0; q < R && !bad; q++) {

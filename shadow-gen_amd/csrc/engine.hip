@@ -4761,7 +4761,7 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
     lds = std::max(lds, exec_lds_bytes(c->S.CAP, c->S.agg_bmin ? c->S.NB : 0));
     sumG += c->S.G;
   }
-  const uint64_t res = resident_wg(c0, rounds_x_fn(kind), lds);
+  const uint64_t res = resident_wg(c0, rounds_x_fn(kind), lds) / std::max<uint32_t>(1, peers ? c0->x_share : 1);
   if (!res || res < sh.size()) return 1;
   if (!c0->x_hxl) SGN_HIP(c0, hipHostMalloc(&c0->x_hxl, sizeof(XLaunch), 0));
   XLaunch& xl = *(XLaunch*)c0->x_hxl;

@@ -595,6 +595,7 @@ struct sgn_ctx {
   bool x_off = false;          // the persistent path was refused (mapping / residency): per-round
   uint32_t x_mode = 0;         // 0 one shard, 1 per-round launches + exchange, 2 persistent rounds
   uint32_t x_grid = 0;         // this shard's workgroups in the last k_rounds_x launch
+  uint32_t x_share = 1;        // shards on this GPU (one shard per GPU: 1)
   uint64_t x_epoch = 0, x_grows = 0, x_over_rounds = 0, x_moved = 0, x_launches = 0;
 
   ~sgn_ctx();
