@@ -601,6 +601,10 @@ int sgn_debug_stamps(sgn_ctx* ctx, uint64_t* out, uint64_t cap, uint64_t* n);
 /* Per-round timeline of the last persistent launch (SGN_STAMPS=1): 128 x {earliest round
  * start, latest arrival at the round barrier, round edge done} on the 100 MHz clock. */
 int sgn_debug_rounds(sgn_ctx* ctx, uint64_t* out);
+/* the persistent multi-shard kernel's per-round timeline (SGN_STAMPS=2): 8 words per round for 128
+ * rounds — earliest start, latest local arrival, local barrier seen, messages sent, latest "all
+ * messages seen", latest imports filed, latest second barrier seen (100 MHz clock); resets */
+int sgn_debug_rounds_x(sgn_ctx* ctx, uint64_t* out);
 
 #ifdef __cplusplus
 }

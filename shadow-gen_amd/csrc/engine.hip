@@ -1715,9 +1715,9 @@ struct HostExec {
       r.pc = payload | (k << 16);
       r.tag = tag;
       if (pos + m < cap) {
-        if (owned)
+        if (owned || !S.xsys)
           st_dev_rec(dstp + pos + m, r);
-        else
+        else  // (another GPU's inbox)
           st_sys_rec(dstp + pos + m, r);
       } else if (owned)  // the slab is full: its extension, or the spill area
         place_overflow(S, ob, sidx, pos + m, r);
@@ -3516,6 +3516,20 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       X.ob->xn = S.xout_n + (size_t)p * R;
       X.ob->xbuf = (uint32_t)((rounds0 + r + 1) & 1);
     }
+    // diagnostics (SGN_STAMPS=2): per round of this launch, on the 100 MHz clock: {earliest start,
+    // latest local arrival, local barrier seen (last workgroup), its messages sent, latest "all
+    // messages seen", latest imports filed, latest second barrier seen}
+    SGN_GLB uint64_t* rd = S.rdbg ? S.rdbg + 8 * (size_t)(r & 127) : nullptr;
+    auto stamp = [&](uint32_t i, bool mx) {
+      if (rd && threadIdx.x == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (mx)
+          __hip_atomic_fetch_max(rd + i, (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_fetch_min(rd + i, (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    stamp(0, false);
     // ---- 1. execute this workgroup's groups ----
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
@@ -3528,6 +3542,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         oall += od;
         if (lastg) {
           flush_bmin<kApp>(S, X);
+          stamp(1, true);
           rb_arrive<kApp>(S, p, w, P, kall, mall, oall);
           arrived = true;
         }
@@ -3541,6 +3556,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       return;
     }
     asm volatile("" ::: "memory");
+    if (w == wbk) stamp(2, true);
     const uint64_t tag = rounds0 + r + 1;  // the global round number + 1 (the same on every shard)
     const uint32_t buf = (uint32_t)(tag & 1);
     const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
@@ -3564,18 +3580,23 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       const uint64_t mu = ld_dev(&C->min_used);
       if (lane < R) {
         SGN_GLB uint64_t* h = S.xp[lane].hdr[buf];
-        st_sys(h + XH_CNT, cnt);
-        st_sys(h + XH_MIN, e.min_next);
-        st_sys(h + XH_MU, mu);
-        st_sys(h + XH_XMAX, xmax);
-        st_sys(h + XH_SPILL, spilled);
-        st_sys(h + XH_PFREE, pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc));
-        st_sys(h + XH_OCC, rs.occ + e.occd);
-        st_sys(h + XH_XSUM, xsum);
-        st_sys(h + XH_CAPB, (uint64_t)S.G * S.CAP + S.ext_total);
+        const uint64_t v[XH_CAPB + 1] = {tag, cnt, e.min_next, mu, xmax, spilled,
+                                         pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
+                                         rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total};
+        if (S.xsys) {
+#pragma unroll
+          for (uint32_t k = 1; k <= XH_CAPB; k++) st_sys(h + k, v[k]);
+        } else {
+#pragma unroll
+          for (uint32_t k = 1; k <= XH_CAPB; k++) st_dev(h + k, v[k]);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the message is in the receiver's memory
-        st_sys(h + XH_TAG, tag);
+        if (S.xsys)
+          st_sys(h + XH_TAG, tag);
+        else
+          st_dev(h + XH_TAG, tag);
       }
+      stamp(3, true);
     }
     // ---- 4. every shard's message, then the next window (the same on every shard) ----
     uint64_t mv[XH_CAPB + 1];
@@ -3584,15 +3605,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       if (lane < R) {
         SGN_GLB uint64_t* h = S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (ld_sys(h + XH_TAG) != tag) {
+        const bool sys = S.xsys != 0;
+        while ((sys ? ld_sys(h + XH_TAG) : ld_dev(h + XH_TAG)) != tag) {
           if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
             ok = false;
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(1);
         }
 #pragma unroll
-        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = ok ? ld_sys(h + k) : 0;
+        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = ok ? (sys ? ld_sys(h + k) : ld_dev(h + k)) : 0;
       } else {
 #pragma unroll
         for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = 0;
@@ -3601,6 +3623,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         if (lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
         return;
       }
+      stamp(4, true);
     }
     const bool sender = lane < R;
     uint64_t gm = sender ? mv[XH_MIN] : INVALID, gmu = sender ? mv[XH_MU] : INVALID;
@@ -3702,7 +3725,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       for (uint32_t i = w * 64 + lane; i < rs.n_in; i += P * 64) {
         uint32_t q = 0, off = i;
         while (off >= rs.nin[q]) off -= rs.nin[q++];
-        const EvRec ev = ld_sys_rec(S.xin_runs + ((size_t)buf * R + q) * S.xislot + off);
+        SGN_GLB const EvRec* src = S.xin_runs + ((size_t)buf * R + q) * S.xislot + off;
+        const EvRec ev = S.xsys ? ld_sys_rec(src) : ld_dev_rec(src);
         if (ev.time >= hz) {
           if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = ev.dst;
           continue;
@@ -3719,11 +3743,13 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
               // spill flag holds the round after that on every shard for the re-layout
           place_overflow(S, nullptr, (uint32_t)idx, pos, ev);
       }
+      stamp(5, true);
       rb2_arrive<kApp>(S, p, w, P);
       if (!rb_wait<kApp>(&S.rb2_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
         if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
         return;
       }
+      stamp(6, true);
       if (threadIdx.x == 0) X.big->spill_imp = ld_dev(&C->spill_n);  // (imports past their slab)
       __syncthreads();
     }
@@ -4675,7 +4701,10 @@ int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot) {
   DevSim& S = ctx->S;
   const XLay l = xlay(ctx->nranks, xislot);
   void* p = nullptr;
-  hipError_t e = hipExtMallocWithFlags(&p, l.bytes, hipDeviceMallocUncached);
+  // (a local group's shards share this GPU: ordinary device memory, device-scope accesses;
+  // one shard per GPU: uncached, the peers write it over xGMI)
+  S.xsys = ctx->comm_local ? 0u : 1u;
+  hipError_t e = S.xsys ? hipExtMallocWithFlags(&p, l.bytes, hipDeviceMallocUncached) : hipMalloc(&p, l.bytes);
   if (e != hipSuccess) return set_error(ctx, SGN_ENOMEM, std::string("inbox allocation: ") + hipGetErrorString(e));
   if ((e = hipMemset(p, 0, l.bytes)) != hipSuccess) {
     (void)hipFree(p);
@@ -5260,7 +5289,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // atomic min and max per workgroup and round on shared words: it slows the rounds it times)
   if (const char* e = getenv("SGN_STAMPS")) {
     S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
-    if (atoi(e) >= 2) S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 3 * 128);
+    if (atoi(e) >= 2) S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 8 * 128);
   }
   if (ctx->trace_cap) {
     S.trace = (decltype(S.trace))dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
@@ -5813,6 +5842,17 @@ int sgn_debug_rounds(sgn_ctx* ctx, uint64_t* out) {
   SGN_HIP(ctx, hipMemcpy(out, (const void*)ctx->S.rdbg, 3 * 128 * 8, hipMemcpyDeviceToHost));
   std::vector<uint64_t> init(3 * 128, 0);
   for (int r = 0; r < 128; r++) init[3 * r] = ~0ULL;
+  SGN_HIP(ctx, hipMemcpy((void*)ctx->S.rdbg, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// The same for k_rounds_x: per round 8 words (see the kernel's stamps), 128 rounds; resets.
+int sgn_debug_rounds_x(sgn_ctx* ctx, uint64_t* out) {
+  if (!ctx || !ctx->sim_ready || !ctx->S.rdbg) return SGN_EINVAL;
+  SGN_HIP(ctx, hipDeviceSynchronize());
+  SGN_HIP(ctx, hipMemcpy(out, (const void*)ctx->S.rdbg, 8 * 128 * 8, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> init(8 * 128, 0);
+  for (int r = 0; r < 128; r++) init[8 * r] = ~0ULL;
   SGN_HIP(ctx, hipMemcpy((void*)ctx->S.rdbg, init.data(), init.size() * 8, hipMemcpyHostToDevice));
   return 0;
 }

@@ -419,7 +419,8 @@ struct DevSim {
   SGN_GLB uint64_t* xin_cen;
   SGN_GLB uint32_t* rb2_cnt;  // [3][RB_CB_MAX]
   uint32_t xislot;            // inbox runs per sender and round parity
-  uint32_t pad_x;
+  uint32_t xsys;              // 1: the inboxes are other GPUs' (uncached, system-scope accesses);
+                              // 0: one GPU's (a local group: device-scope accesses, L2-served)
 };
 
 // Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and

@@ -86,8 +86,11 @@ def test_xpersist_shards_match_single(k, kind, dynamic):
     one = unsharded(args)
     shards, _, done = local_group(args, k)
     info = shards[0].engine_info()
-    assert info["exchange_mode"] == 2 and info["persistent_x_launches"] > 0, info
-    assert shards[0].kernel_times()["k_rounds_x"][0] > 0
+    if info["calendar_buckets"] <= 256:  # (longer calendars run per-round launches, as on one shard)
+        assert info["exchange_mode"] == 2 and info["persistent_x_launches"] > 0, info
+        assert shards[0].kernel_times()["k_rounds_x"][0] > 0
+    else:
+        assert info["exchange_mode"] == 1 and one.engine_info()["persistent_grid"] == 0
     s1 = compare(one, shards, n)
     assert s1["packets_sent"] > 1000 and done == s1["rounds"]
 
@@ -125,26 +128,30 @@ def test_xpersist_inbox_overflow_and_growth(monkeypatch, islot):
     shards, _, _ = local_group(args, 4)
     info = [c.engine_info() for c in shards]
     assert all(i["exchange_mode"] == 2 for i in info)
-    assert info[0]["inbox_grows"] > 0 and info[0]["inbox_slot_runs"] > islot, info[0]
+    if islot <= 6:
+        assert info[0]["inbox_grows"] > 0 and info[0]["inbox_slot_runs"] > islot, info[0]
     if islot == 1:
         assert info[0]["inbox_overflow_rounds"] > 0 and sum(i["inbox_moved_runs"] for i in info) > 0, info
     compare(one, shards, n)
 
 
 def test_xpersist_hot_fan_in(monkeypatch):
-    """Thousands of clients on other shards requesting from a few servers within one bucket
-    width: imported runs past their slab's capacity go to the spill area (the next round's gathers
-    read them there; the spill flag holds the round after for the re-layout), slabs take
-    extensions and the big-slab path orders them (bench workload H)."""
-    sys.path.insert(0, str(ROOT))
-    import bench
-    monkeypatch.setenv("SGN_SLAB_LIM", "64")
-    args = bench.build_workload_h(6000, 100)
-    one = unsharded(args, rounds=300)
-    shards, _, done = local_group(args, 4, rounds=300)
-    assert done == 300
-    compare(one, shards, 6000)
-    assert sum(c.engine_info()["slab_extensions"] for c in shards) + one.engine_info()["slab_extensions"] > 0
+    """Clients on every shard fetching from a few servers on shard 0 within one bucket width
+    (16-run slabs that may grow to 32: test hooks): imported runs past their slab's capacity go to
+    the spill area, the next round's gathers read them there and order the hot slabs in pieces
+    (the big-slab path), and the spill flag holds the round after for the re-layout, which gives
+    the hot slabs extensions."""
+    from test_gpu_pools import _hot_args
+    monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    monkeypatch.setenv("SGN_SLAB_LIM", "32")
+    n = 1600
+    args = _hot_args(n)
+    one = unsharded(args)
+    shards, _, done = local_group(args, 4)
+    assert shards[0].engine_info()["exchange_mode"] == 2
+    assert shards[0].engine_info()["big_slab_pieces"] > 0
+    assert sum(c.engine_info()["calendar_spill_runs"] for c in shards) > 0
+    compare(one, shards, n)
 
 
 def test_config_c_eight_shards_one_launch(oracle):
