@@ -3345,6 +3345,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 // re-layout, are held on every shard alike (the same messages, the same decisions) and the host
 // completes them between launches.
 constexpr uint32_t XR_MAX = 8;  // shards of a persistent multi-shard run (one MI355X node)
+// imports of a round up to this many runs are filed by their own workgroups at the next round's
+// start (each workgroup scans them all: ~64 KB), more are shared out before a second barrier
+// (DevSim::xown; SGN_XOWN: a test hook, 0 = always shared)
+constexpr uint32_t kOwnFile = 2048;
 constexpr uint64_t kXWaitTicks = 2000000000ull;  // 20 s on the 100 MHz clock: a peer that never
                                                  // answers is an error (OVF_TIMEOUT), not a hang
 
@@ -3457,8 +3461,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
   struct RoundLDS {
     uint64_t ws, we, pend_ws, pend_we, pend_nb1, pg_avail;
     uint64_t pg_alloc, occ, hold_need;
+    uint64_t fhz;                // imports: the horizon of the round they were sent in
     uint32_t active, ks, pend, pend_new, ngap, hold;
     uint32_t n_in, nin[XR_MAX];  // runs to file this round: in all, and from each shard
+    uint32_t fpend, fbuf;        // imports left for the next round's start (and their slot parity)
   };
   __shared__ RoundLDS rs;
   if (threadIdx.x == 0) {
@@ -3473,8 +3479,47 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     rs.occ = ld_dev(&C->cal_occ);
     rs.hold = ld_dev(&C->hold);
     rs.hold_need = ld_dev(&C->hold_need);
+    rs.fpend = 0;
+    rs.n_in = 0;
+    // (every spill-area entry so far may hold an import a gather must read: the re-layout at a
+    // held edge empties the area)
+    X.big->spill_imp = ld_dev(&C->spill_n);
   }
   const uint64_t rounds0 = ld_dev(&C->rounds);
+  // The runs other shards sent this shard (inbox slot parity fbuf, rs.nin per sender) into the
+  // calendar with the bucket -> slab table as it is now; their bucket minima except for the
+  // buckets of the window [nws, nwe) they will be gathered in (its first bucket's minimum is not
+  // read while it is the window's, and its last bucket's later runs join the kept minimum).
+  // own: this workgroup's groups only (every workgroup scans every run: no barrier needed
+  // before its own gathers); else a share of all of them (then a barrier).
+  auto file_in = [&](uint32_t fbuf, uint64_t fhz, uint64_t nws, uint64_t nwe, bool own) {
+    uint32_t ln = threadIdx.x;
+    asm volatile("" : "+v"(ln));
+    const uint32_t sb0 = bucket_of(S, nws), sbn = ((bucket_of(S, nwe - 1) - sb0) & (S.NB - 1)) + 1;
+    const uint32_t n = rs.n_in;
+    for (uint32_t i = (own ? 0u : w * 64) + ln; i < n; i += own ? 64u : P * 64) {
+      uint32_t q = 0, off = i;
+      while (off >= rs.nin[q]) off -= rs.nin[q++];
+      SGN_GLB const EvRec* src = S.xin_runs + ((size_t)fbuf * R + q) * S.xislot + off;
+      const EvRec ev = S.xsys ? ld_sys_rec(src) : ld_dev_rec(src);
+      const uint32_t g = (ev.dst - S.lo) >> S.gsh;
+      if (own && (g < gq0 || g >= gq1 || (g - gq0) % gqs != 0)) continue;
+      if (ev.time >= fhz) {
+        if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = ev.dst;
+        continue;
+      }
+      const uint32_t b = bucket_of(S, ev.time);
+      const size_t idx = (size_t)X.lbs[b] * S.G + g;
+      const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+      if (((b - sb0) & (S.NB - 1)) >= sbn) min_nr(&S.bucket_min[b], ev.time);
+      if (pos < S.CAP)
+        st_dev_rec(S.pool + idx * S.CAP + pos, ev);
+      else  // the extension, or the spill area: the gathers read it there, and the spill flag
+            // holds the round after on every shard for the re-layout
+        place_overflow(S, nullptr, (uint32_t)idx, pos, ev);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
   for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
   init_bmin<kApp>(S, X);
   __syncthreads();
@@ -3530,6 +3575,17 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       }
     };
     stamp(0, false);
+    // the previous round's imports for this workgroup's groups (few of them: every workgroup
+    // scans them all instead of a second barrier), before its gathers read the slabs
+    if (uni32(rs.fpend)) {
+      file_in(rs.fbuf, rs.fhz, ws, we, true);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        X.big->spill_imp = ld_dev(&C->spill_n);
+        rs.fpend = 0;
+      }
+      __syncthreads();
+    }
     // ---- 1. execute this workgroup's groups ----
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
@@ -3559,16 +3615,23 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     if (w == wbk) stamp(2, true);
     const uint64_t tag = rounds0 + r + 1;  // the global round number + 1 (the same on every shard)
     const uint32_t buf = (uint32_t)(tag & 1);
-    const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
     // (the lane index laundered every round: the compiler would otherwise hoist this section's
     // lane-dependent values out of the round loop and keep them in registers through the
     // execute phase, where the round kernels have none to spare)
     uint32_t lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
+    // the message's own inputs are loaded beside the round edge's (no dependent round trips)
+    SGN_GLB uint64_t* hmsg = nullptr;
+    uint64_t cnt = 0, spilled = 0, mu = 0;
+    if (w == wbk) {
+      if (lane < R) hmsg = S.xp[lane].hdr[buf];
+      if (lane < R && lane != me) cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
+      spilled = ld_dev(&C->spill_n);
+      mu = ld_dev(&C->min_used);
+    }
+    const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
     // ---- 3. this shard's message to every shard ----
     if (w == wbk) {
-      uint64_t cnt = 0;
-      if (lane < R && lane != me) cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
       uint64_t xmax = cnt, xsum = cnt;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
@@ -3576,11 +3639,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         xmax = o > xmax ? o : xmax;
         xsum += shfl_xor64(xsum, off);
       }
-      const uint64_t spilled = ld_dev(&C->spill_n) != 0 ? 1u : 0u;
-      const uint64_t mu = ld_dev(&C->min_used);
       if (lane < R) {
-        SGN_GLB uint64_t* h = S.xp[lane].hdr[buf];
-        const uint64_t v[XH_CAPB + 1] = {tag, cnt, e.min_next, mu, xmax, spilled,
+        SGN_GLB uint64_t* h = hmsg;
+        const uint64_t v[XH_CAPB + 1] = {tag, cnt, e.min_next, mu, xmax, spilled ? 1ull : 0ull,
                                          pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
                                          rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total};
         if (S.xsys) {
@@ -3719,41 +3780,34 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       }
     }
     __syncthreads();
-    // ---- 5. the runs other shards sent this shard into its calendar, then a local barrier ----
+    // ---- 5. the runs other shards sent this shard: a few are filed by their own workgroups at
+    // the next round's start; many are shared out now and a second local barrier follows ----
     if (uni32(rs.n_in)) {
       const uint64_t hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
-      for (uint32_t i = w * 64 + lane; i < rs.n_in; i += P * 64) {
-        uint32_t q = 0, off = i;
-        while (off >= rs.nin[q]) off -= rs.nin[q++];
-        SGN_GLB const EvRec* src = S.xin_runs + ((size_t)buf * R + q) * S.xislot + off;
-        const EvRec ev = S.xsys ? ld_sys_rec(src) : ld_dev_rec(src);
-        if (ev.time >= hz) {
-          if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = ev.dst;
-          continue;
+      if (uni32(rs.n_in) <= S.xown) {
+        if (threadIdx.x == 0) {
+          rs.fpend = 1;
+          rs.fbuf = buf;
+          rs.fhz = hz;
         }
-        const uint32_t b = bucket_of(S, ev.time);
-        const size_t idx = (size_t)X.lbs[b] * S.G + ((ev.dst - S.lo) >> S.gsh);
-        const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
-        // (bucket b1's minimum is not needed: a run there makes the next window start in b1,
-        // whose minimum no round edge reads while it is the window's first bucket)
-        if (b != b1) min_nr(&S.bucket_min[b], ev.time);
-        if (pos < S.CAP)
-          st_dev_rec(S.pool + idx * S.CAP + pos, ev);
-        else  // the extension, or the spill area: the next round's gathers read it there, and the
-              // spill flag holds the round after that on every shard for the re-layout
-          place_overflow(S, nullptr, (uint32_t)idx, pos, ev);
+        __syncthreads();
+      } else {
+        file_in(buf, hz, uni64(rs.ws), uni64(rs.we), false);
+        stamp(5, true);
+        rb2_arrive<kApp>(S, p, w, P);
+        if (!rb_wait<kApp>(&S.rb2_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
+          if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+          return;
+        }
+        stamp(6, true);
+        if (threadIdx.x == 0) X.big->spill_imp = ld_dev(&C->spill_n);  // (imports past their slab)
+        __syncthreads();
       }
-      stamp(5, true);
-      rb2_arrive<kApp>(S, p, w, P);
-      if (!rb_wait<kApp>(&S.rb2_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
-        if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
-        return;
-      }
-      stamp(6, true);
-      if (threadIdx.x == 0) X.big->spill_imp = ld_dev(&C->spill_n);  // (imports past their slab)
-      __syncthreads();
     }
   }
+  // imports left for a next round this launch does not run: shared out now (the launch's end is
+  // the barrier)
+  if (uni32(rs.fpend)) file_in(rs.fbuf, rs.fhz, uni64(rs.ws), uni64(rs.we), false);
   // the launch's per-wave statistics (k_rounds)
   __syncthreads();
   if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x] && gq0 < gq1) {
@@ -5335,6 +5389,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     ctx->d_xl = dalloc<XLaunch>(ctx, 1);
     if (!S.rb2_cnt || !ctx->d_xp || !ctx->d_xl) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
     S.xp = (decltype(S.xp))ctx->d_xp;
+    S.xown = kOwnFile;
+    if (const char* e = getenv("SGN_XOWN")) S.xown = (uint32_t)atoi(e);
     uint64_t xis = ctx->xslot;
     if (const char* e = getenv("SGN_XISLOT")) xis = std::max<uint64_t>(1, std::min<uint64_t>(xis, (uint64_t)atoll(e)));
     ctx->S = S;  // (xinbox_alloc / xpeer_upload work on ctx->S)

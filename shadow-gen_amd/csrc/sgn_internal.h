@@ -421,6 +421,9 @@ struct DevSim {
   uint32_t xislot;            // inbox runs per sender and round parity
   uint32_t xsys;              // 1: the inboxes are other GPUs' (uncached, system-scope accesses);
                               // 0: one GPU's (a local group: device-scope accesses, L2-served)
+  uint32_t xown;              // a round's imports up to this many runs: filed by their own
+                              // workgroups at the next round's start (else shared + a barrier)
+  uint32_t pad_x;
 };
 
 // Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and

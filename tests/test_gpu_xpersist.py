@@ -95,6 +95,21 @@ def test_xpersist_shards_match_single(k, kind, dynamic):
     assert s1["packets_sent"] > 1000 and done == s1["rounds"]
 
 
+@pytest.mark.parametrize("xown", ["0", "1", "16"])
+def test_xpersist_import_modes(monkeypatch, xown):
+    """A round's imports are filed by the receiving shard's workgroups either for their own
+    groups at the next round's start (few: no second barrier) or shared out before a second local
+    barrier (many); SGN_XOWN moves the threshold (0: always shared) — identical either way."""
+    monkeypatch.setenv("SGN_XOWN", xown)
+    n = 500
+    bw = np.where(np.arange(n) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+    args = scenario(n=n, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=400_000_000, bw=bw, tor=True, tgen_think=50_000_000)
+    one = unsharded(args)
+    shards, _, _ = local_group(args, 4)
+    assert shards[0].engine_info()["exchange_mode"] == 2
+    compare(one, shards, n)
+
+
 def test_xpersist_matches_per_round_group(monkeypatch):
     """The same group through the per-round launches and local copies (SGN_LOCAL_PERSIST=0) and
     through k_rounds_x: identical."""
