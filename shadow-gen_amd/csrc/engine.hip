@@ -3375,6 +3375,39 @@ __device__ __forceinline__ void rb2_arrive(const DevSim& S, uint32_t p, uint32_t
   if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the local arrival of k_rounds_x (k_rounds' chunk counters): *last = 1 for the workgroup whose
+// count completes the shard's barrier (it computes the round edge and sends the messages)
+template <uint32_t kApp>
+__device__ __forceinline__ void rb_arrive_x(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
+                                            uint64_t m, uint64_t occd, uint32_t* last) {
+  if (threadIdx.x != 0) return;
+  const uint32_t ch = w >> 6;
+  const uint32_t csz = min(64u, nw - (ch << 6));
+  const uint32_t nch = (nw + 63) >> 6;
+  using Y = RbLayout<kApp>;
+  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
+  if (kmin != INVALID) min_nr(mn, kmin);
+  if (m != INVALID) min_nr(mn + 1, m);
+  if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
+  SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * Y::CB;
+  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t l = 0;
+  if (c == csz - 1)
+    l = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1 ? 1u : 0u;
+  *last = l;
+}
+
+// a 16-byte message granule {value, tag}: one load (device scope: sc1; system: sc0 sc1)
+__device__ __forceinline__ u64x2 ld_gran16(SGN_GLB const uint64_t* p, bool sys) {
+  u64x2 v;
+  if (sys)
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"((uint64_t)p) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"((uint64_t)p) : "memory");
+  return v;
+}
+
 template <uint32_t kApp>
 __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ L, uint32_t max_rounds) {
   // this workgroup's shard and its place in the shard's range
@@ -3465,6 +3498,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     uint32_t active, ks, pend, pend_new, ngap, hold;
     uint32_t n_in, nin[XR_MAX];  // runs to file this round: in all, and from each shard
     uint32_t fpend, fbuf;        // imports left for the next round's start (and their slot parity)
+    uint32_t last;               // this workgroup arrived last at the shard's local barrier
   };
   __shared__ RoundLDS rs;
   if (threadIdx.x == 0) {
@@ -3481,6 +3515,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     rs.hold_need = ld_dev(&C->hold_need);
     rs.fpend = 0;
     rs.n_in = 0;
+    rs.last = 0;
     // (every spill-area entry so far may hold an import a gather must read: the re-layout at a
     // held edge empties the area)
     X.big->spill_imp = ld_dev(&C->spill_n);
@@ -3586,7 +3621,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       }
       __syncthreads();
     }
-    // ---- 1. execute this workgroup's groups ----
+    // ---- 1. execute this workgroup's groups, then arrive (the last arrival learns it is) ----
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
     for (uint32_t g = gq0; g < gq1; g += gqs) {
@@ -3599,20 +3634,14 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         if (lastg) {
           flush_bmin<kApp>(S, X);
           stamp(1, true);
-          rb_arrive<kApp>(S, p, w, P, kall, mall, oall);
+          rb_arrive_x<kApp>(S, p, w, P, kall, mall, oall, &rs.last);
           arrived = true;
         }
       });
       __syncthreads();
     }
-    if (!arrived) rb_arrive<kApp>(S, p, w, P, INVALID, INVALID, 0);
-    // ---- 2. the local barrier and this shard's round edge ----
-    if (!rb_wait<kApp>(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
-      if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
-      return;
-    }
-    asm volatile("" ::: "memory");
-    if (w == wbk) stamp(2, true);
+    if (!arrived) rb_arrive_x<kApp>(S, p, w, P, INVALID, INVALID, 0, &rs.last);
+    __syncthreads();
     const uint64_t tag = rounds0 + r + 1;  // the global round number + 1 (the same on every shard)
     const uint32_t buf = (uint32_t)(tag & 1);
     // (the lane index laundered every round: the compiler would otherwise hoist this section's
@@ -3620,18 +3649,17 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     // execute phase, where the round kernels have none to spare)
     uint32_t lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
-    // the message's own inputs are loaded beside the round edge's (no dependent round trips)
-    SGN_GLB uint64_t* hmsg = nullptr;
-    uint64_t cnt = 0, spilled = 0, mu = 0;
-    if (w == wbk) {
-      if (lane < R) hmsg = S.xp[lane].hdr[buf];
+    // ---- 2. the shard's last arrival: its round edge, and its message to every shard ----
+    if (uni32(rs.last)) {
+      stamp(2, true);
+      // the message's own inputs beside the round edge's loads (no dependent round trips)
+      SGN_GLB uint64_t* hm = nullptr;
+      uint64_t cnt = 0;
+      if (lane < R) hm = S.xp[lane].hdr[buf];
       if (lane < R && lane != me) cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
-      spilled = ld_dev(&C->spill_n);
-      mu = ld_dev(&C->min_used);
-    }
-    const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
-    // ---- 3. this shard's message to every shard ----
-    if (w == wbk) {
+      const uint64_t spilled = ld_dev(&C->spill_n);
+      const uint64_t mu = ld_dev(&C->min_used);
+      const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
       uint64_t xmax = cnt, xsum = cnt;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
@@ -3640,65 +3668,63 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         xsum += shfl_xor64(xsum, off);
       }
       if (lane < R) {
-        SGN_GLB uint64_t* h = hmsg;
-        const uint64_t v[XH_CAPB + 1] = {tag, cnt, e.min_next, mu, xmax, spilled ? 1ull : 0ull,
-                                         pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
-                                         rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total};
+        const uint64_t v[XH_N] = {cnt, e.min_next, mu, xmax, spilled ? 1ull : 0ull,
+                                  pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
+                                  rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total, S.nH,
+                                  e.nb1, e.occd, e.nalloc, e.nfree};
         if (S.xsys) {
 #pragma unroll
-          for (uint32_t k = 1; k <= XH_CAPB; k++) st_sys(h + k, v[k]);
+          for (uint32_t k = 0; k < XH_N; k++) st_sys16(hm + 2 * k, v[k], tag);
         } else {
 #pragma unroll
-          for (uint32_t k = 1; k <= XH_CAPB; k++) st_dev(h + k, v[k]);
+          for (uint32_t k = 0; k < XH_N; k++) st_wt16(hm + 2 * k, v[k], tag);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the message is in the receiver's memory
-        if (S.xsys)
-          st_sys(h + XH_TAG, tag);
-        else
-          st_dev(h + XH_TAG, tag);
       }
       stamp(3, true);
     }
-    // ---- 4. every shard's message, then the next window (the same on every shard) ----
-    uint64_t mv[XH_CAPB + 1];
+    // ---- 3. every shard's message (granule q + 8 j: words 2 j, 2 j + 1 of sender q) ----
+    uint64_t ga = 0, gb = 0;
     {
+      const uint32_t q = lane & 7, jj = lane >> 3;
+      const bool mine = q < R && 2 * jj < XH_N;
+      SGN_GLB const uint64_t* h = S.xin_hdr + ((size_t)buf * R + q) * XH_WORDS + 4 * jj;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
-      if (lane < R) {
-        SGN_GLB uint64_t* h = S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        const bool sys = S.xsys != 0;
-        while ((sys ? ld_sys(h + XH_TAG) : ld_dev(h + XH_TAG)) != tag) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
-            ok = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+      while (true) {
+        bool good = true;
+        if (mine) {
+          const u64x2 x = ld_gran16(h, S.xsys != 0), y = ld_gran16(h + 2, S.xsys != 0);
+          ga = x.x;
+          gb = y.x;
+          good = x.y == tag && (2 * jj + 1 >= XH_N || y.y == tag);
         }
-#pragma unroll
-        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = ok ? (sys ? ld_sys(h + k) : ld_dev(h + k)) : 0;
-      } else {
-#pragma unroll
-        for (uint32_t k = 1; k <= XH_CAPB; k++) mv[k] = 0;
+        if (__ballot(!good) == 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (__ballot(!ok)) {
+      if (!ok) {
         if (lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
         return;
       }
       stamp(4, true);
     }
-    const bool sender = lane < R;
-    uint64_t gm = sender ? mv[XH_MIN] : INVALID, gmu = sender ? mv[XH_MU] : INVALID;
-    uint64_t xs = sender ? mv[XH_XSUM] : 0, xmax = sender ? mv[XH_XMAX] : 0;
-    uint32_t spill_any = sender && mv[XH_SPILL] ? 1u : 0u;
-    // runs this shard files from each sender (the slot holds at most xslot; the rest wait in the
-    // sender's spill area and the round edge holds for the host to move them)
-    const uint32_t nin_l = sender && lane != me ? (uint32_t)min(mv[XH_CNT], (uint64_t)S.xislot) : 0u;
-    gm = wave_min_u64(gm);
-    gmu = wave_min_u64(gmu);
-    xmax = wave_max_u64(xmax);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) xs += shfl_xor64(xs, off);
-    spill_any = __ballot(spill_any) ? 1u : 0u;
+    // word k of sender q
+    auto xw = [&](uint32_t k, uint32_t q) { return shfl64((k & 1) ? gb : ga, (int)(q + 8 * (k >> 1))); };
+    uint64_t gm = INVALID, gmu = INVALID, xs = 0, xmax = 0;
+    uint32_t spill_any = 0, nin_l = 0;
+    for (uint32_t q = 0; q < R; q++) {
+      const uint64_t a0 = xw(XH_MIN, q), a1 = xw(XH_MU, q), a2 = xw(XH_XSUM, q), a3 = xw(XH_XMAX, q);
+      const uint64_t a4 = xw(XH_SPILL, q), a5 = xw(XH_CNT, q);
+      gm = a0 < gm ? a0 : gm;
+      gmu = a1 < gmu ? a1 : gmu;
+      xs += a2;
+      xmax = a3 > xmax ? a3 : xmax;
+      spill_any |= a4 ? 1u : 0u;
+      if (lane == q && q != me) nin_l = (uint32_t)min(a5, (uint64_t)S.xislot);
+    }
     // Runahead::get (runahead.rs:44-57) over the global min used latency; the controller
     // (controller.rs:88-112) over the global min next event
     const uint64_t min_next = gm;  // (each message's minimum is already unwrapped: EMU_MAX = none)
@@ -3715,19 +3741,19 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     uint64_t own_need = 0;
     if (active) {
       const uint32_t nbk = ((bucket_of(S, ne - 1) - bucket_of(S, min_next)) & (S.NB - 1)) + 1;
-      uint32_t hq = 0;
-      if (sender) {
-        const uint64_t occ = mv[XH_OCC] + xs, capb = (uint64_t)nbk * mv[XH_CAPB] + xs;
-        const uint64_t need = codel_pages_bound(occ < capb ? occ : capb, S.rank_lo[lane + 1] - S.rank_lo[lane]);
-        if (mv[XH_PFREE] < need) hq |= HOLD_CODEL;
-        if (lane == me) own_need = need;
+      for (uint32_t q = 0; q < R; q++) {
+        const uint64_t occ = xw(XH_OCC, q) + xs, capb = (uint64_t)nbk * xw(XH_CAPB, q) + xs;
+        const uint64_t need = codel_pages_bound(occ < capb ? occ : capb, xw(XH_NH, q));
+        if (xw(XH_PFREE, q) < need) hflags |= HOLD_CODEL;
+        if (q == me) own_need = need;
       }
-      hflags = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u64(hq));  // (one flag)
-      own_need = shfl64(own_need, (int)me);
       if (spill_any) hflags |= HOLD_SPILL;
       if (xmax > S.xislot) hflags |= HOLD_XSLOT;
       else if (2 * xmax > S.xislot) hflags |= HOLD_XGROW;
     }
+    // this shard's own round edge, from its message to itself
+    const uint64_t e_nb1 = xw(XH_NB1, me), e_occd = xw(XH_OCCD, me), e_nalloc = xw(XH_NALLOC, me),
+                   e_nfree = xw(XH_NFREE, me);
     uint32_t n_in = nin_l;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off, 64);
@@ -3737,7 +3763,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     const uint64_t bstart = SIM_START + S.bw_div.div(ws - SIM_START) * S.BW;
     const bool gap = active && (ne + S.max_lat >= bstart + span || ne + S.max_lat < ne);
     if (gap) {
-      if (w == wbk) rb_bookkeep(S, ws, we, e.nb1, ks);
+      if (w == wbk) rb_bookkeep(S, ws, we, e_nb1, ks);
       if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         SGN_GLB uint32_t* gc = S.rb_cnt + 3 * RB_CB_MAX;
@@ -3759,18 +3785,19 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       rs.pend = gap ? 0u : 1u;
       rs.pend_ws = ws;
       rs.pend_we = we;
-      rs.pend_nb1 = e.nb1;
+      rs.pend_nb1 = e_nb1;
       rs.pend_new = ks;
       rs.ks = slab_b1;
       rs.ws = min_next;
       rs.we = ne;
       rs.active = active;
-      rs.pg_avail += e.nfree;
-      rs.pg_alloc += e.nalloc;
-      rs.occ += e.occd + n_in;
+      rs.pg_avail += e_nfree;
+      rs.pg_alloc += e_nalloc;
+      rs.occ += e_occd + n_in;
       rs.n_in = n_in;
       rs.hold = hflags;
       rs.hold_need = own_need;
+      rs.last = 0;
       if (w == wbk) {
         st_dev(&C->last_min_next, min_next);
         st_dev(&C->prev_we, we);
