@@ -3061,8 +3061,69 @@ __device__ __forceinline__ void rb_bookkeep(const DevSim& S, uint64_t ws, uint64
 // queues) belongs to this workgroup's groups.
 // kBig: compiled with the big-slab path (launched while some slab has an extension; without
 // one, the path's code cost config C 2.6 % per launch in same-box A/B, round 4)
+// The persistent kernels' per-launch state, reset by the launch itself (no host memsets before
+// a launch): round buffer 0 (chunk minima, counters of both barriers, spare-slab
+// minimum, freed / allocated / spilled counts, exports) and the idle-gap counter, by the shard's
+// bookkeeping workgroup BEFORE it counts itself into the residency census — every workgroup
+// waits for the whole census, so no arrival can reach the buffers first. Buffers 1 and 2 are
+// reset during rounds 0 and 1 as before.
+template <uint32_t kApp>
+__device__ __forceinline__ void rb_reset0(const DevSim& S, uint32_t nch) {
+  using Y = RbLayout<kApp>;
+  for (uint32_t i = threadIdx.x; i < nch; i += 64) {
+    st_dev(&S.rb_min[(size_t)i * Y::MS], (uint64_t)INVALID);
+    st_dev(&S.rb_min[(size_t)i * Y::MS + 1], (uint64_t)INVALID);
+    st_dev(&S.rb_occ[(size_t)i * Y::OS], (uint64_t)0);
+  }
+  for (uint32_t i = threadIdx.x; i <= nch; i += 64) {
+    const size_t o = (size_t)(i == nch ? RB_CH : i) * Y::CS;
+    st_dev(&S.rb_cnt[o], 0u);
+    if (S.rb2_cnt) st_dev(&S.rb2_cnt[o], 0u);
+  }
+  if (S.xout_n)
+    for (uint32_t i = threadIdx.x; i < S.n_ranks; i += 64) st_dev(&S.xout_n[i], 0u);
+  if (threadIdx.x == 0) {
+    st_dev(&S.rb_keep[0], (uint64_t)INVALID);
+    st_dev(&S.rb_free[0], (uint64_t)0);
+    st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX], (uint64_t)0);
+    st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3], (uint64_t)0);
+    st_dev(&S.rb_cnt[3 * RB_CB_MAX], 0u);  // the idle-gap barrier's counter
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Residency census (thread 0 of each workgroup): the workgroup counts itself in and waits,
+// bounded, for the whole grid of P; the first to see it, or to give up, sets the verdict with a
+// compare-and-swap, so every workgroup acts on the same one. The arrival counter is never reset
+// (the host passes its value before the launch, base) and the verdict carries the launch's epoch
+// (epoch << 2 | verdict: 1 resident, 2 not). *decided: this workgroup set it.
+__device__ __forceinline__ uint32_t census(SGN_GLB Ctrl* C, uint32_t P, uint32_t epoch, uint32_t base,
+                                           bool* decided) {
+  __hip_atomic_fetch_add(&C->res_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t want = epoch << 2;
+  uint32_t v = 0, spins = 0;
+  *decided = false;
+  while (((v = ld_dev(&C->res_verdict)) & ~3u) != want) {
+    uint32_t nv;
+    if (ld_dev(&C->res_arrive) - base >= P) {
+      nv = want | 1u;
+    } else if (++spins > (1u << 14)) {
+      nv = want | 2u;
+    } else {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    uint32_t expect = v;
+    if (__hip_atomic_compare_exchange_strong(&C->res_verdict, &expect, nv, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      *decided = true;
+  }
+  return v & 3u;
+}
+
 template <uint32_t kApp, bool kBig>
-__global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds) {
+__global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg, uint32_t max_rounds, uint32_t epoch,
+                                                  uint32_t res_base) {
   const DevSim& S = *Sg;
   SGN_GLB Ctrl* C = S.ctrl;
   SGN_EXEC_LDS(X)
@@ -3099,25 +3160,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
   // leaves untouched and the host runs the rounds with per-round launches instead.
   {
     __shared__ uint32_t verdict;
+    if (w == P - 1) rb_reset0<kApp>(S, (P + 63) >> 6);
     if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(&C->res_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t v = 0, spins = 0;
-      while ((v = ld_dev(&C->res_verdict)) == 0) {
-        if (ld_dev(&C->res_arrive) >= P) {
-          v = 1;
-        } else if (++spins > (1u << 14)) {
-          v = 2;
-        } else {
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        uint32_t expect = 0;
-        __hip_atomic_compare_exchange_strong(&C->res_verdict, &expect, v, __ATOMIC_RELAXED,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v = ld_dev(&C->res_verdict);
-        break;
-      }
-      verdict = v;
+      bool decided;
+      verdict = census(C, P, epoch, res_base, &decided);
     }
     __syncthreads();
     if (verdict != 1) return;
@@ -3444,25 +3490,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
   {
     __shared__ uint32_t verdict;
     SGN_GLB Ctrl* C0 = L->S[0]->ctrl;
+    if (w == P - 1) rb_reset0<kApp>(S, (P + 63) >> 6);
     if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(&C0->res_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t v = 0, spins = 0;
-      bool decided = false;
-      while ((v = ld_dev(&C0->res_verdict)) == 0) {
-        if (ld_dev(&C0->res_arrive) >= gridDim.x) {
-          v = 1;
-        } else if (++spins > (1u << 14)) {
-          v = 2;
-        } else {
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        uint32_t expect = 0;
-        decided = __hip_atomic_compare_exchange_strong(&C0->res_verdict, &expect, v, __ATOMIC_RELAXED,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v = ld_dev(&C0->res_verdict);
-        break;
-      }
+      bool decided;
+      uint32_t v = census(C0, gridDim.x, (uint32_t)L->epoch, L->res_base, &decided);
       if (L->peers_census) {
         const uint64_t ep = L->epoch << 2;
         if (decided)  // the deciding workgroup tells every shard (its own inbox too)
@@ -3487,7 +3518,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     }
     __syncthreads();
     if (verdict != 1) {
-      if (verdict == 3 && w == P - 1 && threadIdx.x == 0) st_dev(&C->res_verdict, 3u);
+      if (verdict == 3 && w == P - 1 && threadIdx.x == 0) st_dev(&C->res_verdict, ((uint32_t)L->epoch << 2) | 3u);
       return;
     }
   }
@@ -4223,12 +4254,20 @@ void launch_k_rounds_t(sgn_ctx* ctx, uint32_t n) {
   const dim3 grid(ctx->persist_grid), block(64);
   const size_t lds = exec_lds_bytes(ctx->S.CAP, ctx->S.agg_bmin ? ctx->S.NB : 0);
   const DevSim* d = (const DevSim*)ctx->d_S;
+  // (the census: this launch's epoch, and the arrivals of the launches before it)
+  const uint32_t ep = ++ctx->res_epoch, base = ctx->res_base;
+  ctx->res_base += ctx->persist_grid;
   if (k == SGN_TRAFFIC_TGEN)
-    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_TGEN, kBig>), grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_TGEN, kBig>), grid, block, lds, ctx->stream, d, n, ep, base);
   else if (k == SGN_TRAFFIC_EXTERNAL)
-    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_EXTERNAL, kBig>), grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_EXTERNAL, kBig>), grid, block, lds, ctx->stream, d, n, ep, base);
   else
-    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_PERIODIC, kBig>), grid, block, lds, ctx->stream, d, n);
+    hipLaunchKernelGGL((k_rounds<SGN_TRAFFIC_PERIODIC, kBig>), grid, block, lds, ctx->stream, d, n, ep, base);
+}
+// the census verdict of the last persistent launch: 1 resident, 2 not (0: none recorded)
+uint32_t census_verdict(const sgn_ctx* ctx, uint32_t epoch) {
+  const uint32_t v = ctx->h_ctrl->res_verdict;
+  return (v >> 2) == (epoch & 0x3FFFFFFFu) ? (v & 3u) : 0u;
 }
 void launch_k_rounds(sgn_ctx* ctx, uint32_t n) {
   if (rounds_big(ctx))
@@ -4891,16 +4930,11 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
     b += (uint32_t)P;
     c->x_grid = (uint32_t)P;
     const DevSim& S = c->S;
-    hipStream_t st = c0->stream;
-    SGN_HIP(c, hipMemsetAsync((void*)S.rb_min, 0xFF, (3 * RB_CH * RB_MS_MAX + 4) * 8, st));
-    SGN_HIP(c, hipMemsetAsync((void*)S.rb_cnt, 0, (3 * RB_CB_MAX + 1) * 4, st));
-    SGN_HIP(c, hipMemsetAsync((void*)S.rb2_cnt, 0, 3 * RB_CB_MAX * 4, st));
-    SGN_HIP(c, hipMemsetAsync((void*)S.rb_free, 0, 3 * 8, st));
-    SGN_HIP(c, hipMemsetAsync((void*)S.rb_occ, 0, (3 * RB_CH * RB_OS_MAX + 6) * 8, st));
-    SGN_HIP(c, hipMemsetAsync((void*)S.xout_n, 0, (3 * (size_t)c->nranks + 8) * 4, st));
-    SGN_HIP(c, hipMemsetAsync((char*)S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, st));
+    (void)S;  // (no per-launch memsets: each shard's launch resets its round buffers itself)
   }
   xl.base[sh.size()] = b;
+  xl.res_base = c0->res_base;  // (the census counts in the first shard's control block)
+  c0->res_base += b;
   SGN_HIP(c0, hipMemcpyAsync(c0->d_xl, &xl, sizeof(XLaunch), hipMemcpyHostToDevice, c0->stream));
   time_begin(c0, K_EXECUTE);
   const dim3 grid(b), block(64);
@@ -5027,7 +5061,7 @@ int run_xpersist(const std::vector<sgn_ctx*>& sh, bool peers, uint64_t max_round
     for (sgn_ctx* c : sh)
       if ((rc = sync_ctrl(c))) break;
     if (rc) break;
-    if (lr == 1 || c0->h_ctrl->res_verdict != 1) {
+    if (lr == 1 || census_verdict(c0, (uint32_t)c0->x_epoch) != 1) {
       // not resident (here or on a peer): nothing ran; per-round launches from now on
       for (sgn_ctx* c : sh) {
         c->x_off = true;
@@ -5102,6 +5136,7 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   const uint32_t nH = ctx->hi - ctx->lo;
   const uint32_t N = ctx->n_all;
   ctx->persist_off = false;
+  ctx->res_epoch = ctx->res_base = 0;  // (the new control block's census words are zero)
   ctx->codel_grows = ctx->cal_grows = ctx->cal_spill_runs = ctx->xslot_grows = ctx->rounds_held = 0;
   ctx->codel_allocs_before = 0;
   ctx->ext_slabs = ctx->spill_grows = 0;
@@ -5558,18 +5593,14 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
     // a launch ends early at a held round edge (a pool grows here, then the rounds go on)
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(kPersistRounds, max_rounds - enq);
-      SGN_HIP(ctx, hipMemsetAsync((char*)ctx->S.ctrl + offsetof(Ctrl, res_arrive), 0, 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_min, 0xFF, (3 * RB_CH * RB_MS_MAX + 4) * 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_cnt, 0, (3 * RB_CB_MAX + 1) * 4, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_free, 0, 3 * 8, ctx->stream));
-      SGN_HIP(ctx, hipMemsetAsync((void*)ctx->S.rb_occ, 0, (3 * RB_CH * RB_OS_MAX + 6) * 8, ctx->stream));
+      // (no per-launch memsets: the launch resets its round buffers before its census)
       time_begin(ctx, K_EXECUTE);
       launch_k_rounds(ctx, n);
       time_end(ctx);
       ctx->kt[K_EXECUTE].total++;
       SGN_HIP(ctx, hipGetLastError());
       if ((rc = sync_ctrl(ctx))) return rc;
-      if (ctx->h_ctrl->res_verdict != 1) {
+      if (census_verdict(ctx, ctx->res_epoch) != 1) {
         // the grid was not resident (the occupancy model was wrong, or another context holds
         // part of the GPU): nothing ran; continue with one launch per round
         ctx->persist_grid = 0;

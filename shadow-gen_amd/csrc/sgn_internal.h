@@ -468,6 +468,7 @@ struct XLaunch {
   uint32_t n_local;              // shards in this launch
   uint32_t peers_census;         // 1: one shard per GPU: the census is exchanged with the peers
   uint64_t epoch;                // launch number (census tags)
+  uint32_t res_base, pad_l;      // the first shard's census arrival count before this launch
   uint32_t base[XL_MAX + 1];     // workgroup range of local shard i: [base[i], base[i + 1])
   const struct DevSim* S[XL_MAX];
 };
@@ -585,6 +586,7 @@ struct sgn_ctx {
   bool use_graph = true;
   uint32_t persist_grid = 0;  // persistent-rounds grid size (0: per-round launches)
   uint32_t persist_fallbacks = 0;  // persistent launches refused by the residency census
+  uint32_t res_epoch = 0, res_base = 0;  // persistent launches so far / census arrivals so far
   bool persist_off = false;        // ... since sim_init: per-round launches from then on
   uint32_t lds_per_cu = 0;         // LDS bytes per CU (device attribute; the residency model)
   // pool growth (a held round, then a larger pool): counts for sgn_engine_info
