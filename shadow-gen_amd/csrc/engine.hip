@@ -3721,7 +3721,20 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       SGN_GLB const uint64_t* h = S.xin_hdr + ((size_t)buf * R + q) * XH_WORDS + 4 * jj;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
+      // every workgroup of every shard waits here: only the first granule of each message is
+      // polled (R lanes; a poll of every granule by every workgroup swamped the L2 channel that
+      // holds them), then every granule is read once and its tag checked (re-read if late)
       while (true) {
+        bool good = true;
+        if (lane < R) good = ld_gran16(S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS, S.xsys != 0).y == tag;
+        if (__ballot(!good) == 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(kApp == SGN_TRAFFIC_TGEN ? 8 : 4);
+      }
+      while (ok) {
         bool good = true;
         if (mine) {
           const u64x2 x = ld_gran16(h, S.xsys != 0), y = ld_gran16(h + 2, S.xsys != 0);
@@ -3730,11 +3743,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
           good = x.y == tag && (2 * jj + 1 >= XH_N || y.y == tag);
         }
         if (__ballot(!good) == 0) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) ok = false;
       }
       if (!ok) {
         if (lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
