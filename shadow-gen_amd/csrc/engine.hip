@@ -432,6 +432,11 @@ struct OutboxN : OutboxHdr {
 };
 template <uint32_t kApp>
 using Outbox = OutboxN<kObox<kApp>>;
+#ifdef SGN_EXP_NOPAIR  // cost experiment (build_exp.sh): one lane per outbox record
+constexpr bool kPairOff = true;
+#else
+constexpr bool kPairOff = false;
+#endif
 
 // A run whose calendar slab is full goes to the spill area with its slab index (lossless; the
 // round edge holds and the host re-lays the calendar out before the run can be due). Only a
@@ -2700,13 +2705,39 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   // completes them before the round edge)
   {
     const uint32_t no = min(ob->n, kObox<kApp>);
-    for (uint32_t i = lane; i < no; i += 64) {
-      const uint32_t idx = ob->idx[i];
-      const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
-      if (pos < S.CAP)
-        st_dev_rec(S.pool + (size_t)idx * S.CAP + pos, ob->rec[i]);
-      else
-        place_overflow(S, ob, idx, pos, ob->rec[i]);
+    if constexpr (kApp == SGN_TRAFFIC_PERIODIC && !kBig && !kPairOff) {  // (not with the big-slab path: registers)
+      // two lanes per record, each storing one 16-byte half: the record is one 32-byte write
+      // (a lane's two 16-byte write-through stores of one record are two; config D writes a
+      // record per host-round, MI355X_MICROARCH.md: write-through stores and their granules)
+      for (uint32_t i0 = 0; i0 < no; i0 += 32) {
+        const uint32_t i = i0 + (lane >> 1), half = lane & 1;
+        const bool has = i < no;
+        uint32_t idx = 0, pos = 0;
+        if (has) idx = ob->idx[i];
+        if (has && !half) pos = atomicAdd(&S.slab_n[idx], 1u);
+        pos = __shfl(pos, (int)(lane & ~1u), 64);
+        if (has) {
+          const EvRec& r = ob->rec[i];
+          if (pos < S.CAP) {
+            SGN_GLB char* q = (SGN_GLB char*)(S.pool + (size_t)idx * S.CAP + pos) + 16 * half;
+            if (half)
+              st_wt16(q, (uint64_t)r.src | ((uint64_t)r.dst << 32), (uint64_t)r.pc | ((uint64_t)r.tag << 32));
+            else
+              st_wt16(q, r.time, r.eid);
+          } else if (!half) {
+            place_overflow(S, ob, idx, pos, r);
+          }
+        }
+      }
+    } else {
+      for (uint32_t i = lane; i < no; i += 64) {
+        const uint32_t idx = ob->idx[i];
+        const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+        if (pos < S.CAP)
+          st_dev_rec(S.pool + (size_t)idx * S.CAP + pos, ob->rec[i]);
+        else
+          place_overflow(S, ob, idx, pos, ob->rec[i]);
+      }
     }
   }
   uint64_t my_min = lmin;  // a host with nothing due sleeps through the window
@@ -3391,6 +3422,11 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 // re-layout, are held on every shard alike (the same messages, the same decisions) and the host
 // completes them between launches.
 constexpr uint32_t XR_MAX = 8;  // shards of a persistent multi-shard run (one MI355X node)
+#ifdef SGN_KX_NOBIG  // cost experiment only (build_exp.sh): k_rounds_x without the big-slab path
+constexpr bool kKxBig = false;
+#else
+constexpr bool kKxBig = true;
+#endif
 // imports of a round up to this many runs are filed by their own workgroups at the next round's
 // start (each workgroup scans them all: ~64 KB), more are shared out before a second barrier
 // (DevSim::xown; SGN_XOWN: a test hook, 0 = always shared)
@@ -3658,7 +3694,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     for (uint32_t g = gq0; g < gq1; g += gqs) {
       uint64_t kmin, m;
       const bool lastg = g + gqs >= gq1;
-      exec_group<false, kApp, true>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
+      exec_group<false, kApp, kKxBig>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
         oall += od;

@@ -25,6 +25,22 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 300
 g, used, hosts, cfg, tr = bench.build_workload(n, 1000)
+if k == 1:  # the single-shard persistent kernel's own timeline: {earliest start, latest arrival,
+    # round edge known by the bookkeeping workgroup} (sgn_debug_rounds, 3 words per round)
+    c = sgn.Context(flags=2)
+    c.routes_build(g, used)
+    c.hosts_set(hosts)
+    c.sim_init(cfg, tr)
+    c.run(warm)
+    b3 = np.zeros(3 * 128, dtype=np.uint64)
+    c.check(c.L.sgn_debug_rounds(c.h, sgn.ptr(b3, C.c_uint64)))
+    c.run(100)
+    c.check(c.L.sgn_debug_rounds(c.h, sgn.ptr(b3, C.c_uint64)))
+    t = b3.reshape(128, 3)[:100].astype(np.int64)
+    d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], np.append(t[1:, 0] - t[:-1, 2], 0)], axis=1) / 100.0
+    med = np.median(d[:-1], axis=0)
+    print(f"one shard: exec {med[0]:6.2f}  edge {med[1]:6.2f}  gap {med[2]:6.2f}  round {np.median(np.diff(t[:, 0])) / 100:.2f} us")
+    sys.exit(0)
 ctxs = [sgn.Context(shard_rank=r, shard_count=k, flags=2) for r in range(k)]
 arr = (C.c_void_p * k)(*[c.h.value for c in ctxs])
 for c in ctxs:
