@@ -532,8 +532,10 @@ def main():
     for _ in range(args.warmup):
         ctx.run(args.rounds_per_step)
     st0 = ctx.stats()
-    # the round kernel: k_rounds (persistent, many rounds per launch) or k_execute
-    rk = "k_rounds" if "k_rounds" in ctx.kernel_times() else "k_execute"
+    # the round kernel: k_rounds (one shard, persistent: many rounds per launch), k_rounds_x
+    # (N > 1, persistent: peer inboxes), or k_execute (per-round launches)
+    kts = ctx.kernel_times()
+    rk = next(k for k in ("k_rounds", "k_rounds_x", "k_execute") if k in kts)
     kt0 = ctx.kernel_times()[rk]
     barrier()
     t0 = time.perf_counter()
@@ -563,7 +565,8 @@ def main():
     # are timed one in eight (an event pair around every launch cost ~20 % of the rounds), so
     # their average duration comes from the sample and the launch count is the round count.
     timed = kt1[0] - kt0[0]
-    launches = timed if rk == "k_rounds" else rounds
+    persistent = rk in ("k_rounds", "k_rounds_x")
+    launches = timed if persistent else rounds
     exec_ms = kt1[1] - kt0[1]
     n_pkt = d["packets_sent"] + d["packets_loss_dropped"]
     host_exec = d["host_executions"]
@@ -604,7 +607,7 @@ def main():
         # why the kernel sits far below the HBM roof: a latency chain on a partly filled chip.
         # Workgroups are one wave; k_rounds keeps its grid resident (each workgroup serves
         # groups g, g + grid, ...), k_execute launches one workgroup per group every round.
-        grid = info["persistent_grid"] if rk == "k_rounds" else info["host_groups"]
+        grid = {"k_rounds": info["persistent_grid"], "k_rounds_x": info["persistent_x_grid"]}.get(rk, info["host_groups"])
         wave_rounds = info["host_groups"] * max(1, rounds)
         roof["occupancy"] = {
             "compute_units": info["compute_units"],

@@ -605,6 +605,9 @@ int sgn_debug_rounds(sgn_ctx* ctx, uint64_t* out);
  * rounds — earliest start, latest local arrival, local barrier seen, messages sent, latest "all
  * messages seen", latest imports filed, latest second barrier seen (100 MHz clock); resets */
 int sgn_debug_rounds_x(sgn_ctx* ctx, uint64_t* out);
+/* the same per workgroup (SGN_STAMPS=3: plain stores, no shared words): [128 rounds][2048
+ * workgroups of this shard][8] u64, the same 8 stamps (0: not written); resets */
+int sgn_debug_rounds_xw(sgn_ctx* ctx, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -423,6 +423,8 @@ struct OutboxHdr {
   SGN_GLB uint64_t* pg_allocd;// ... and allocated-page counter (the round edge's guard)
   SGN_GLB uint64_t* spilled;  // runs this round put in the calendar's spill area
   SGN_GLB uint32_t* xn;       // multi-shard: this round's per-peer run counters
+  uint32_t* xc;               // k_rounds_x: this workgroup's runs per peer this round (LDS; null:
+                              // no inbox bins, every remote run goes to its peer's slot)
   uint32_t xbuf;              // ... and the peer blocks they go to (XPeer::runs[xbuf])
 };
 template <uint32_t N>
@@ -1697,18 +1699,39 @@ struct HostExec {
       cap = S.CAP;
       sidx = (uint32_t)idx;
     } else {
-      uint32_t lo = 0, hi = S.n_ranks;
+      uint32_t lo = 0, hi = S.n_ranks, lov = 0;  // (rank_lo[0] = 0)
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (S.rank_lo[mid] <= dst) lo = mid; else hi = mid;
+        const uint32_t v = S.rank_lo[mid];
+        if (v <= dst) {
+          lo = mid;
+          lov = v;
+        } else {
+          hi = mid;
+        }
       }
       atomicMin((unsigned long long*)&ob->xmin, (unsigned long long)deliver);  // LDS
-      pos = atomicAdd(&ob->xn[lo], nrec);
       sidx = SPILL_PEER | lo;  // (runs beyond the peer's slot: the slot grows at a held round)
-      // the peer's block: the RCCL transport's send block (after its message records), or the
-      // peer's inbox slot for this shard and round parity (persistent rounds: peer-mapped memory)
-      dstp = S.xp[lo].runs[ob->xbuf];
-      cap = ob->xbuf == 2 ? S.xslot : S.xislot;
+      bool binned = false;
+      if (ob->xc) {
+        // persistent rounds: the receiving host group's bin in the peer's inbox (its gather
+        // reads it next round); a full bin sends the run to the peer's slot instead
+        atomicAdd(&ob->xc[lo], nrec);  // LDS
+        const uint32_t gr = (dsid - lov) >> S.gsh;
+        pos = atomicAdd(&S.xbin_n[((size_t)ob->xbuf * S.n_ranks + lo) * S.xgx + gr], nrec);
+        if (pos + nrec <= S.xbk) {
+          binned = true;
+          dstp = S.xp[lo].bins[ob->xbuf] + (size_t)gr * S.xbk;
+          cap = S.xbk;
+        }
+      }
+      if (!binned) {
+        pos = atomicAdd(&ob->xn[lo], nrec);
+        // the peer's block: the RCCL transport's send block (after its message records), or the
+        // peer's inbox slot for this shard and round parity (persistent rounds: peer-mapped memory)
+        dstp = S.xp[lo].runs[ob->xbuf];
+        cap = ob->xbuf == 2 ? S.xslot : S.xislot;
+      }
     }
     for (uint32_t m = 0; m < nrec; m++) {
       const uint32_t k = min(RUN_MAX, nsent - m * RUN_MAX);
@@ -2224,7 +2247,9 @@ struct ExecLDS {
 // at_end(kmin, next) runs once the group's cross-workgroup data (calendar records, slab
 // fills, minima) is issued and before the host records are written back: the round's
 // arrival goes there, so its wait covers only what other workgroups read.
-template <bool kTrace, uint32_t kApp, bool kBig, typename AtEnd>
+// kXb (k_rounds_x): the group's inbox bins (the runs other shards sent it last round) are read in
+// the round trip of its first gather and taken into the calendar (see take_bins).
+template <bool kTrace, uint32_t kApp, bool kBig, bool kXb = false, typename AtEnd>
 __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t ws, uint64_t we, uint32_t ks,
                            const ExecLDS& X, uint64_t* kmin_out, uint64_t* next_out,
                            AtEnd&& at_end) {
@@ -2540,6 +2565,58 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
                                __HIP_MEMORY_SCOPE_AGENT);  // high-water mark, this wave's slot
     }
   };
+  // ---- k_rounds_x: the runs other shards sent this group last round (its inbox bins) ----
+  // A run for a bucket of this window goes into its slab before the gathers read it (returns
+  // true: the first gather's loads are redone); a later one goes through the outbox into its
+  // bucket's slab like a send, with the bucket's minimum (its first bucket is not read while
+  // it is the window's: k_import's rule). bp, r: this lane's entry of the first pass (r loaded);
+  // a sender whose last entry of a pass was full is read on. Taken entries are zeroed (pc 0 is
+  // an empty entry) for the bin's next use two rounds later; the runs were counted in this
+  // shard's occupancy at the round edge (XH_TOT).
+  auto take_bins = [&](SGN_GLB EvRec* bp, EvRec r, uint32_t q, uint32_t e, bool on) -> bool {
+    const uint32_t E = 1u << (S.n_ranks <= 2 ? 5u : S.n_ranks <= 4 ? 4u : 3u);
+    bool slow = false;
+    bool more = on;
+    for (uint32_t e0 = 0;;) {
+      const bool ok = more && r.pc != 0;
+      if (ok) {
+        SGN_GLB uint64_t* pw = (SGN_GLB uint64_t*)(bp + e0) + 3;
+        if (S.xsys) st_sys(pw, 0ull); else st_dev(pw, (uint64_t)0);
+        if (r.time >= ob->hz) {
+          if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = r.dst;
+        } else {
+          const uint32_t b = bucket_of(S, r.time);
+          const size_t idx = (size_t)lbs[b] * S.G + g;
+          bool direct = ((b - bs) & (S.NB - 1)) < nbk;
+          slow |= direct;
+          if (!direct) {
+            min_nr(&S.bucket_min[b], r.time);
+            const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
+            if (k < kObox<kApp>) {
+              ob->rec[k] = r;
+              ob->idx[k] = (uint32_t)idx;
+            } else {
+              direct = true;
+            }
+          }
+          if (direct) {
+            const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+            if (pos < S.CAP)
+              st_dev_rec(S.pool + idx * S.CAP + pos, r);
+            else
+              place_overflow(S, ob, (uint32_t)idx, pos, r);
+          }
+        }
+      }
+      const uint64_t m = __ballot(ok && e == E - 1);
+      e0 += E;
+      if (!m || e0 >= S.xbk) break;
+      more = on && ((m >> (q * E + E - 1)) & 1ull) && e0 + e < S.xbk;
+      r = EvRec{};
+      if (more) r = S.xsys ? ld_sys_rec(bp + e0) : ld_dev_rec(bp + e0);
+    }
+    return __ballot(slow) != 0;
+  };
   for (uint32_t bi = 0; bi < nbk; bi++) {
     const uint64_t c0 = S.stamps ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t b = (bs + bi) & (S.NB - 1);
@@ -2568,12 +2645,21 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       ib1 = (size_t)(S.NB <= LDS_BSLAB ? lbs[(b + 1) & (S.NB - 1)] : ld_dev(&S.bucket_slab[(b + 1) & (S.NB - 1)])) * S.G + g;
       pb1 = S.pool + ib1 * S.CAP;
     }
+    // k_rounds_x: the first pass over the group's inbox bins, in the same round trip (lane =
+    // sender x E + entry, E entries per sender and pass)
+    const bool bins = kXb && bi == 0 && S.xin_bins != nullptr;
+    const uint32_t bsh = S.n_ranks <= 2 ? 5u : S.n_ranks <= 4 ? 4u : 3u;
+    const uint32_t bq = lane >> bsh, be_ = lane & ((1u << bsh) - 1);
+    const bool bon = bins && bq < S.n_ranks && bq != S.rank && be_ < S.xbk;
+    SGN_GLB EvRec* bp = bon ? S.xin_bins + (((size_t)(ob->xbuf ^ 1u) * S.n_ranks + bq) * S.G + g) * S.xbk + be_ : nullptr;
+    EvRec br{};
+    if (bon) br = S.xsys ? ld_sys_rec(bp) : ld_dev_rec(bp);
     if (lane < S.gspec) {
       r0 = ld_dev_rec(pb + lane);
       if (pair) r1 = ld_dev_rec(pb1 + lane);
     }
-    const uint32_t nraw_v = ld_dev(&S.slab_n[ib]);
-    const uint32_t n1raw_v = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
+    uint32_t nraw_v = ld_dev(&S.slab_n[ib]);
+    uint32_t n1raw_v = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
     // PERIODIC traffic (configs B and D: most executed hosts have their app timer due): the
     // host record of a lane whose local event is due in the window loads in the same round trip
     // as the gather, and the app's next route is prefetched behind the sort
@@ -2582,6 +2668,18 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
       ex.load();
       ex.prefetch_peer(np);
       loaded = true;
+    }
+    if (bins && take_bins(bp, br, bq, be_, bon)) {
+      // runs due in this window's buckets went into their slabs ahead of the gathers: the
+      // first bucket's (and its pair's) loads again (spill-area entries included, big path)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (kBig && lane == 0) X.big->spill_imp = ld_dev(&C->spill_n);
+      if (lane < S.gspec) {
+        r0 = ld_dev_rec(pb + lane);
+        if (pair) r1 = ld_dev_rec(pb1 + lane);
+      }
+      nraw_v = ld_dev(&S.slab_n[ib]);
+      n1raw_v = pair ? ld_dev(&S.slab_n[ib1]) : 0u;
     }
     // (scalar copies after the host record's loads are issued: a readfirstlane waits for its load)
     const uint32_t nraw = uni32(nraw_v), n1raw = uni32(n1raw_v);
@@ -2854,6 +2952,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
   X.wacc = nullptr;                                                                  \
   if (threadIdx.x == 0) {                                                            \
     ob_.bmin = X.bmin;                                                               \
+    ob_.xc = nullptr;                                                                \
     big_.spill_imp = ld_dev(&S.ctrl->spill_imp);                                     \
   }
 
@@ -3112,7 +3211,10 @@ __device__ __forceinline__ void rb_reset0(const DevSim& S, uint32_t nch) {
     if (S.rb2_cnt) st_dev(&S.rb2_cnt[o], 0u);
   }
   if (S.xout_n)
-    for (uint32_t i = threadIdx.x; i < S.n_ranks; i += 64) st_dev(&S.xout_n[i], 0u);
+    for (uint32_t i = threadIdx.x; i < S.n_ranks; i += 64) {
+      st_dev(&S.xout_n[i], 0u);
+      st_dev(&S.xout_n[3 * S.n_ranks + i], 0u);  // (k_rounds_x: the per-peer totals)
+    }
   if (threadIdx.x == 0) {
     st_dev(&S.rb_keep[0], (uint64_t)INVALID);
     st_dev(&S.rb_free[0], (uint64_t)0);
@@ -3431,6 +3533,9 @@ constexpr bool kKxBig = true;
 // start (each workgroup scans them all: ~64 KB), more are shared out before a second barrier
 // (DevSim::xown; SGN_XOWN: a test hook, 0 = always shared)
 constexpr uint32_t kOwnFile = 2048;
+// inbox bins: runs per (round parity, sender, receiving host group). Config C at 8 shards sends
+// a group ~0.6 runs per sender and round, config D ~8; a fuller bin sends the rest to the slot.
+constexpr uint32_t kXBin = 32;
 constexpr uint64_t kXWaitTicks = 2000000000ull;  // 20 s on the 100 MHz clock: a peer that never
                                                  // answers is an error (OVF_TIMEOUT), not a hang
 
@@ -3461,7 +3566,14 @@ __device__ __forceinline__ void rb2_arrive(const DevSim& S, uint32_t p, uint32_t
 // count completes the shard's barrier (it computes the round edge and sends the messages)
 template <uint32_t kApp>
 __device__ __forceinline__ void rb_arrive_x(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
-                                            uint64_t m, uint64_t occd, uint32_t* last) {
+                                            uint64_t m, uint64_t occd, uint32_t* last, const uint32_t* xc) {
+  // this workgroup's runs per peer this round (LDS, bins and slots) into the shard's totals
+  if (xc && threadIdx.x < S.n_ranks && threadIdx.x != S.rank) {
+    const uint32_t v = xc[threadIdx.x];
+    if (v)
+      (void)__hip_atomic_fetch_add(&S.xout_n[(size_t)(3 + p) * S.n_ranks + threadIdx.x], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (threadIdx.x != 0) return;
   const uint32_t ch = w >> 6;
   const uint32_t csz = min(64u, nw - (ch << 6));
@@ -3496,7 +3608,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
   const uint32_t nl = L->n_local;
   uint32_t si = 0;
   while (si + 1 < nl && blockIdx.x >= L->base[si + 1]) si++;
-  const DevSim& S = *L->S[si];
+  const DevSim& S = *(const DevSim*)L->S[si];
   SGN_GLB Ctrl* C = S.ctrl;
   const uint32_t w_i = blockIdx.x - L->base[si], P_i = L->base[si + 1] - L->base[si];
   SGN_EXEC_LDS(X)
@@ -3561,10 +3673,13 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
   struct RoundLDS {
     uint64_t ws, we, pend_ws, pend_we, pend_nb1, pg_avail;
     uint64_t pg_alloc, occ, hold_need;
-    uint64_t fhz;                // imports: the horizon of the round they were sent in
     uint32_t active, ks, pend, pend_new, ngap, hold;
-    uint32_t n_in, nin[XR_MAX];  // runs to file this round: in all, and from each shard
-    uint32_t fpend, fbuf;        // imports left for the next round's start (and their slot parity)
+    // runs to file from the inbox slots this round: in all, and from each shard (nin, from the
+    // exchange until they are filed); while the workgroup executes, nin counts its runs to each
+    // shard instead (OutboxHdr::xc; reset after the filing, flushed at the arrival)
+    uint32_t n_in, nin[XR_MAX];
+    uint32_t fpend, fbuf;        // imports left for the next round's start (and their slot parity;
+                                 // their horizon: the round pend_ws started)
     uint32_t last;               // this workgroup arrived last at the shard's local barrier
   };
   __shared__ RoundLDS rs;
@@ -3583,11 +3698,21 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     rs.fpend = 0;
     rs.n_in = 0;
     rs.last = 0;
+    rs.pend_ws = rs.ws;
     // (every spill-area entry so far may hold an import a gather must read: the re-layout at a
     // held edge empties the area)
     X.big->spill_imp = ld_dev(&C->spill_n);
   }
   const uint64_t rounds0 = ld_dev(&C->rounds);
+  // the calendar horizon of a round starting at ws0 (OutboxHdr::hz)
+  auto hz_of = [&](uint64_t ws0) { return SIM_START + (S.bw_div.div(ws0 - SIM_START) + S.NB) * S.BW; };
+  // this workgroup's share of the senders' bin counters of round parity k (zeroed in the round
+  // before their next use: no workgroup of this shard sends with them then)
+  auto bin_counters_reset = [&](uint32_t k) {
+    if (!S.xin_bins) return;
+    const uint32_t nb = R * S.xgx;
+    for (uint32_t i = w * 64 + threadIdx.x; i < nb; i += P * 64) st_dev(&S.xbin_n[(size_t)k * nb + i], 0u);
+  };
   // The runs other shards sent this shard (inbox slot parity fbuf, rs.nin per sender) into the
   // calendar with the bucket -> slab table as it is now; their bucket minima except for the
   // buckets of the window [nws, nwe) they will be gathered in (its first bucket's minimum is not
@@ -3645,7 +3770,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         st_dev(&S.rb_cnt[o], 0u);
         st_dev(&S.rb2_cnt[o], 0u);
       }
-      for (uint32_t i = threadIdx.x; i < R; i += 64) st_dev(&S.xout_n[q * R + i], 0u);
+      for (uint32_t i = threadIdx.x; i < R; i += 64) {
+        st_dev(&S.xout_n[q * R + i], 0u);
+        st_dev(&S.xout_n[(3 + q) * R + i], 0u);
+      }
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
@@ -3653,6 +3781,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         st_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + q], (uint64_t)0);
       }
     }
+    // (the bins this round's gathers read were filled with parity (rounds0 + r) & 1 last round;
+    // the next round sends with it again)
+    bin_counters_reset((uint32_t)((rounds0 + r) & 1));
     if (threadIdx.x == 0) {
       X.ob->keepmin = &S.rb_keep[p];
       X.ob->bbase = ws;
@@ -3661,16 +3792,20 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       X.ob->pg_allocd = &S.rb_occ[3 * RB_CH * RB_OS_MAX + p];
       X.ob->spilled = &S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p];
       X.ob->xn = S.xout_n + (size_t)p * R;
+      X.ob->xc = S.xin_bins ? rs.nin : nullptr;
       X.ob->xbuf = (uint32_t)((rounds0 + r + 1) & 1);
     }
     // diagnostics (SGN_STAMPS=2): per round of this launch, on the 100 MHz clock: {earliest start,
     // latest local arrival, local barrier seen (last workgroup), its messages sent, latest "all
     // messages seen", latest imports filed, latest second barrier seen}
-    SGN_GLB uint64_t* rd = S.rdbg ? S.rdbg + 8 * (size_t)(r & 127) : nullptr;
+    // (SGN_STAMPS=3: every workgroup's own stamps, plain stores: [128 rounds][2048][8])
+    SGN_GLB uint64_t* rd = S.rdbg ? S.rdbg + (S.rdbg_wg ? ((size_t)(r & 127) * 2048 + w) * 8 : 8 * (size_t)(r & 127)) : nullptr;
     auto stamp = [&](uint32_t i, bool mx) {
       if (rd && threadIdx.x == 0) {
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        if (mx)
+        if (S.rdbg_wg)
+          rd[i] = t;
+        else if (mx)
           __hip_atomic_fetch_max(rd + i, (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
           __hip_atomic_fetch_min(rd + i, (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3680,7 +3815,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     // the previous round's imports for this workgroup's groups (few of them: every workgroup
     // scans them all instead of a second barrier), before its gathers read the slabs
     if (uni32(rs.fpend)) {
-      file_in(rs.fbuf, rs.fhz, ws, we, true);
+      file_in(rs.fbuf, hz_of(rs.pend_ws), ws, we, true);
       __syncthreads();
       if (threadIdx.x == 0) {
         X.big->spill_imp = ld_dev(&C->spill_n);
@@ -3688,26 +3823,27 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       }
       __syncthreads();
     }
+    if (threadIdx.x < XR_MAX) rs.nin[threadIdx.x] = 0;  // (now the per-peer send counts: xc)
     // ---- 1. execute this workgroup's groups, then arrive (the last arrival learns it is) ----
     uint64_t kall = INVALID, mall = INVALID, oall = 0;
     bool arrived = false;
     for (uint32_t g = gq0; g < gq1; g += gqs) {
       uint64_t kmin, m;
       const bool lastg = g + gqs >= gq1;
-      exec_group<false, kApp, kKxBig>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
+      exec_group<false, kApp, kKxBig, true>(S, g, ws, we, ks, X, &kmin, &m, [&](uint64_t k, uint64_t n, uint64_t od) {
         kall = k < kall ? k : kall;
         mall = n < mall ? n : mall;
         oall += od;
         if (lastg) {
           flush_bmin<kApp>(S, X);
           stamp(1, true);
-          rb_arrive_x<kApp>(S, p, w, P, kall, mall, oall, &rs.last);
+          rb_arrive_x<kApp>(S, p, w, P, kall, mall, oall, &rs.last, X.ob->xc);
           arrived = true;
         }
       });
       __syncthreads();
     }
-    if (!arrived) rb_arrive_x<kApp>(S, p, w, P, INVALID, INVALID, 0, &rs.last);
+    if (!arrived) rb_arrive_x<kApp>(S, p, w, P, INVALID, INVALID, 0, &rs.last, nullptr);
     __syncthreads();
     const uint64_t tag = rounds0 + r + 1;  // the global round number + 1 (the same on every shard)
     const uint32_t buf = (uint32_t)(tag & 1);
@@ -3721,13 +3857,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       stamp(2, true);
       // the message's own inputs beside the round edge's loads (no dependent round trips)
       SGN_GLB uint64_t* hm = nullptr;
-      uint64_t cnt = 0;
+      uint64_t cnt = 0, tot = 0;  // runs to the peer: in its slot; in all (bins and slot)
       if (lane < R) hm = S.xp[lane].hdr[buf];
-      if (lane < R && lane != me) cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
+      if (lane < R && lane != me) {
+        cnt = ld_dev(&S.xout_n[(size_t)p * R + lane]);
+        tot = S.xin_bins ? (uint64_t)ld_dev(&S.xout_n[(size_t)(3 + p) * R + lane]) : cnt;
+      }
       const uint64_t spilled = ld_dev(&C->spill_n);
       const uint64_t mu = ld_dev(&C->min_used);
       const RbEdge e = rb_edge<kApp>(S, p, nch, ws, we);  // (its window: this shard's view only)
-      uint64_t xmax = cnt, xsum = cnt;
+      uint64_t xmax = cnt, xsum = tot;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = shfl_xor64(xmax, off);
@@ -3738,7 +3877,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         const uint64_t v[XH_N] = {cnt, e.min_next, mu, xmax, spilled ? 1ull : 0ull,
                                   pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
                                   rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total, S.nH,
-                                  e.nb1, e.occd, e.nalloc, e.nfree};
+                                  e.nb1, e.occd, e.nalloc, e.nfree, tot};
         if (S.xsys) {
 #pragma unroll
           for (uint32_t k = 0; k < XH_N; k++) st_sys16(hm + 2 * k, v[k], tag);
@@ -3791,15 +3930,19 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     auto xw = [&](uint32_t k, uint32_t q) { return shfl64((k & 1) ? gb : ga, (int)(q + 8 * (k >> 1))); };
     uint64_t gm = INVALID, gmu = INVALID, xs = 0, xmax = 0;
     uint32_t spill_any = 0, nin_l = 0;
+    uint64_t bin_l = 0;  // (lane q: runs sender q put in this shard's bins)
     for (uint32_t q = 0; q < R; q++) {
       const uint64_t a0 = xw(XH_MIN, q), a1 = xw(XH_MU, q), a2 = xw(XH_XSUM, q), a3 = xw(XH_XMAX, q);
-      const uint64_t a4 = xw(XH_SPILL, q), a5 = xw(XH_CNT, q);
+      const uint64_t a4 = xw(XH_SPILL, q), a5 = xw(XH_CNT, q), a6 = xw(XH_TOT, q);
       gm = a0 < gm ? a0 : gm;
       gmu = a1 < gmu ? a1 : gmu;
       xs += a2;
       xmax = a3 > xmax ? a3 : xmax;
       spill_any |= a4 ? 1u : 0u;
-      if (lane == q && q != me) nin_l = (uint32_t)min(a5, (uint64_t)S.xislot);
+      if (lane == q && q != me) {
+        nin_l = (uint32_t)min(a5, (uint64_t)S.xislot);
+        bin_l = a6 - a5;
+      }
     }
     // Runahead::get (runahead.rs:44-57) over the global min used latency; the controller
     // (controller.rs:88-112) over the global min next event
@@ -3832,7 +3975,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
                    e_nfree = xw(XH_NFREE, me);
     uint32_t n_in = nin_l;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+      n_in += __shfl_xor(n_in, off, 64);
+      bin_l += shfl_xor64(bin_l, off);
+    }
     // the idle-gap case of k_rounds: the bookkeeping now, and a local barrier before any send of
     // the next round can reach this round's bucket indices again
     const uint64_t span = (uint64_t)S.NB * S.BW;
@@ -3869,7 +4015,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       rs.active = active;
       rs.pg_avail += e_nfree;
       rs.pg_alloc += e_nalloc;
-      rs.occ += e_occd + n_in;
+      rs.occ += e_occd + n_in + bin_l;  // (every import counts from here: slots and bins)
       rs.n_in = n_in;
       rs.hold = hflags;
       rs.hold_need = own_need;
@@ -3886,16 +4032,14 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
     // ---- 5. the runs other shards sent this shard: a few are filed by their own workgroups at
     // the next round's start; many are shared out now and a second local barrier follows ----
     if (uni32(rs.n_in)) {
-      const uint64_t hz = SIM_START + (S.bw_div.div(ws - SIM_START) + S.NB) * S.BW;
       if (uni32(rs.n_in) <= S.xown) {
         if (threadIdx.x == 0) {
           rs.fpend = 1;
           rs.fbuf = buf;
-          rs.fhz = hz;
         }
         __syncthreads();
       } else {
-        file_in(buf, hz, uni64(rs.ws), uni64(rs.we), false);
+        file_in(buf, hz_of(ws), uni64(rs.ws), uni64(rs.we), false);
         stamp(5, true);
         rb2_arrive<kApp>(S, p, w, P);
         if (!rb_wait<kApp>(&S.rb2_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS], nch)) {
@@ -3907,10 +4051,58 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         __syncthreads();
       }
     }
+    stamp(7, true);
   }
   // imports left for a next round this launch does not run: shared out now (the launch's end is
   // the barrier)
-  if (uni32(rs.fpend)) file_in(rs.fbuf, rs.fhz, uni64(rs.ws), uni64(rs.we), false);
+  if (uni32(rs.fpend)) file_in(rs.fbuf, hz_of(uni64(rs.pend_ws)), uni64(rs.ws), uni64(rs.we), false);
+  // ... and the last round's bins of this workgroup's groups (file_in's rules: the launch's end
+  // leaves every bin empty and every counter zero, whatever runs next)
+  if (S.xin_bins) {
+    const uint32_t ib = (uint32_t)((rounds0 + r) & 1);
+    const uint64_t nws = uni64(rs.ws), nwe = uni64(rs.we), fhz = hz_of(uni64(rs.pend_ws));
+    const uint32_t sb0 = bucket_of(S, nws), sbn = ((bucket_of(S, nwe - 1) - sb0) & (S.NB - 1)) + 1;
+    uint32_t ln = threadIdx.x;
+    asm volatile("" : "+v"(ln));
+    const uint32_t bsh = R <= 2 ? 5u : R <= 4 ? 4u : 3u, E = 1u << bsh, q = ln >> bsh, e = ln & (E - 1);
+    const bool on = q < R && q != me && e < S.xbk;
+    bool spilled = false;
+    for (uint32_t g = gq0; g < gq1; g += gqs) {
+      SGN_GLB EvRec* bp = on ? S.xin_bins + (((size_t)ib * R + q) * S.G + g) * S.xbk + e : nullptr;
+      bool more = on;
+      for (uint32_t e0 = 0; e0 < S.xbk; e0 += E) {
+        EvRec ev{};
+        if (more) ev = S.xsys ? ld_sys_rec(bp + e0) : ld_dev_rec(bp + e0);
+        const bool ok = more && ev.pc != 0;
+        if (ok) {
+          SGN_GLB uint64_t* pw = (SGN_GLB uint64_t*)(bp + e0) + 3;
+          if (S.xsys) st_sys(pw, 0ull); else st_dev(pw, (uint64_t)0);
+          if (ev.time >= fhz) {
+            if ((atomicOr(&C->overflow, OVF_HORIZON) & OVF_HORIZON) == 0) C->overflow_info = ev.dst;
+          } else {
+            const uint32_t b = bucket_of(S, ev.time);
+            const size_t idx = (size_t)X.lbs[b] * S.G + g;
+            const uint32_t pos = atomicAdd(&S.slab_n[idx], 1u);
+            if (((b - sb0) & (S.NB - 1)) >= sbn) min_nr(&S.bucket_min[b], ev.time);
+            if (pos < S.CAP) {
+              st_dev_rec(S.pool + idx * S.CAP + pos, ev);
+            } else {
+              place_overflow(S, nullptr, (uint32_t)idx, pos, ev);
+              spilled = true;
+            }
+          }
+        }
+        const uint64_t m = __ballot(ok && e == E - 1);
+        if (!m) break;
+        more = on && ((m >> (q * E + E - 1)) & 1ull) && e0 + E + e < S.xbk;
+      }
+    }
+    bin_counters_reset(ib);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (runs past their slab: the next launch's gathers read the spill area up to here)
+    if (__ballot(spilled) && threadIdx.x == 0)
+      (void)__hip_atomic_fetch_max(&C->spill_imp, ld_dev(&C->spill_n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // the launch's per-wave statistics (k_rounds)
   __syncthreads();
   if (X.wacc && threadIdx.x < W_N && X.wacc[threadIdx.x] && gq0 < gq1) {
@@ -3930,7 +4122,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       st_dev(&C->rounds, rounds0 + r);
       st_dev(&C->pg_avail, rs.pg_avail);
       st_dev(&C->cal_occ, rs.occ);
-      st_dev(&C->spill_imp, X.big->spill_imp);
+      (void)__hip_atomic_fetch_max(&C->spill_imp, X.big->spill_imp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (rs.hold) {
         st_dev(&C->hold, rs.hold);
         st_dev(&C->hold_need, rs.hold_need);
@@ -4835,12 +5027,14 @@ void drop_graph(sgn_ctx* ctx) {
 // ---- persistent multi-shard rounds (k_rounds_x): host side ----
 // Inbox layout (one uncached allocation per shard): headers [2][R][XH_WORDS], census words [R]
 // (padded to a line), runs [2][R][xislot].
-XLay xlay(uint32_t R, uint64_t xislot) {
+// (then the bins: [2][R][G][xbk] runs, G = the receiving shard's host groups)
+XLay xlay(uint32_t R, uint64_t xislot, uint32_t G, uint32_t xbk) {
   XLay l;
   l.hdr = 0;
   l.cen = (size_t)2 * R * XH_WORDS * 8;
   l.runs = l.cen + ((size_t)R * 8 + 127) / 128 * 128;
-  l.bytes = l.runs + (size_t)2 * R * xislot * sizeof(EvRec);
+  l.bins = l.runs + (size_t)2 * R * xislot * sizeof(EvRec);
+  l.bytes = l.bins + (size_t)2 * R * G * xbk * sizeof(EvRec);
   return l;
 }
 
@@ -4864,7 +5058,7 @@ void xinbox_release(sgn_ctx* ctx) {
 // inbox and the peer mappings go (the caller maps the new ones).
 int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot) {
   DevSim& S = ctx->S;
-  const XLay l = xlay(ctx->nranks, xislot);
+  const XLay l = xlay(ctx->nranks, xislot, S.G, S.xbk);
   void* p = nullptr;
   // (a local group's shards share this GPU: ordinary device memory, device-scope accesses;
   // one shard per GPU: uncached, the peers write it over xGMI)
@@ -4883,6 +5077,7 @@ int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot) {
   S.xin_cen = (decltype(S.xin_cen))((char*)p + l.cen);
   S.xin_runs = (decltype(S.xin_runs))((char*)p + l.runs);
   S.xislot = (uint32_t)xislot;
+  S.xin_bins = S.xbk ? (decltype(S.xin_bins))((char*)p + l.bins) : nullptr;
   return 0;
 }
 
@@ -4891,16 +5086,19 @@ int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot) {
 int xpeer_upload(sgn_ctx* ctx) {
   DevSim& S = ctx->S;
   const uint32_t R = ctx->nranks, s = ctx->rank;
-  const XLay l = xlay(R, S.xislot);
   std::vector<XPeer> xp(R);
   std::memset(xp.data(), 0, R * sizeof(XPeer));
   for (uint32_t q = 0; q < R; q++) {
     XPeer& x = xp[q];
     char* b = q < ctx->x_base.size() ? ctx->x_base[q] : nullptr;
+    const uint32_t Gq = q < ctx->x_G.size() ? ctx->x_G[q] : 0;
+    const XLay l = xlay(R, S.xislot, Gq, S.xbk);  // (receiver q's inbox)
     if (b) {
       for (uint32_t k = 0; k < 2; k++) {
         x.runs[k] = (std::remove_reference_t<decltype(x.runs[k])>)((EvRec*)(b + l.runs) + ((size_t)k * R + s) * S.xislot);
         x.hdr[k] = (std::remove_reference_t<decltype(x.hdr[k])>)((uint64_t*)(b + l.hdr) + ((size_t)k * R + s) * XH_WORDS);
+        if (S.xbk)
+          x.bins[k] = (std::remove_reference_t<decltype(x.bins[k])>)((EvRec*)(b + l.bins) + ((size_t)k * R + s) * Gq * S.xbk);
       }
       x.cen = (decltype(x.cen))((uint64_t*)(b + l.cen) + s);
     }
@@ -4971,7 +5169,7 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
     if (cap_env) P = std::max<uint64_t>(1, std::min<uint64_t>(P, (uint64_t)atoi(cap_env)));
     P = std::min<uint64_t>(P, 64 * RB_CH);
     xl.base[i] = b;
-    xl.S[i] = (const DevSim*)c->d_S;
+    xl.S[i] = (std::remove_reference_t<decltype(xl.S[i])>)c->d_S;
     b += (uint32_t)P;
     c->x_grid = (uint32_t)P;
     const DevSim& S = c->S;
@@ -5119,7 +5317,7 @@ int run_xpersist(const std::vector<sgn_ctx*>& sh, bool peers, uint64_t max_round
     enq = c0->h_ctrl->rounds - r_start;
   }
   for (sgn_ctx* c : sh)  // (the per-round path counts its sends in row 0 from zero)
-    if (c->S.xout_n) (void)hipMemsetAsync((void*)c->S.xout_n, 0, (3 * (size_t)c->nranks + 8) * 4, c->stream);
+    if (c->S.xout_n) (void)hipMemsetAsync((void*)c->S.xout_n, 0, (6 * (size_t)c->nranks + 8) * 4, c->stream);
   if (rounds_done) *rounds_done = c0->h_ctrl->rounds - r_start;
   return rc;
 }
@@ -5450,7 +5648,10 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   // atomic min and max per workgroup and round on shared words: it slows the rounds it times)
   if (const char* e = getenv("SGN_STAMPS")) {
     S.stamps = (decltype(S.stamps))dalloc<uint64_t>(ctx, SGN_STAMP_WORDS * G);
-    if (atoi(e) >= 2) S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, 8 * 128);
+    if (atoi(e) >= 2) {
+      S.rdbg_wg = atoi(e) >= 3 ? 1u : 0u;
+      S.rdbg = (decltype(S.rdbg))dalloc<uint64_t>(ctx, S.rdbg_wg ? (size_t)8 * 128 * 2048 : 8 * 128);
+    }
   }
   if (ctx->trace_cap) {
     S.trace = (decltype(S.trace))dalloc<sgn_trace_rec>(ctx, ctx->trace_cap);
@@ -5486,7 +5687,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     S.xout = (decltype(S.xout))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
     S.xin = (decltype(S.xin))dalloc<EvRec>(ctx, (size_t)ctx->nranks * (ctx->xslot + XHDR));
     // (per-round launches count in row 0; k_rounds_x in row round % 3)
-    S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 3 + 8);
+    // (k_rounds_x: rows [3][n_ranks] of slot counts, then [3][n_ranks] of totals, bins included)
+    S.xout_n = (decltype(S.xout_n))dalloc<uint32_t>(ctx, ctx->nranks * 6 + 8);
     S.xin_n = (decltype(S.xin_n))dalloc<uint32_t>(ctx, ctx->nranks * 2 + 8);
     if (!S.xout || !S.xin || !S.xout_n || !S.xin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (exchange)");
     // persistent rounds: the second barrier's counters, the XPeer table, the launch descriptor
@@ -5498,6 +5700,30 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
     S.xp = (decltype(S.xp))ctx->d_xp;
     S.xown = kOwnFile;
     if (const char* e = getenv("SGN_XOWN")) S.xown = (uint32_t)atoi(e);
+    // inbox bins: xbk runs per (parity, sender, receiving group), a power of two;
+    // SGN_XBIN: another size, 0 = none (every import through the slots)
+    ctx->x_G.assign(ctx->nranks, 0u);
+    S.xgx = 0;
+    for (uint32_t q = 0; q < ctx->nranks; q++) {
+      uint32_t lo = 0, hi = 0;
+      sgn_shard_range(N, q, ctx->nranks, &lo, &hi);
+      ctx->x_G[q] = (hi - lo + gsz - 1) / gsz;
+      S.xgx = std::max(S.xgx, ctx->x_G[q]);
+    }
+    S.xbk = kXBin;
+    if (const char* e = getenv("SGN_XBIN")) {  // (a test hook: small bins send runs to the slots)
+      const uint32_t v = (uint32_t)atoi(e);
+      S.xbk = 0;
+      if (v) {
+        S.xbk = 1;
+        while (S.xbk < v && S.xbk < (1u << 12)) S.xbk *= 2;
+      }
+    }
+    S.xbin_n = nullptr;
+    if (S.xbk) {
+      S.xbin_n = (decltype(S.xbin_n))dalloc<uint32_t>(ctx, (size_t)2 * ctx->nranks * S.xgx);
+      if (!S.xbin_n) return set_error(ctx, SGN_ENOMEM, "device allocation failed (inbox bin counters)");
+    }
     uint64_t xis = ctx->xslot;
     if (const char* e = getenv("SGN_XISLOT")) xis = std::max<uint64_t>(1, std::min<uint64_t>(xis, (uint64_t)atoll(e)));
     ctx->S = S;  // (xinbox_alloc / xpeer_upload work on ctx->S)
@@ -6013,6 +6239,17 @@ int sgn_debug_rounds_x(sgn_ctx* ctx, uint64_t* out) {
   std::vector<uint64_t> init(8 * 128, 0);
   for (int r = 0; r < 128; r++) init[8 * r] = ~0ULL;
   SGN_HIP(ctx, hipMemcpy((void*)ctx->S.rdbg, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// k_rounds_x with SGN_STAMPS=3: every workgroup's stamps, [128 rounds][2048 workgroups][8]
+// (this shard's workgroup index; unwritten: 0); resets.
+int sgn_debug_rounds_xw(sgn_ctx* ctx, uint64_t* out) {
+  if (!ctx || !ctx->sim_ready || !ctx->S.rdbg || !ctx->S.rdbg_wg) return SGN_EINVAL;
+  const size_t n = (size_t)8 * 128 * 2048;
+  SGN_HIP(ctx, hipDeviceSynchronize());
+  SGN_HIP(ctx, hipMemcpy(out, (const void*)ctx->S.rdbg, n * 8, hipMemcpyDeviceToHost));
+  SGN_HIP(ctx, hipMemset((void*)ctx->S.rdbg, 0, n * 8));
   return 0;
 }
 

@@ -30,6 +30,14 @@ namespace sgn {
 #else
 #define SGN_GLB
 #endif
+// Read-only for a kernel's lifetime (the constant address space): loads through it are
+// invariant, so uniform ones are scalar loads (k_rounds_x's per-shard DevSim: read through a
+// plain pointer from the launch descriptor, every field access was a vector flat load)
+#ifdef __HIP_DEVICE_COMPILE__
+#define SGN_CONST __attribute__((address_space(4)))
+#else
+#define SGN_CONST
+#endif
 
 constexpr uint64_t SIM_START = SGN_SIMULATION_START;
 constexpr uint64_t EMU_MAX = SGN_EMUTIME_MAX;
@@ -423,7 +431,15 @@ struct DevSim {
                               // 0: one GPU's (a local group: device-scope accesses, L2-served)
   uint32_t xown;              // a round's imports up to this many runs: filed by their own
                               // workgroups at the next round's start (else shared + a barrier)
-  uint32_t pad_x;
+  uint32_t xbk;               // inbox bins: runs per (round parity, sender, receiving host group)
+  // inbox bins (k_rounds_x): [2][n_ranks][G][xbk] runs sent to this shard, binned by the
+  // receiving host group, which reads its own bins during its next gather (empty entries: pc 0,
+  // the reader zeroes what it took); the senders' position counters per (parity, receiver,
+  // receiving group), [2][n_ranks][xgx]
+  SGN_GLB EvRec* xin_bins;
+  SGN_GLB uint32_t* xbin_n;
+  uint32_t xgx;               // the largest shard's host groups (the counters' row length)
+  uint32_t rdbg_wg;           // diagnostics: rdbg holds every workgroup's stamps (SGN_STAMPS=3)
 };
 
 // Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and
@@ -432,11 +448,12 @@ struct DevSim {
 // across GPUs, ordinary device memory when the shards are workgroup ranges of one launch).
 // XPeer is one sender's view of one receiver's inbox: where its runs and its message go in each
 // round parity, and its census word. runs[2] is the RCCL transport's send block (per-round path).
+// bins[k]: this sender's bins in the receiver's inbox for round parity k ([G_receiver][xbk]).
 struct XPeer {
   SGN_GLB EvRec* runs[3];
   SGN_GLB uint64_t* hdr[2];
   SGN_GLB uint64_t* cen;
-  uint64_t pad[2];
+  SGN_GLB EvRec* bins[2];
 };
 // A message is 16 GRANULES of 16 bytes, {value, tag}, each written by one 16-byte store (the
 // receiver polls them and has the values in the same round trip; a 16-byte store is observed
@@ -459,6 +476,7 @@ enum : uint32_t {  // granule k holds message word k (its tag: the global round 
   XH_OCCD,
   XH_NALLOC,
   XH_NFREE,
+  XH_TOT,        // runs the sender sent this receiver this round: its bins and its slot
   XH_N
 };
 // k_rounds_x launch descriptor (device memory): the shards this launch runs, each on a
@@ -470,7 +488,7 @@ struct XLaunch {
   uint64_t epoch;                // launch number (census tags)
   uint32_t res_base, pad_l;      // the first shard's census arrival count before this launch
   uint32_t base[XL_MAX + 1];     // workgroup range of local shard i: [base[i], base[i + 1])
-  const struct DevSim* S[XL_MAX];
+  const SGN_CONST struct DevSim* S[XL_MAX];
 };
 
 constexpr uint32_t SPILL_PEER = 0x80000000u;  // spill area tag: a run for that peer shard's exchange slot
@@ -612,6 +630,7 @@ struct sgn_ctx {
   uint32_t x_grid = 0;         // this shard's workgroups in the last k_rounds_x launch
   uint32_t x_share = 1;        // shards on this GPU (one shard per GPU: 1)
   uint64_t x_epoch = 0, x_grows = 0, x_over_rounds = 0, x_moved = 0, x_launches = 0;
+  std::vector<uint32_t> x_G;   // every shard's host groups (its bins' rows), by rank
 
   ~sgn_ctx();
 };
@@ -642,9 +661,9 @@ int comm_allreduce_minmax(sgn_ctx* ctx, uint64_t* p, size_t n_min, size_t n_max)
 int comm_allreduce_max_u32(sgn_ctx* ctx, uint32_t* p, size_t n);
 // persistent multi-shard rounds (engine.hip: the launches; comm.cpp: the IPC mapping over RCCL)
 struct XLay {
-  size_t hdr, cen, runs, bytes;
+  size_t hdr, cen, runs, bins, bytes;
 };
-XLay xlay(uint32_t R, uint64_t xislot);
+XLay xlay(uint32_t R, uint64_t xislot, uint32_t G, uint32_t xbk);
 int xinbox_alloc(sgn_ctx* ctx, uint64_t xislot);
 void xinbox_release(sgn_ctx* ctx);
 int xpeer_upload(sgn_ctx* ctx);  // the XPeer table from ctx->x_base (and the RCCL send blocks)

@@ -254,6 +254,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "sgn_debug_stamps": (C.c_int, [vp, u64p, C.c_uint64, u64p]),
         "sgn_debug_rounds": (C.c_int, [vp, u64p]),
         "sgn_debug_rounds_x": (C.c_int, [vp, u64p]),
+        "sgn_debug_rounds_xw": (C.c_int, [vp, u64p]),
         "sgn_submit": (C.c_int, [vp, C.POINTER(PktSoa)]),
         "sgn_drain_enable": (C.c_int, [vp, C.c_uint64]),
         "sgn_drain": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(DrainRec), C.c_uint64, u64p]),

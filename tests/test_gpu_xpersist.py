@@ -1,8 +1,8 @@
 """Persistent multi-shard rounds (k_rounds_x): N shards, each a range of workgroups of
 ONE launch on one GPU — the device code of the N-GPU path (direct stores into the receivers'
-inboxes, per-round tagged messages, every shard computing the same window from the N messages,
-the imports filed before a second local barrier), with the inboxes in ordinary uncached device
-memory instead of peer-mapped memory. Each run is checked against ONE unsharded run (itself
+inboxes: bins per receiving host group, read by its next gather, and per-sender slots; per-round
+tagged messages, every shard computing the same window from the N messages), with the inboxes in
+ordinary device memory instead of peer-mapped uncached memory. Each run is checked against ONE unsharded run (itself
 checked against the oracle by the other GPU tests) and, for config C, against the oracle:
 every host's digests, every counter and the window, bit for bit."""
 import ctypes as C
@@ -130,9 +130,11 @@ def test_xpersist_matches_per_round_group(monkeypatch):
 
 @pytest.mark.parametrize("islot", [1, 6, 64])
 def test_xpersist_inbox_overflow_and_growth(monkeypatch, islot):
-    """Inbox slots far below a round's exports: runs past a slot wait in the sender's spill area,
-    the round edge is held on every shard, the host moves them into their shards' calendars and
-    grows every inbox; slots filled past half are grown before the next round. Bit-exact."""
+    """Inbox slots far below a round's exports (no bins: SGN_XBIN=0, every import through the
+    slots): runs past a slot wait in the sender's spill area, the round edge is held on every
+    shard, the host moves them into their shards' calendars and grows every inbox; slots filled
+    past half are grown before the next round. Bit-exact."""
+    monkeypatch.setenv("SGN_XBIN", "0")
     monkeypatch.setenv("SGN_XISLOT", str(islot))
     n = 500
     bw = np.where(np.arange(n) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
@@ -147,6 +149,27 @@ def test_xpersist_inbox_overflow_and_growth(monkeypatch, islot):
         assert info[0]["inbox_grows"] > 0 and info[0]["inbox_slot_runs"] > islot, info[0]
     if islot == 1:
         assert info[0]["inbox_overflow_rounds"] > 0 and sum(i["inbox_moved_runs"] for i in info) > 0, info
+    compare(one, shards, n)
+
+
+@pytest.mark.parametrize("xbin,islot", [("1", None), ("2", "1"), ("4", None)])
+def test_xpersist_inbox_bins(monkeypatch, xbin, islot):
+    """The inbox bins (runs binned by receiving host group, read by that group's next gather):
+    bins of 1, 2 and 4 runs overflow into the slots every round (and, with 1-run slots, past
+    them into the senders' spill areas: held rounds, moved runs, grown inboxes); runs due in the
+    window they arrive for go into their slabs ahead of the gathers. Bit-exact either way."""
+    n = 500
+    bw = np.where(np.arange(n) % 10 == 0, 100_000_000, 4_000_000).astype(np.uint64)
+    args = scenario(n=n, V=30, kind=sgn.TRAFFIC_TGEN, stop_ns=400_000_000, bw=bw, tor=True, tgen_think=50_000_000)
+    one = unsharded(args)
+    monkeypatch.setenv("SGN_XBIN", xbin)
+    if islot:
+        monkeypatch.setenv("SGN_XISLOT", islot)
+    shards, _, _ = local_group(args, 4)
+    info = [c.engine_info() for c in shards]
+    assert all(i["exchange_mode"] == 2 for i in info)
+    if islot:
+        assert max(i["inbox_overflow_rounds"] for i in info) > 0, info
     compare(one, shards, n)
 
 
