@@ -664,7 +664,12 @@ def main():
         # the whole slot, and bytes this rank sent to peers per round since sim_init
         out["exchange"] = {"slot_runs": info["exchange_slot_runs"], "send_runs": info["exchange_send_runs"],
                            "hwm_runs": info["exchange_hwm_runs"], "spills": info["exchange_spills"],
-                           "bytes_per_round": round(info["exchange_bytes"] / max(1, st1["rounds"]))}
+                           "bytes_per_round": round(info["exchange_bytes"] / max(1, st1["rounds"])),
+                           # 2: persistent rounds (k_rounds_x: peer inboxes over xGMI), 1: per-round
+                           # launches with the RCCL exchange
+                           "mode": info["exchange_mode"], "persistent_launches": info["persistent_x_launches"],
+                           "inbox_slot_runs": info["inbox_slot_runs"], "inbox_grows": info["inbox_grows"],
+                           "inbox_overflow_rounds": info["inbox_overflow_rounds"]}
     ws, we, act = ctx.window()
     out["sim_time_reached_ms"] = (ws - sgn.SIMULATION_START) / 1e6
     out["sim_ms_per_step"] = out["sim_time_reached_ms"] / (args.steps + args.warmup)

@@ -3496,6 +3496,16 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
         st_dev(&C->hold_need, rs.hold_need);
       }
     }
+    // ... and its copy in host memory: after the last barrier no other workgroup writes the
+    // control block (their counters and flags arrived with them)
+    if (S.ctrl_mirror) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      constexpr uint32_t NW = sizeof(Ctrl) / 8;
+      for (uint32_t i = threadIdx.x; i < NW; i += 64) st_sys(&S.ctrl_mirror[i], ld_dev(&((SGN_GLB uint64_t*)C)[i]));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) st_sys(&S.ctrl_mirror[NW], (uint64_t)epoch);
+    }
   }
 }
 
@@ -3536,6 +3546,10 @@ constexpr uint32_t kOwnFile = 2048;
 // inbox bins: runs per (round parity, sender, receiving host group). Config C at 8 shards sends
 // a group ~0.6 runs per sender and round, config D ~8; a fuller bin sends the rest to the slot.
 constexpr uint32_t kXBin = 32;
+// shards of up to this many workgroups arrive on one counter (k_rounds' chunk counters take
+// two returning atomics for the last arrival; at config C's ~200 workgroups per shard, spread
+// over the round's ~15 us of arrivals, one counter does not queue)
+constexpr uint32_t kXFlat = 256;
 constexpr uint64_t kXWaitTicks = 2000000000ull;  // 20 s on the 100 MHz clock: a peer that never
                                                  // answers is an error (OVF_TIMEOUT), not a hang
 
@@ -3585,10 +3599,14 @@ __device__ __forceinline__ void rb_arrive_x(const DevSim& S, uint32_t p, uint32_
   if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
   SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * Y::CB;
-  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t l = 0;
-  if (c == csz - 1)
-    l = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1 ? 1u : 0u;
+  if (nw <= kXFlat) {  // one counter: the last arrival learns it in one round trip
+    l = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nw - 1 ? 1u : 0u;
+  } else {
+    const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == csz - 1)
+      l = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1 ? 1u : 0u;
+  }
   *last = l;
 }
 
@@ -3925,9 +3943,18 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         return;
       }
       stamp(4, true);
+      // the words into LDS (the event list's space, free between rounds): word k of sender q
+      // at [k][q], read below as broadcasts (a shuffle per word and sender serialised ~200
+      // cross-lane reads on the round's critical path)
+      uint64_t* mw = (uint64_t*)X.lev;
+      if (mine) {
+        mw[(2 * jj) * XR_MAX + q] = ga;
+        if (2 * jj + 1 < XH_N) mw[(2 * jj + 1) * XR_MAX + q] = gb;
+      }
+      __syncthreads();
     }
     // word k of sender q
-    auto xw = [&](uint32_t k, uint32_t q) { return shfl64((k & 1) ? gb : ga, (int)(q + 8 * (k >> 1))); };
+    auto xw = [&](uint32_t k, uint32_t q) { return ((const uint64_t*)X.lev)[k * XR_MAX + q]; };
     uint64_t gm = INVALID, gmu = INVALID, xs = 0, xmax = 0;
     uint32_t spill_any = 0, nin_l = 0;
     uint64_t bin_l = 0;  // (lane q: runs sender q put in this shard's bins)
@@ -4632,6 +4659,18 @@ int sync_ctrl(sgn_ctx* ctx) {
   SGN_HIP(ctx, hipMemcpyAsync(ctx->h_ctrl, ctx->S.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost,
                               ctx->stream));
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  time_collect(ctx);
+  return check_overflow(ctx);
+}
+// After a persistent launch of census epoch ep: its own copy of the control block when it wrote
+// one (no device-to-host copy on the launch edge), else sync_ctrl.
+int sync_ctrl_persist(sgn_ctx* ctx, uint32_t ep) {
+  if (!ctx->failed.empty()) return set_error(ctx, SGN_ESTATE, "simulation unusable: " + ctx->failed);
+  if (!ctx->h_mirror) return sync_ctrl(ctx);
+  SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  constexpr size_t NW = sizeof(Ctrl) / 8;
+  if (__atomic_load_n(&ctx->h_mirror[NW], __ATOMIC_ACQUIRE) != ep) return sync_ctrl(ctx);
+  std::memcpy(ctx->h_ctrl, ctx->h_mirror, sizeof(Ctrl));
   time_collect(ctx);
   return check_overflow(ctx);
 }
@@ -5343,6 +5382,11 @@ void free_sim(sgn_ctx* ctx) {
     hipHostFree(ctx->h_ctrl);
     ctx->h_ctrl = nullptr;
   }
+  if (ctx->h_mirror) {
+    hipHostFree(ctx->h_mirror);
+    ctx->h_mirror = nullptr;
+  }
+  ctx->ctrl_fresh = false;
   ctx->sim_ready = false;
 }
 
@@ -5358,6 +5402,7 @@ int sgn_trace_enable(sgn_ctx* ctx, uint64_t capacity) {
 }
 
 int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx || !cfg || !tr) return SGN_EINVAL;
   if (!ctx->routes_ready) return set_error(ctx, SGN_ESTATE, "sgn_routes_build must precede sgn_sim_init");
   if (!ctx->hosts_ready) return set_error(ctx, SGN_ESTATE, "sgn_hosts_set must precede sgn_sim_init");
@@ -5761,6 +5806,14 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!S.ctrl) return set_error(ctx, SGN_ENOMEM, "device allocation failed");
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
+  static_assert(sizeof(Ctrl) % 8 == 0, "the control block's copy is written in u64 words");
+  if (!ctx->h_mirror) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_mirror, sizeof(Ctrl) + 8, 0));
+  std::memset(ctx->h_mirror, 0, sizeof(Ctrl) + 8);
+  {
+    void* dm = nullptr;
+    SGN_HIP(ctx, hipHostGetDevicePointer(&dm, ctx->h_mirror, 0));
+    S.ctrl_mirror = (decltype(S.ctrl_mirror))dm;
+  }
   *ctx->h_ctrl = c;
   S.fuse_finalize = ctx->nranks == 1 ? 1u : 0u;
   // PERIODIC traffic: each host receives ~BW / period runs per bucket, so a group's slab holds
@@ -5820,6 +5873,7 @@ int sgn_window(sgn_ctx* ctx, uint64_t* start, uint64_t* end, int32_t* active) {
 }
 
 int sgn_round(sgn_ctx* ctx, uint64_t* min_next) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx || !ctx->sim_ready) return ctx ? set_error(ctx, SGN_ESTATE, "no simulation") : SGN_EINVAL;
   if (int e = rng_release(ctx)) return e;
   if (ctx->comm_local)
@@ -5841,7 +5895,9 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   if (int e = rng_release(ctx)) return e;
   if (ctx->comm_local)
     return set_error(ctx, SGN_ESTATE, "a local shard group runs with sgn_run_local_group, not sgn_run");
-  int rc = sync_ctrl(ctx);
+  // (the control block as the last sgn_run left it, unless a call since may have changed it)
+  int rc = ctx->ctrl_fresh ? 0 : sync_ctrl(ctx);
+  ctx->ctrl_fresh = false;
   if (rc) return rc;
   // a round still held (an earlier pool growth failed and the caller runs again): grow first
   if ((ctx->h_ctrl->hold || ctx->h_ctrl->spill_n) && (rc = resolve_hold(ctx))) return rc;
@@ -5860,6 +5916,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
   const bool graph = ctx->use_graph && (ctx->nranks == 1 || ctx->comm) &&
                      getenv("SGN_GRAPH") && atoi(getenv("SGN_GRAPH")) == 1;
   if (ctx->nranks == 1 && ctx->persist_grid) {
+    bool fresh = true;
     // persistent rounds: one launch runs up to kPersistRounds rounds (grid barriers inside);
     // a launch ends early at a held round edge (a pool grows here, then the rounds go on)
     while (ctx->h_ctrl->active && enq < max_rounds && ctx->persist_grid) {
@@ -5870,7 +5927,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
       time_end(ctx);
       ctx->kt[K_EXECUTE].total++;
       SGN_HIP(ctx, hipGetLastError());
-      if ((rc = sync_ctrl(ctx))) return rc;
+      if ((rc = sync_ctrl_persist(ctx, ctx->res_epoch))) return rc;
       if (census_verdict(ctx, ctx->res_epoch) != 1) {
         // the grid was not resident (the occupancy model was wrong, or another context holds
         // part of the GPU): nothing ran; continue with one launch per round
@@ -5879,6 +5936,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
         ctx->persist_off = true;
         break;
       }
+      if (ctx->h_ctrl->hold || ctx->h_ctrl->spill_n) fresh = false;  // (the host grows a pool)
       if ((rc = resolve_hold(ctx))) return rc;
       enq = ctx->h_ctrl->rounds - r_start;
     }
@@ -5889,6 +5947,7 @@ int sgn_run(sgn_ctx* ctx, uint64_t max_rounds, uint64_t* rounds_done) {
       return rc;
     }
     if (rounds_done) *rounds_done = ctx->h_ctrl->rounds - r_start;
+    ctx->ctrl_fresh = fresh;
     return 0;
   }
   // multi-shard, one shard per GPU: persistent rounds with the peers' inboxes mapped into this
@@ -6273,6 +6332,7 @@ int sgn_drain_enable(sgn_ctx* ctx, uint64_t capacity) {
 }
 
 int sgn_submit(sgn_ctx* ctx, const sgn_pkt_soa* b) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx || !b) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   const DevSim& S = ctx->S;
@@ -6397,6 +6457,7 @@ uint64_t sgn_stage_pending(const sgn_stage* st) {
 }
 
 int sgn_stage_flush(sgn_ctx* ctx) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx) return SGN_EINVAL;
   std::vector<uint32_t> src, dst, pay, wire;
   std::vector<uint64_t> time, handle;
@@ -6436,6 +6497,7 @@ int sgn_stage_flush(sgn_ctx* ctx) {
 }
 
 int sgn_drain(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64_t cap, uint64_t* n_out) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx || (!out && cap)) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   if (ctx->S.tkind != SGN_TRAFFIC_EXTERNAL)
@@ -6474,6 +6536,7 @@ int sgn_drain(sgn_ctx* ctx, uint32_t lo, uint32_t hi, sgn_drain_rec* out, uint64
 }
 
 int sgn_set_window(sgn_ctx* ctx, uint64_t start, uint64_t end) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx) return SGN_EINVAL;
   if (!ctx->sim_ready) return set_error(ctx, SGN_ESTATE, "no simulation");
   int rc = sync_ctrl(ctx);
@@ -6578,12 +6641,17 @@ int rng_draw(sgn_ctx* ctx, uint32_t host, uint32_t n, uint64_t* out) {
 
 int sgn_rng_next_u64_batch(sgn_ctx* ctx, const uint32_t* hosts, const uint32_t* counts, uint32_t n,
                            uint64_t* out) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   return rng_draws(ctx, hosts, counts, n, out);
 }
 
-int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out) { return rng_draw(ctx, host, 1, out); }
+int sgn_rng_next_u64(sgn_ctx* ctx, uint32_t host, uint64_t* out) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
+  return rng_draw(ctx, host, 1, out);
+}
 
 int sgn_rng_double(sgn_ctx* ctx, uint32_t host, double* out) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!out) return SGN_EINVAL;
   uint64_t x = 0;
   int rc = rng_draw(ctx, host, 1, &x);
@@ -6592,6 +6660,7 @@ int sgn_rng_double(sgn_ctx* ctx, uint32_t host, double* out) {
 }
 
 int sgn_rng_fill_bytes(sgn_ctx* ctx, uint32_t host, uint8_t* buf, size_t len) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!buf && len) return SGN_EINVAL;
   if (len / 8 + 1 > 0xFFFFFFFFull) return set_error(ctx, SGN_ERANGE, "sgn_rng_fill_bytes: len too large");
   const size_t full = len / 8, rem = len % 8;
@@ -6610,6 +6679,7 @@ int sgn_rng_fill_bytes(sgn_ctx* ctx, uint32_t host, uint8_t* buf, size_t len) {
 
 // Test hook: device CoDel control-law increments for count in [0, n).
 int sgn_selftest_codel_law(sgn_ctx* ctx, uint64_t n, uint64_t* out) {
+  if (ctx) ctx->ctrl_fresh = false;  // (it may change the device control block)
   if (!ctx || !out) return SGN_EINVAL;
   SGN_HIP(ctx, hipSetDevice(ctx->device));
   uint64_t* d = nullptr;

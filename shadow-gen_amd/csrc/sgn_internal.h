@@ -440,6 +440,10 @@ struct DevSim {
   SGN_GLB uint32_t* xbin_n;
   uint32_t xgx;               // the largest shard's host groups (the counters' row length)
   uint32_t rdbg_wg;           // diagnostics: rdbg holds every workgroup's stamps (SGN_STAMPS=3)
+  // the control block's host-visible copy (pinned host memory): the persistent kernel's last
+  // workgroup writes it at the launch's end, then the launch's census epoch in the word after it
+  // (the host reads it after the stream synchronises, instead of a device-to-host copy)
+  SGN_GLB uint64_t* ctrl_mirror;
 };
 
 // Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and
@@ -551,6 +555,9 @@ struct sgn_ctx {
   std::vector<void*> allocs;
   uint64_t sim_bytes = 0;  // device bytes in allocs
   sgn::Ctrl* h_ctrl = nullptr;  // pinned mirror for reads
+  uint64_t* h_mirror = nullptr; // the persistent kernel's copy of the control block (DevSim::ctrl_mirror)
+  bool ctrl_fresh = false;      // h_ctrl is the device's control block (set by sgn_run; cleared by
+                                // every call that may change it)
   uint64_t trace_cap = 0;
   uint64_t drain_cap = 0;                 // sgn_drain_enable (EXTERNAL traffic)
   std::vector<uint64_t> handles;          // sgn_submit handles by slot (tag & ~SGN_TAG_EXT)

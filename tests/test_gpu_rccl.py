@@ -62,6 +62,27 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload, pool
         assert x["slot_runs"] > 64 and x["spills"] >= 1
 
 
+@pytest.mark.parametrize("workload,port", [("C", 29548), ("D", 29549)])
+def test_xpeer_two_processes_one_gpu_persistent(workload, port):
+    """The N-GPU persistent path itself (k_rounds_x with peer-mapped inboxes): two processes on
+    device 0 (SGN_XPEER_SHARED=1 lets the IPC mapping accept a peer on the same GPU; each grid
+    is sized for half the GPU), every round's runs stored straight into the other process's
+    inbox bins and slots, the messages and the residency census across processes — against
+    the unsharded run, bit for bit."""
+    env = dict(os.environ, SGN_GRAPH="0", NCCL_DEBUG="WARN", TMPDIR="/tmp", SGN_XPEER_SHARED="1")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--one-gpu", "--rounds-per-step", "70", "--workload", workload]
+    if workload == "D":
+        cmd += ["--hosts", "100000"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["exchange"]["mode"] == 2 and line["exchange"]["persistent_launches"] > 0, line["exchange"]
+    assert line["roofline"]["kernel"] == "k_rounds_x"
+    assert line["parity"] is True, line.get("parity_detail")
+
+
 def test_rccl_eight_ranks_one_gpu_match_unsharded():
     """The driver's N = 8 configuration: config C's 100 k hosts over eight ranks (12.5 k each),
     every rank exchanging with seven peers each round, against one unsharded run."""
