@@ -73,6 +73,8 @@ def test_two_shards_grow_together(ctxf, oracle, monkeypatch, slot):
     runs past a peer's exchange slot spill, the round is held on both shards, the slots grow
     alike and the round is exchanged again."""
     monkeypatch.setenv("SGN_SLAB_CAP", "16")
+    if slot == 16:  # (every import through the slots: persistent rounds' inbox bins would take them)
+        monkeypatch.setenv("SGN_XBIN", "0")
     n = 300
     args = _codel_args(n=n)
     g, used, hosts, cfg, tr = args
@@ -101,8 +103,13 @@ def test_two_shards_grow_together(ctxf, oracle, monkeypatch, slot):
     assert held[0] == held[1] >= 1, held
     assert max(s.engine_info()["codel_pool_grows"] for s in shards) >= 1
     if slot == 16:
-        assert all(s.engine_info()["exchange_slot_grows"] >= 1 for s in shards)
-        assert shards[0].engine_info()["exchange_slot_runs"] == shards[1].engine_info()["exchange_slot_runs"] > 16
+        info = [s.engine_info() for s in shards]
+        if info[0]["exchange_mode"] == 2:  # persistent rounds: the inbox slots grow
+            assert all(i["inbox_grows"] >= 1 for i in info), info
+            assert info[0]["inbox_slot_runs"] == info[1]["inbox_slot_runs"] > 16
+        else:
+            assert all(i["exchange_slot_grows"] >= 1 for i in info)
+            assert info[0]["exchange_slot_runs"] == info[1]["exchange_slot_runs"] > 16
     for r, s in enumerate(shards):
         lo, hi = C.c_uint32(), C.c_uint32()
         s.L.sgn_shard_range(n, r, 2, C.byref(lo), C.byref(hi))
