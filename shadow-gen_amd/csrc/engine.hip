@@ -2590,7 +2590,12 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
           bool direct = ((b - bs) & (S.NB - 1)) < nbk;
           slow |= direct;
           if (!direct) {
-            min_nr(&S.bucket_min[b], r.time);
+            // (the workgroup's LDS table of bucket minima where the kernel has one, as for sends:
+            // config D's ~100 k imports a round per shard would queue on a few bucket words)
+            if (kAggBmin<kApp> && S.agg_bmin)
+              atomicMin(&ob->bmin[b], (uint32_t)(r.time - ob->bbase));
+            else
+              min_nr(&S.bucket_min[b], r.time);
             const uint32_t k = atomicAdd(&ob->n, 1u);  // LDS
             if (k < kObox<kApp>) {
               ob->rec[k] = r;

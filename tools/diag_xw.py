@@ -10,7 +10,7 @@ Per round, on the 100 MHz clock (us), medians over 100 rounds:
   seen_all  = last workgroup with all messages - latest message stored
   post    = median (round end - all messages seen) per workgroup
   gap     = next round's earliest start - latest round end
-usage: python tools/diag_xw.py [hosts] [shards] [warmup_rounds]"""
+usage: python tools/diag_xw.py [hosts] [shards] [warmup_rounds] [C|D]"""
 import ctypes as C
 import os
 import pathlib
@@ -28,7 +28,12 @@ import sgn  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 300
-g, used, hosts, cfg, tr = bench.build_workload(n, 1000)
+wl = sys.argv[4] if len(sys.argv) > 4 else "C"
+if wl == "D":
+    g, used, hosts, cfg, tr = bench.build_workload_d(n, 1000, stop_ns=3_000_000_000)
+    cfg.event_capacity = 257 * -(-(-(-n // k)) // 64) * 128 * k  # (divided by k below)
+else:
+    g, used, hosts, cfg, tr = bench.build_workload(n, 1000)
 ctxs = [sgn.Context(shard_rank=r, shard_count=k, flags=2) for r in range(k)]
 arr = (C.c_void_p * k)(*[c.h.value for c in ctxs])
 for c in ctxs:

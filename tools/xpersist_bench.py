@@ -20,18 +20,19 @@ import bench  # noqa: E402
 import sgn  # noqa: E402
 
 
-def workload(name, n):
+def workload(name, n, k=1):
     if name == "C":
         return bench.build_workload(n, 1000)
     if name == "B":
         return bench.build_workload_b(n, 1000)
     g, used, hosts, cfg, tr = bench.build_workload_d(n, 1000, stop_ns=3_000_000_000)
-    cfg.event_capacity = 257 * -(-n // 64) * 128
+    # (bench.py's sizing: 128-run slabs per host group of a shard, 257 slab sets)
+    cfg.event_capacity = 257 * -(-(-(-n // k)) // 64) * 128
     return g, used, hosts, cfg, tr
 
 
 def run(name, n, k, rounds, warmup):
-    g, used, hosts, cfg, tr = workload(name, n)
+    g, used, hosts, cfg, tr = workload(name, n, k)
     if k == 1:
         ctxs = [sgn.Context(flags=2)]
     else:
