@@ -65,7 +65,10 @@
 enum { DG_RO = 0, DG_RI, DG_APP, DG_BATCH, DG_HDLOAD, DG_FQLOAD, DG_RMISS, DG_POPRUN, DG_N };
 // diagnostic timers: cycles while this lane was inside ...
 enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD,
-       DGT_HDLD, DGT_FHLD, DGT_RTLD, DGT_SVLD, DGT_SLAB, DGT_N };
+       DGT_HDLD, DGT_FHLD, DGT_RTLD, DGT_SVLD, DGT_SLAB,
+       DGT_DRAWS,   // (counts, not cycles) loss draws of this lane's trains
+       DGT_RENTRY,  // ... and the wave's entries into the draw loop (its lowest lane counts)
+       DGT_N };
 #ifdef SGN_DIAG
 #define DGT_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
 #else
@@ -406,6 +409,11 @@ __host__ __device__ __forceinline__ size_t exec_lds_runs_bytes(uint32_t cap) {
 // leaves C at 7 workgroups per CU), 24 for the others (config D's PERIODIC kernel must keep 8
 // workgroups per CU WITH its bucket-minimum table of 256 buckets: at 48 records the table no
 // longer fit and D ran 3.4x slower; 32 measured the same as 24, round 4).
+// a forwarding step of more packets than this waits for the wave's other lanes (HostExec::run)
+#ifndef SGN_TRAIN_WAIT
+#define SGN_TRAIN_WAIT 8
+#endif
+constexpr uint32_t kTrainWait = SGN_TRAIN_WAIT;
 template <uint32_t kApp>
 #ifndef SGN_OBOX_PERIODIC
 #define SGN_OBOX_PERIODIC 24
@@ -1539,6 +1547,10 @@ struct HostExec {
     const bool can_drop = !boot && payload > 0;
     uint32_t run = 0;  // consecutive sent packets not yet folded into the digest
     DGT_BEGIN(tr0);
+#ifdef SGN_DIAG
+    dgt[DGT_DRAWS] += n;
+    if ((uint32_t)(__ffsll((long long)__ballot(1)) - 1) == (threadIdx.x & 63)) dgt[DGT_RENTRY] += 1;
+#endif
 #ifdef SGN_EXP_NORNG
     if (true) {
       run = n;
@@ -1954,6 +1966,7 @@ struct HostExec {
 #ifdef SGN_DIAG
 #endif
     while (true) {
+      const uint64_t act = __ballot(1);  // (the wave's lanes still in their event loops)
       // earliest local event by (time, event id)
       uint64_t lt = st0, le = se0;
       int ls = 0;
@@ -2039,6 +2052,16 @@ struct HostExec {
         st0 = INVALID;
         set_relay_state<0>(RELAY_FORWARDING);
         fl |= F_RO_CONT;
+      }
+      // Trains side by side (TGEN: the servers' responses): a lane whose step is a long train
+      // waits while other lanes of the wave are still on other events — they may reach a train
+      // of their own, and then the trains' per-packet loss draws run in one pass instead of one
+      // pass per lane (config C's slowest waves ran their servers' draw loops 3 to 7 times
+      // over, diag build). Waiting changes nothing of the host's own sequence: `now` is fixed
+      // inside the forwarding task, and other lanes are other hosts.
+      if constexpr (kApp == SGN_TRAFFIC_TGEN) {
+        const bool lng = !(fl & F_RO_NEXT) && fq_len > 0 && fifo_head().count > kTrainWait;
+        if (lng && __ballot(1) != act) continue;
       }
       forward_out_step();
     }
