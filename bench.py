@@ -396,6 +396,16 @@ def apsp_roofline(apsp, V, U):
                    "hbm_frac": round(hbm / (lms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "l2_bytes": int(b_lat),
                    "l2_frac": round(b_lat / (lms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)})
         valu_bound(lp, 1.5 * Vp ** 3 * max(1, apsp["latency_passes"]), lms)
+    if apsp.get("latency_bf") and apsp["latency_ms"] > 0:
+        # per-source relaxation (sparse graphs): its arc re-reads (the model above) are served by
+        # the L2s — every (source, arc, sweep) is one add and one min (1.5 lane-ops with the
+        # v_min3 fold), the compulsory HBM bytes are the arc list once and the u64 rows written
+        lp, lms = out["latency_phase"], apsp["latency_ms"]
+        hbm = 12.0 * E + 8.0 * U * V
+        lp.update({"hbm_bytes": int(hbm), "hbm_GBps": round(hbm / (lms * 1e-3) / 1e9, 2),
+                   "hbm_frac": round(hbm / (lms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "l2_bytes": int(b_lat),
+                   "l2_frac": round(b_lat / (lms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)})
+        valu_bound(lp, 1.5 * U * E * max(1, apsp["latency_passes"]), lms)
     if k and ms > 0:
         valu_bound(out["loss_phase"], 1.5 * U * E, ms)
     out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
@@ -403,8 +413,8 @@ def apsp_roofline(apsp, V, U):
                     "u32 min-plus squaring, all passes in one launch (sq_run)"),
                    "loss": f"{k}-source sweep (tail-ordered arcs, branch-free add3/min3 filter) + LDS fold" if k
                    else "one-source arc sweep + LDS fold"}
-    out["note"] = ("frac is the fraction of each phase's bound: the squaring passes and the multi-source "
-                   "sweep are bound by 32-bit integer VALU issue (lane-ops over the phase's time, each "
+    out["note"] = ("frac is the fraction of each phase's bound: the squaring passes, the per-source "
+                   "relaxation and the multi-source sweep are bound by 32-bit integer VALU issue (lane-ops over the phase's time, each "
                    "phase timed whole including its launches and barrier); hbm_frac (HBM bytes / 8 TB/s) "
                    "and l2_frac (L2-served bytes / 34.5 TB/s) are reported beside it")
     return out
