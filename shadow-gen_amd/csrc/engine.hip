@@ -510,7 +510,13 @@ struct LaneRc {
 };
 struct LaneNoRc {};
 template <uint32_t kApp>
-constexpr bool kRcReg = kApp == SGN_TRAFFIC_PERIODIC;  // (TGEN with them in registers: C unchanged)
+constexpr bool kRcReg = kApp == SGN_TRAFFIC_PERIODIC;
+// the hot host line in per-64-host tiles, field-major (DevSim::htile, hot_idx): every chunk load
+// or store of a wave is one contiguous access instead of one line per lane. PERIODIC only:
+// same-box A/B, D 4.45 -> 4.61 G, B +0.3 %; the TGEN kernel of config C
+// measured 1.1 % slower (its cold lines are read with the hot one anyway)
+template <uint32_t kApp>
+constexpr bool kSoa = kApp == SGN_TRAFFIC_PERIODIC;  // (TGEN with them in registers: C unchanged)
 // the kernels whose sends fold their bucket minima in an LDS table (S.agg_bmin, flush_bmin):
 // PERIODIC (configs B and D: ~1 M sends a round on a few bucket words at D). TGEN has the LDS
 // since round 3's slimmer lane slots, but measured 2 % slower with the table on C.
@@ -623,6 +629,29 @@ struct HostExec {
       lr().tbc[1] = r.k_tbinc[1];
     }
     // the hot line
+    if constexpr (kSoa<kApp>) {
+      const SGN_GLB u64x2* T = (const SGN_GLB u64x2*)S.htile + hot_idx(h, 0);
+      // (chunk 7 first: the flags decide the cold loads below; then the rest in order of use)
+      const u64x2 c7 = T[448];
+      fl = (uint32_t)c7.y;
+      cq_head = (uint32_t)(c7.y >> 32);
+      lr().app_k = c7.x;
+      const u64x2 c0 = T[0], c1 = T[64], c2 = T[128], c3 = T[192], c4 = T[256], c5 = T[320], c6 = T[384];
+      r0 = c0.x;
+      r1 = c0.y;
+      r2 = c1.x;
+      r3 = c1.y;
+      eid = c2.x;
+      st2 = c2.y;
+      se2 = c3.x;
+      tbb0 = c3.y;
+      tbb1 = c4.x;
+      tbl0 = c4.y;
+      tbl1 = c5.x;
+      L->dig[0] = c5.y;
+      L->dig[1] = c6.x;
+      L->dig[2] = c6.y;
+    } else {
     r0 = r.rng[0];
     r1 = r.rng[1];
     r2 = r.rng[2];
@@ -640,6 +669,7 @@ struct HostExec {
     L->dig[0] = r.dig[0];
     L->dig[1] = r.dig[1];
     L->dig[2] = r.dig[2];
+    }
     // the cold lines (PERIODIC: only when the host ended its last round with state there)
     if (kApp != SGN_TRAFFIC_PERIODIC || (fl & F_COLD)) {
       st0 = r.st0;
@@ -755,6 +785,7 @@ struct HostExec {
   // and at config B's 16-host waves each was a partial-line write of its own)
   __device__ __forceinline__ void store(uint64_t old_next, uint32_t old_peer) {
     HostRec& r = *R;
+    if constexpr (!kSoa<kApp>) {
     r.rng[0] = r0;
     r.rng[1] = r1;
     r.rng[2] = r2;
@@ -771,6 +802,7 @@ struct HostExec {
     r.dig[2] = L->dig[2];
     r.app_k = lr().app_k;
     r.cq_head = cq_head;
+    }
     if (fl & F_FH_DIRTY) *fq_slot(0) = L->fh;  // a queued head that lived in LDS
     // the cold lines: PERIODIC writes them only when the host leaves state there (load() gives
     // an idle host its defaults: this must list every field that differs from them)
@@ -778,7 +810,20 @@ struct HostExec {
                       (fl & (F_RO_STATE | (3u << F_RI_STATE_SHIFT) | F_RO_NEXT | F_RI_NEXT | F_CODEL_IE |
                              F_CODEL_DN | F_CODEL_DROP)) ||
                       cq_nr || cq_len || cq_bytes || fq_len || fq_head;
-    r.flags = (fl & ~(F_FH_DIRTY | F_COLD)) | (cold ? F_COLD : 0u);
+    if constexpr (kSoa<kApp>) {
+      SGN_GLB u64x2* T = (SGN_GLB u64x2*)S.htile + hot_idx(h, 0);
+      const uint32_t f = (fl & ~(F_FH_DIRTY | F_COLD)) | (cold ? F_COLD : 0u);
+      T[0] = u64x2{r0, r1};
+      T[64] = u64x2{r2, r3};
+      T[128] = u64x2{eid, st2};
+      T[192] = u64x2{se2, tbb0};
+      T[256] = u64x2{tbb1, tbl0};
+      T[320] = u64x2{tbl1, L->dig[0]};
+      T[384] = u64x2{L->dig[1], L->dig[2]};
+      T[448] = u64x2{lr().app_k, (uint64_t)f | ((uint64_t)cq_head << 32)};
+    } else {
+      r.flags = (fl & ~(F_FH_DIRTY | F_COLD)) | (cold ? F_COLD : 0u);
+    }
     if (cold) {
       r.st0 = st0;
       r.st1 = st1;
@@ -3106,21 +3151,45 @@ template <uint32_t kApp> struct RbLayout {
 };
 constexpr uint32_t RB_CS_MAX = 32, RB_MS_MAX = 16, RB_OS_MAX = 16, RB_CB_MAX = (RB_CH + 1) * RB_CS_MAX;
 
+// SGN_RB_REL (experiment build): the chunk completer that completes the grid writes a release
+// word into every chunk's line, and each workgroup polls its own chunk's (64 pollers per line
+// instead of the whole grid on the top counter's)
+#ifdef SGN_RB_REL
+constexpr bool kRbRel = true;
+#else
+constexpr bool kRbRel = false;
+#endif
 template <uint32_t kApp>
 __device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
                                           uint64_t m, uint64_t occd) {
-  if (threadIdx.x != 0) return;
+  using Y = RbLayout<kApp>;
+  constexpr bool rel = kRbRel && Y::pad;
+  if (!rel && threadIdx.x != 0) return;
   const uint32_t ch = w >> 6;
   const uint32_t csz = min(64u, nw - (ch << 6));
-  using Y = RbLayout<kApp>;
-  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
-  if (kmin != INVALID) min_nr(mn, kmin);
-  if (m != INVALID) min_nr(mn + 1, m);
-  if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
   SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * Y::CB;
-  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t last = 0;
+  if (threadIdx.x == 0) {
+    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
+    if (kmin != INVALID) min_nr(mn, kmin);
+    if (m != INVALID) min_nr(mn + 1, m);
+    if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
+    const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == csz - 1) {
+      if (rel)
+        last = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               ((nw + 63) >> 6) - 1;
+      else
+        (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if constexpr (rel) {
+    if (__shfl(last, 0, 64)) {
+      const uint32_t nch = (nw + 63) >> 6;
+      for (uint32_t i = threadIdx.x; i < nch; i += 64) st_dev(&cnt[i * Y::CS + 1], 1u);
+    }
+  }
 }
 
 // The next window from buffer p after the barrier (every workgroup, identical results).
@@ -3236,6 +3305,7 @@ __device__ __forceinline__ void rb_reset0(const DevSim& S, uint32_t nch) {
   for (uint32_t i = threadIdx.x; i <= nch; i += 64) {
     const size_t o = (size_t)(i == nch ? RB_CH : i) * Y::CS;
     st_dev(&S.rb_cnt[o], 0u);
+    if (kRbRel && Y::pad) st_dev(&S.rb_cnt[o + 1], 0u);  // (the chunk's release word)
     if (S.rb2_cnt) st_dev(&S.rb2_cnt[o], 0u);
   }
   if (S.xout_n)
@@ -3358,7 +3428,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     rs.hold = ld_dev(&C->hold);  // (a round still held: the launch returns at once)
     rs.hold_need = ld_dev(&C->hold_need);
   }
-  const uint64_t rounds0 = ld_dev(&C->rounds);
+  // (the launch's first round number is read back at its end: nothing else writes it, and a
+  // register live across the whole launch spilled the PERIODIC big-slab kernel)
   const bool lds_tab = S.NB <= LDS_BSLAB;
   if (lds_tab)
     for (uint32_t i = threadIdx.x; i < S.NB; i += 64) X.lbs[i] = (uint16_t)ld_dev(&S.bucket_slab[i]);
@@ -3380,8 +3451,11 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
         st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS + 1], (uint64_t)INVALID);
         st_dev(&S.rb_occ[((size_t)q * RB_CH + i) * RbLayout<kApp>::OS], (uint64_t)0);
       }
-      for (uint32_t i = threadIdx.x; i <= nch; i += 64)  // the grid's chunks, then the top counter
-        st_dev(&S.rb_cnt[(size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS], 0u);
+      for (uint32_t i = threadIdx.x; i <= nch; i += 64) {  // the grid's chunks, then the top counter
+        const size_t o = (size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS;
+        st_dev(&S.rb_cnt[o], 0u);
+        if (kRbRel && RbLayout<kApp>::pad) st_dev(&S.rb_cnt[o + 1], 0u);  // (the chunk's release word)
+      }
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
@@ -3427,7 +3501,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     // grid barrier: every chunk complete, bounded
     uint32_t spins = 0;
     bool ok = true;
-    while (ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
+    while (kRbRel && RbLayout<kApp>::pad
+               ? ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + (w >> 6) * RbLayout<kApp>::CS + 1]) == 0
+               : ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
       // (TGEN: 1563 workgroups poll one word; a longer sleep between polls leaves the memory
       // side to the last arrivals' atomics: same-box A/B on C, 3639 -> 3586 us per 100-round
       // launch; PERIODIC: 8, see RbLayout)
@@ -3516,7 +3592,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       st_dev(&C->ws, rs.ws);
       st_dev(&C->we, rs.we);
       st_dev(&C->active, rs.active);
-      st_dev(&C->rounds, rounds0 + r);
+      st_dev(&C->rounds, ld_dev(&C->rounds) + r);
       st_dev(&C->pg_avail, rs.pg_avail);
       st_dev(&C->cal_occ, rs.occ);
       if (rs.hold) {
@@ -4396,7 +4472,10 @@ __global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* c
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   SGN_GLB HostRec* R = Sp->hrec + hosts[i];
-  uint64_t s0 = R->rng[0], s1 = R->rng[1], s2 = R->rng[2], s3 = R->rng[3];
+  // (the state's two chunks: in the tiles, or in the record's hot line)
+  SGN_GLB uint64_t* rg0 = Sp->htile ? Sp->htile + 2 * hot_idx(hosts[i], 0) : &R->rng[0];
+  SGN_GLB uint64_t* rg1 = Sp->htile ? Sp->htile + 2 * hot_idx(hosts[i], 1) : &R->rng[2];
+  uint64_t s0 = rg0[0], s1 = rg0[1], s2 = rg1[0], s3 = rg1[1];
   uint64_t* o = out + off[i];
   for (uint32_t k = 0; k < count[i]; k++) {
     o[k] = rotl64(s0 + s3, 23) + s0;
@@ -4408,10 +4487,10 @@ __global__ void k_rng(const DevSim* Sp, const uint32_t* hosts, const uint32_t* c
     s2 ^= t;
     s3 = rotl64(s3, 45);
   }
-  R->rng[0] = s0;
-  R->rng[1] = s1;
-  R->rng[2] = s2;
-  R->rng[3] = s3;
+  rg0[0] = s0;
+  rg0[1] = s1;
+  rg1[0] = s2;
+  rg1[1] = s3;
   R->rng_pos += count[i];
 }
 
@@ -4422,10 +4501,12 @@ __global__ void k_rng_set(const DevSim* Sp, const uint64_t* st, uint32_t n) {
   if (i >= n) return;
   const uint64_t* e = st + 6 * (size_t)i;
   SGN_GLB HostRec* R = Sp->hrec + (uint32_t)e[0];
-  R->rng[0] = e[1];
-  R->rng[1] = e[2];
-  R->rng[2] = e[3];
-  R->rng[3] = e[4];
+  SGN_GLB uint64_t* rg0 = Sp->htile ? Sp->htile + 2 * hot_idx((uint32_t)e[0], 0) : &R->rng[0];
+  SGN_GLB uint64_t* rg1 = Sp->htile ? Sp->htile + 2 * hot_idx((uint32_t)e[0], 1) : &R->rng[2];
+  rg0[0] = e[1];
+  rg0[1] = e[2];
+  rg1[0] = e[3];
+  rg1[1] = e[4];
   R->rng_pos += e[5];
 }
 
@@ -4434,9 +4515,12 @@ __global__ void k_rng_set(const DevSim* Sp, const uint64_t* st, uint32_t n) {
 __global__ void k_next_local(const DevSim* Sp, uint32_t lo, uint32_t n, uint64_t* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const HostRec& r = Sp->hrec[Sp->sid_of[lo + i] - Sp->lo];
-  uint64_t m = r.st2;
-  if (Sp->tkind != SGN_TRAFFIC_PERIODIC || (r.flags & F_COLD)) {  // (else both relays idle)
+  const uint32_t slot = Sp->sid_of[lo + i] - Sp->lo;
+  const HostRec& r = Sp->hrec[slot];
+  const uint64_t m0 = Sp->htile ? Sp->htile[2 * hot_idx(slot, 2) + 1] : r.st2;                   // st2
+  const uint32_t flg = Sp->htile ? (uint32_t)Sp->htile[2 * hot_idx(slot, 7) + 1] : r.flags;     // flags
+  uint64_t m = m0;
+  if (Sp->tkind != SGN_TRAFFIC_PERIODIC || (flg & F_COLD)) {  // (else both relays idle)
     m = r.st0 < m ? r.st0 : m;
     m = r.st1 < m ? r.st1 : m;
   }
@@ -5652,6 +5736,16 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   if (!S.hrec || !S.codel || !S.fifo || !S.cq_next || !S.rb_free)
     return set_error(ctx, SGN_ENOMEM, "device allocation failed (host state)");
   SGN_HIP(ctx, hipMemcpy((void*)S.hrec, recs.data(), recs.size() * sizeof(HostRec), hipMemcpyHostToDevice));
+  S.htile = nullptr;
+  if (tr->kind == SGN_TRAFFIC_PERIODIC) {  // the hot lines, tiled (kSoa)
+    const size_t nt = ((size_t)nH + 63) / 64;
+    std::vector<uint64_t> tile(nt * 8 * 64 * 2, 0);
+    for (uint32_t h = 0; h < nH; h++)
+      for (uint32_t c = 0; c < 8; c++) std::memcpy(&tile[2 * hot_idx(h, c)], (const char*)&recs[h] + 16 * c, 16);
+    S.htile = (decltype(S.htile))dalloc<uint64_t>(ctx, tile.size());
+    if (!S.htile) return set_error(ctx, SGN_ENOMEM, "device allocation failed (host tiles)");
+    SGN_HIP(ctx, hipMemcpy((void*)S.htile, tile.data(), tile.size() * 8, hipMemcpyHostToDevice));
+  }
   {
     HostConst* dk = dalloc<HostConst>(ctx, nH);
     S.n_cnt = (decltype(S.n_cnt))dalloc<uint64_t>(ctx, (size_t)N_CNT * nH);
@@ -6052,6 +6146,15 @@ int read_recs(sgn_ctx* ctx, uint32_t off, uint32_t n, std::vector<HostRec>* out)
   out->resize(n);
   if (n) SGN_HIP(ctx, hipMemcpy(out->data(), (const void*)(ctx->S.hrec + off), (size_t)n * sizeof(HostRec),
                                 hipMemcpyDeviceToHost));
+  if (n && ctx->S.htile) {  // the hot lines from their tiles
+    const uint32_t t0 = off >> 6, t1 = (off + n + 63) >> 6;
+    std::vector<uint64_t> tile((size_t)(t1 - t0) * 8 * 64 * 2);
+    SGN_HIP(ctx, hipMemcpy(tile.data(), (const void*)(ctx->S.htile + (size_t)t0 * 8 * 64 * 2), tile.size() * 8,
+                           hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; i++)
+      for (uint32_t c = 0; c < 8; c++)
+        std::memcpy((char*)&(*out)[i] + 16 * c, &tile[2 * (hot_idx(off + i, c) - (size_t)t0 * 8 * 64)], 16);
+  }
   return 0;
 }
 // the per-host totals of owned slots [off, off + n): N_CNT rows, then the CoDel maxima
@@ -6612,7 +6715,12 @@ int rng_cpu_draws(sgn_ctx* ctx, uint32_t host, uint64_t n, uint64_t* out) {
   if (it == ctx->rng_held.end()) {
     sgn_ctx::RngHeld h{};
     SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    SGN_HIP(ctx, hipMemcpy(h.s, (const void*)(ctx->S.hrec + slot), 32, hipMemcpyDeviceToHost));
+    if (ctx->S.htile) {
+      SGN_HIP(ctx, hipMemcpy(h.s, (const void*)(ctx->S.htile + 2 * hot_idx(slot, 0)), 16, hipMemcpyDeviceToHost));
+      SGN_HIP(ctx, hipMemcpy(h.s + 2, (const void*)(ctx->S.htile + 2 * hot_idx(slot, 1)), 16, hipMemcpyDeviceToHost));
+    } else {
+      SGN_HIP(ctx, hipMemcpy(h.s, (const void*)(ctx->S.hrec + slot), 32, hipMemcpyDeviceToHost));
+    }
     it = ctx->rng_held.emplace(slot, h).first;
   }
   for (uint64_t i = 0; i < n; i++) out[i] = host_xoshiro_next(it->second.s);

@@ -220,6 +220,11 @@ struct __attribute__((aligned(128))) HostRec {
   uint64_t pad[16];
 };
 static_assert(sizeof(HostRec) == 512, "HostRec is 4 cache lines");
+// PERIODIC simulations (configs B and D): the hot line lives in per-64-host tiles, field-major —
+// its 16-byte chunk c of host slot h at DevSim::htile[hot_idx(h, c)], so a wave's load of one
+// chunk is one contiguous 1 KB access instead of 64 lines (HostRec's line 0 is then unused on
+// the device; engine.hip kSoa)
+__host__ __device__ inline size_t hot_idx(uint32_t h, uint32_t c) { return ((size_t)(h >> 6) * 8 + c) * 64 + (h & 63); }
 static_assert(offsetof(HostRec, cq_nr) == 128, "line 0: the hot line");
 // the constants of a host's slot, read with the hot line (32 B)
 struct __attribute__((aligned(32))) HostConst {
@@ -444,6 +449,7 @@ struct DevSim {
   // workgroup writes it at the launch's end, then the launch's census epoch in the word after it
   // (the host reads it after the stream synchronises, instead of a device-to-host copy)
   SGN_GLB uint64_t* ctrl_mirror;
+  SGN_GLB uint64_t* htile;    // PERIODIC: the hot lines, tiled (hot_idx; null: in HostRec)
 };
 
 // Persistent multi-shard rounds (k_rounds_x): every shard owns an INBOX — per sender shard and
