@@ -3151,45 +3151,21 @@ template <uint32_t kApp> struct RbLayout {
 };
 constexpr uint32_t RB_CS_MAX = 32, RB_MS_MAX = 16, RB_OS_MAX = 16, RB_CB_MAX = (RB_CH + 1) * RB_CS_MAX;
 
-// SGN_RB_REL (experiment build): the chunk completer that completes the grid writes a release
-// word into every chunk's line, and each workgroup polls its own chunk's (64 pollers per line
-// instead of the whole grid on the top counter's)
-#ifdef SGN_RB_REL
-constexpr bool kRbRel = true;
-#else
-constexpr bool kRbRel = false;
-#endif
 template <uint32_t kApp>
 __device__ __forceinline__ void rb_arrive(const DevSim& S, uint32_t p, uint32_t w, uint32_t nw, uint64_t kmin,
                                           uint64_t m, uint64_t occd) {
-  using Y = RbLayout<kApp>;
-  constexpr bool rel = kRbRel && Y::pad;
-  if (!rel && threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return;
   const uint32_t ch = w >> 6;
   const uint32_t csz = min(64u, nw - (ch << 6));
+  using Y = RbLayout<kApp>;
+  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
+  if (kmin != INVALID) min_nr(mn, kmin);
+  if (m != INVALID) min_nr(mn + 1, m);
+  if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
   SGN_GLB uint32_t* cnt = S.rb_cnt + (size_t)p * Y::CB;
-  uint32_t last = 0;
-  if (threadIdx.x == 0) {
-    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + ch) * Y::MS;
-    if (kmin != INVALID) min_nr(mn, kmin);
-    if (m != INVALID) min_nr(mn + 1, m);
-    if (occd) cnt_add(&S.rb_occ[((size_t)p * RB_CH + ch) * Y::OS], occd);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stores and atomics done
-    const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c == csz - 1) {
-      if (rel)
-        last = __hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               ((nw + 63) >> 6) - 1;
-      else
-        (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if constexpr (rel) {
-    if (__shfl(last, 0, 64)) {
-      const uint32_t nch = (nw + 63) >> 6;
-      for (uint32_t i = threadIdx.x; i < nch; i += 64) st_dev(&cnt[i * Y::CS + 1], 1u);
-    }
-  }
+  const uint32_t c = __hip_atomic_fetch_add(&cnt[ch * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (c == csz - 1) (void)__hip_atomic_fetch_add(&cnt[RB_CH * Y::CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The next window from buffer p after the barrier (every workgroup, identical results).
@@ -3305,7 +3281,6 @@ __device__ __forceinline__ void rb_reset0(const DevSim& S, uint32_t nch) {
   for (uint32_t i = threadIdx.x; i <= nch; i += 64) {
     const size_t o = (size_t)(i == nch ? RB_CH : i) * Y::CS;
     st_dev(&S.rb_cnt[o], 0u);
-    if (kRbRel && Y::pad) st_dev(&S.rb_cnt[o + 1], 0u);  // (the chunk's release word)
     if (S.rb2_cnt) st_dev(&S.rb2_cnt[o], 0u);
   }
   if (S.xout_n)
@@ -3451,11 +3426,8 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
         st_dev(&S.rb_min[((size_t)q * RB_CH + i) * RbLayout<kApp>::MS + 1], (uint64_t)INVALID);
         st_dev(&S.rb_occ[((size_t)q * RB_CH + i) * RbLayout<kApp>::OS], (uint64_t)0);
       }
-      for (uint32_t i = threadIdx.x; i <= nch; i += 64) {  // the grid's chunks, then the top counter
-        const size_t o = (size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS;
-        st_dev(&S.rb_cnt[o], 0u);
-        if (kRbRel && RbLayout<kApp>::pad) st_dev(&S.rb_cnt[o + 1], 0u);  // (the chunk's release word)
-      }
+      for (uint32_t i = threadIdx.x; i <= nch; i += 64)  // the grid's chunks, then the top counter
+        st_dev(&S.rb_cnt[(size_t)q * RbLayout<kApp>::CB + (i == nch ? RB_CH : i) * RbLayout<kApp>::CS], 0u);
       if (threadIdx.x == 0) {
         st_dev(&S.rb_keep[q], (uint64_t)INVALID);
         st_dev(&S.rb_free[q], (uint64_t)0);
@@ -3501,9 +3473,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
     // grid barrier: every chunk complete, bounded
     uint32_t spins = 0;
     bool ok = true;
-    while (kRbRel && RbLayout<kApp>::pad
-               ? ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + (w >> 6) * RbLayout<kApp>::CS + 1]) == 0
-               : ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
+    while (ld_dev(&S.rb_cnt[(size_t)p * RbLayout<kApp>::CB + RB_CH * RbLayout<kApp>::CS]) < nch) {
       // (TGEN: 1563 workgroups poll one word; a longer sleep between polls leaves the memory
       // side to the last arrivals' atomics: same-box A/B on C, 3639 -> 3586 us per 100-round
       // launch; PERIODIC: 8, see RbLayout)
