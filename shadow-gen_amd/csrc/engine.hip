@@ -3180,54 +3180,57 @@ __device__ __forceinline__ RbEdge rb_edge(const DevSim& S, uint32_t p, uint32_t 
   using Y = RbLayout<kApp>;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b0 = bucket_of(S, ws), b1 = bucket_of(S, we - 1);
-  uint64_t kk = INVALID, wn = INVALID, m = INVALID, km = INVALID, mu = INVALID;
-  uint64_t od = 0, na = 0, nf = 0, ns = 0;
-  if (lane < nch) {
-    SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + lane) * Y::MS;
-    kk = ld_dev(mn);
-    wn = ld_dev(mn + 1);
-    od = ld_dev(&S.rb_occ[((size_t)p * RB_CH + lane) * Y::OS]);
-  }
-  if (S.tkind != SGN_TRAFFIC_EXTERNAL) {
-    // synthetic traffic: every pending event is a delivery, so it lies in [we, we + max_lat)
-    // (sends happen inside a window and arrive at most max_lat later, worker.rs:386-390): only
-    // the buckets after b1 up to bucket_of(we + max_lat - 1) can hold one (b1: nb1 below).
-    // 1563 workgroups read these words at once after the barrier: C reads ~151 of its 256
-    // buckets, B and D ~51 (same-box A/B: C -0.6 %, B -0.5 % per launch, D unchanged)
-    const uint32_t span = (b1 - b0) & (S.NB - 1);
-    uint32_t nscan = (uint32_t)min<uint64_t>(S.NB - 1 - span, S.bw_div.div(S.max_lat + S.BW - 1) + 1);
-    for (uint32_t k = lane; k < nscan; k += 64) {
-      const uint64_t bm = ld_dev(&S.bucket_min[(b1 + 1 + k) & (S.NB - 1)]);
-      m = bm < m ? bm : m;
+  // Every load of the edge is issued before any is used: one round trip. (The loop form of the
+  // bucket scan — one load per 64 buckets, each waited for before the next — and the counters
+  // loaded after it made the edge ~5 dependent round trips; C scans ~151 buckets.) Lanes past
+  // a range load a valid word of it and ignore it; the single words are loaded by every lane
+  // (one request), so no broadcast follows.
+  const uint32_t nc = nch ? nch : 1u;
+  SGN_GLB uint64_t* mn = S.rb_min + ((size_t)p * RB_CH + min(lane, nc - 1)) * Y::MS;
+  uint64_t kk = ld_dev(mn), wn = ld_dev(mn + 1);
+  uint64_t od = ld_dev(&S.rb_occ[((size_t)p * RB_CH + min(lane, nc - 1)) * Y::OS]);
+  const uint64_t km = ld_dev(&S.rb_keep[p]), mu = ld_dev(&S.ctrl->min_used);
+  const uint64_t na = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + p]), ns = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p]);
+  const uint64_t nf = ld_dev(&S.rb_free[p]);
+  // the buckets to scan: synthetic traffic — every pending event is a delivery, so it lies in
+  // [we, we + max_lat) (sends happen inside a window and arrive at most max_lat later,
+  // worker.rs:386-390): only the buckets after b1 up to bucket_of(we + max_lat - 1) can hold
+  // one (b1: nb1 below; C scans ~151 of its 256 buckets, B and D ~51). CPU-submitted datagrams
+  // may be filed further ahead: every bucket the window has not consumed. (The persistent
+  // kernels run with NB <= LDS_BSLAB = 256: at most four buckets per lane.)
+  const bool ext = S.tkind == SGN_TRAFFIC_EXTERNAL;
+  const uint32_t span = (b1 - b0) & (S.NB - 1);
+  const uint32_t nscan = ext ? S.NB - 1 - span
+                             : (uint32_t)min<uint64_t>(S.NB - 1 - span, S.bw_div.div(S.max_lat + S.BW - 1) + 1);
+  uint64_t m = INVALID;
+  if (nscan) {
+    uint64_t bm[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+      bm[q] = ld_dev(&S.bucket_min[(b1 + 1 + min(lane + 64 * q, nscan - 1)) & (S.NB - 1)]);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+      if (lane + 64 * q < nscan) m = bm[q] < m ? bm[q] : m;
+    for (uint32_t k = lane + 256; k < nscan; k += 64) {  // (NB > 256: not on the persistent path)
+      const uint64_t v = ld_dev(&S.bucket_min[(b1 + 1 + k) & (S.NB - 1)]);
+      m = v < m ? v : m;
     }
-  } else {  // (CPU-submitted datagrams may be filed further ahead)
-    for (uint32_t b = lane; b < S.NB; b += 64) {
-      const bool consumed = ((b - b0) & (S.NB - 1)) < ((b1 - b0) & (S.NB - 1)) || b == b1;
-      if (!consumed) {
-        const uint64_t bm = ld_dev(&S.bucket_min[b]);
-        m = bm < m ? bm : m;
-      }
-    }
   }
-  if (lane == 0) {
-    km = ld_dev(&S.rb_keep[p]);
-    mu = ld_dev(&S.ctrl->min_used);
-    na = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + p]);
-    ns = ld_dev(&S.rb_occ[3 * RB_CH * RB_OS_MAX + 3 + p]);
-    nf = ld_dev(&S.rb_free[p]);
+  if (lane >= nch) {
+    kk = INVALID;
+    wn = INVALID;
+    od = 0;
   }
   kk = wave_min_u64(kk);
   wn = wave_min_u64(wn);
   m = wave_min_u64(m);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) od += shfl_xor64(od, off);
-  km = shfl64(km, 0);
-  mu = shfl64(mu, 0);
   RbEdge e;
   e.occd = od;
-  e.nalloc = shfl64(na, 0);
-  e.nfree = shfl64(nf, 0);
-  e.nspill = shfl64(ns, 0);
+  e.nalloc = na;
+  e.nfree = nf;
+  e.nspill = ns;
   e.nb1 = km < kk ? km : kk;  // the spare slab set becomes bucket b1
   m = e.nb1 < m ? e.nb1 : m;
   m = wn < m ? wn : m;
