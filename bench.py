@@ -291,8 +291,11 @@ def cpu_baseline(g, used, hosts, cfg, tr, args, gpu):
         s0 = events_of(sim.stats())
         t1 = time.perf_counter()
         r = 0
+        # (rounds per call: config D's 1M hosts take ~1 s a round in the single-core faithful
+        # mode, so its samples step 2 rounds at a time to stay near the budget)
+        step = 20 if hosts.n <= 200_000 else 2
         while time.perf_counter() - t1 < budget and sim.window()[2]:
-            r += sim.run(20)
+            r += sim.run(step)
             progress(f"{name} sample")
         e1 = time.perf_counter() - t1
         e = events_of(sim.stats()) - s0
@@ -420,6 +423,22 @@ def apsp_roofline(apsp, V, U):
     return out
 
 
+def launch_ranks(n, argv):
+    """Runs `python -m torch.distributed.run --nproc-per-node n bench.py <argv>` as a child (the
+    driver's own launch line: one node, 127.0.0.1, a free port) and returns its exit status.
+    SGN_BENCH_LAUNCH_DRY=1 prints the command as JSON instead (tests/test_bench_launch.py)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py")] + list(argv)
+    if os.environ.get("SGN_BENCH_LAUNCH_DRY"):
+        print(json.dumps(cmd), flush=True)
+        return 0
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -453,7 +472,15 @@ def main():
                     help="N > 1: skip the unsharded re-run on rank 0 that checks the sharded results")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start the N ranks (one per GPU) under
+        # torch.distributed.run as a CHILD process — before anything in this process touches a
+        # GPU — and exit with its status (--gpus was ignored, and N > 1 ran one GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.one_gpu:
@@ -605,8 +632,11 @@ def main():
         if tf.exists():
             want = {"name": args.workload, "hosts_per_gpu": n_shard, "graph_nodes": args.nodes,
                     "rounds_per_launch": round(rpl), "n_gpus": world, "steps": args.steps, "warmup": args.warmup}
+            build = sgn.build_id()
+            roof["traffic_note"] = f"no PMC entry for this invocation on this libsgn build ({build})"
             for t in json.loads(tf.read_text()).get("entries", []):
-                if t.get("workload") == want and t.get("kernel") == rk:
+                if t.get("workload") == want and t.get("kernel") == rk and t.get("build") == build:
+                    roof["traffic_note"] = f"measured on this libsgn build ({build})"
                     roof["traffic"] = t["traffic_bytes_per_launch"]
                     roof["traffic_unit"] = "bytes/launch (PMC, profiles/round_kernel_traffic.json)"
                     roof["traffic_provenance"] = t.get("bench_args")

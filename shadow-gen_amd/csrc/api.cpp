@@ -132,6 +132,11 @@ int sgn_create(sgn_ctx** out, const sgn_create_opts* opts) {
     g_create_error = "shard_rank must be < shard_count";
     return SGN_EINVAL;
   }
+  if (sgn::layout_sig_engine() != kLayoutSig || sgn::layout_sig_routes() != kLayoutSig ||
+      sgn::layout_sig_comm() != kLayoutSig) {
+    g_create_error = "libsgn's objects were compiled against different versions of sgn_internal.h (rebuild all of them)";
+    return SGN_ESTATE;
+  }
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) {
@@ -338,3 +343,5 @@ uint64_t sgn_worker_get_bandwidth_down_bytes(sgn_ctx* ctx, uint32_t ip_be) {
 }
 
 }  // extern "C"
+
+uint64_t sgn::layout_sig_api() { return kLayoutSig; }

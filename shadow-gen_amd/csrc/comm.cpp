@@ -457,3 +457,5 @@ int sgn_run_local_group(sgn_ctx* const* ctxs, uint32_t n, uint64_t max_rounds, u
 }
 
 }  // extern "C"
+
+uint64_t sgn::layout_sig_comm() { return kLayoutSig; }

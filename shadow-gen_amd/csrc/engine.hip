@@ -3316,6 +3316,16 @@ __device__ __forceinline__ void rb_reset0(const DevSim& S, uint32_t nch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// A workgroup of k_rounds that gives up on a barrier (OVF_TIMEOUT) may do so after the
+// bookkeeping workgroup copied the control block into host memory: it also marks the copy
+// stale (the word after the epoch), and the host then reads the device's block.
+static_assert(sizeof(Ctrl) % 8 == 0, "the control block is copied as 8-byte words");
+constexpr uint32_t kMirrorWords = sizeof(Ctrl) / 8 + 2;  // the block, the epoch, the stale mark
+__device__ __forceinline__ void fail_timeout(const DevSim& S) {
+  atomicOr((unsigned int*)&S.ctrl->overflow, OVF_TIMEOUT);
+  if (S.ctrl_mirror) st_sys(&S.ctrl_mirror[kMirrorWords - 1], 1ull);
+}
+
 // Residency census (thread 0 of each workgroup): the workgroup counts itself in and waits,
 // bounded, for the whole grid of P; the first to see it, or to give up, sets the verdict with a
 // compare-and-swap, so every workgroup acts on the same one. The arrival counter is never reset
@@ -3502,7 +3512,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
       }
     }
     if (!ok) {
-      if (threadIdx.x == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+      if (threadIdx.x == 0) fail_timeout(S);
       return;
     }
     asm volatile("" ::: "memory");
@@ -3526,7 +3536,7 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
         __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t sp = 0;
         while (ld_dev(gc) < target && ++sp < (1u << 24)) __builtin_amdgcn_s_sleep(2);
-        if (sp >= (1u << 24)) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+        if (sp >= (1u << 24)) fail_timeout(S);
         rs.ngap++;
       }
     }
@@ -3626,6 +3636,15 @@ __global__ __launch_bounds__(64, 2) void k_rounds(const DevSim* __restrict__ Sg,
 // re-layout, are held on every shard alike (the same messages, the same decisions) and the host
 // completes them between launches.
 constexpr uint32_t XR_MAX = 8;  // shards of a persistent multi-shard run (one MI355X node)
+#ifdef SGN_XNOFENCE  // cost experiments only (build_exp.sh): the messages without system-scope fences
+constexpr bool kXFenceRel = false, kXFenceAcq = false;
+#elif defined(SGN_XNOACQ)
+constexpr bool kXFenceRel = true, kXFenceAcq = false;
+#elif defined(SGN_XNOREL)
+constexpr bool kXFenceRel = false, kXFenceAcq = true;
+#else
+constexpr bool kXFenceRel = true, kXFenceAcq = true;
+#endif
 #ifdef SGN_KX_NOBIG  // cost experiment only (build_exp.sh): k_rounds_x without the big-slab path
 constexpr bool kKxBig = false;
 #else
@@ -3644,6 +3663,9 @@ constexpr uint32_t kXBin = 32;
 constexpr uint32_t kXFlat = 256;
 constexpr uint64_t kXWaitTicks = 2000000000ull;  // 20 s on the 100 MHz clock: a peer that never
                                                  // answers is an error (OVF_TIMEOUT), not a hang
+// the census across GPUs: 60 s, so that shards whose launches start far apart (one of them
+// re-laying its calendar out or growing a pool first) wait instead of failing
+constexpr uint64_t kXCensusTicks = 6000000000ull;
 
 template <uint32_t kApp>
 __device__ __forceinline__ bool rb_wait(SGN_GLB uint32_t* top, uint32_t nch) {
@@ -3748,35 +3770,58 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
   {
     __shared__ uint32_t verdict;
     SGN_GLB Ctrl* C0 = L->S[0]->ctrl;
-    if (w == P - 1) rb_reset0<kApp>(S, (P + 63) >> 6);
+    const uint32_t ep32 = (uint32_t)L->epoch << 2;
+    if (w == P - 1 && !L->refuse) rb_reset0<kApp>(S, (P + 63) >> 6);
     if (threadIdx.x == 0) {
-      bool decided;
-      uint32_t v = census(C0, gridDim.x, (uint32_t)L->epoch, L->res_base, &decided);
+      bool decided = true;
+      // (a refused launch is one workgroup on a GPU that cannot hold the grid: it only tells the
+      // peers, so that every shard falls back together — ADVICE r5)
+      uint32_t v = L->refuse ? 2u : census(C0, gridDim.x, (uint32_t)L->epoch, L->res_base, &decided);
+      if (L->refuse) st_dev(&C->res_verdict, ep32 | 2u);
       if (L->peers_census) {
         const uint64_t ep = L->epoch << 2;
-        if (decided)  // the deciding workgroup tells every shard (its own inbox too)
+        if (decided) {
+          // the deciding workgroup tells every shard (its own inbox too), then combines the
+          // peers' verdicts for its whole shard under ONE deadline: a peer that is not resident,
+          // or never answers, stops this shard too
           for (uint32_t q = 0; q < R; q++) st_sys(S.xp[q].cen, ep | v);
-        if (v == 1) {  // a peer that is not resident (or never answers) stops this shard too
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          for (uint32_t q = 0; q < R && v == 1; q++) {
-            uint64_t c;
-            while (((c = ld_sys(&S.xin_cen[q])) >> 2) != L->epoch) {
-              if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
-                c = ep | 2;
-                atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
-                break;
+          if (v == 1) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t q = 0; q < R && v == 1; q++) {
+              uint64_t c;
+              while (((c = ld_sys(&S.xin_cen[q])) >> 2) != L->epoch) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kXCensusTicks) {
+                  c = ep | 2;
+                  atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(8);
               }
-              __builtin_amdgcn_s_sleep(8);
+              if ((c & 3) != 1) v = 3;
             }
-            if ((c & 3) != 1) v = 3;
           }
+          st_dev(&C->res_xverdict, ep32 | v);
+        } else if (v == 1) {
+          // the other workgroups act on the decider's combined verdict only (its deadline, then
+          // a margin: they never time out on their own before it does)
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          uint32_t c;
+          while (((c = ld_dev(&C->res_xverdict)) & ~3u) != ep32) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * kXCensusTicks) {
+              c = ep32 | 3u;
+              atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+          }
+          v = c & 3u;
         }
       }
       verdict = v;
     }
     __syncthreads();
     if (verdict != 1) {
-      if (verdict == 3 && w == P - 1 && threadIdx.x == 0) st_dev(&C->res_verdict, ((uint32_t)L->epoch << 2) | 3u);
+      if (verdict == 3 && w == P - 1 && threadIdx.x == 0) st_dev(&C->res_verdict, ep32 | 3u);
       return;
     }
   }
@@ -3983,17 +4028,32 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         xmax = o > xmax ? o : xmax;
         xsum += shfl_xor64(xsum, off);
       }
+      if (kXFenceRel && S.xsys) {
+        // System-scope release before the message (the peers are other GPUs): every run this
+        // shard stored into a peer's bins or slot was a write-through sc0 sc1 store whose wave
+        // waited for it (s_waitcnt vmcnt(0)) before arriving, and the arrivals completed before
+        // this workgroup learned it is last; the fence writes back anything else of this XCD's
+        // L2 and orders it all before the message words. (The wait after it is explicit: the
+        // compiler may drop its own, MI355X_MICROARCH.md "compiler hazard".)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       if (lane < R) {
         const uint64_t v[XH_N] = {cnt, e.min_next, mu, xmax, spilled ? 1ull : 0ull,
                                   pages_free(rs.pg_avail + e.nfree, rs.pg_alloc + e.nalloc),
                                   rs.occ + e.occd, xsum, (uint64_t)S.G * S.CAP + S.ext_total, S.nH,
                                   e.nb1, e.occd, e.nalloc, e.nfree, tot};
+        // every 8-byte word tagged (xh_lo / xh_hi): across GPUs each is its own 8-byte atomic
+        // store, so no receiver relies on a 16-byte store arriving untorn over xGMI
         if (S.xsys) {
 #pragma unroll
-          for (uint32_t k = 0; k < XH_N; k++) st_sys16(hm + 2 * k, v[k], tag);
+          for (uint32_t k = 0; k < XH_N; k++) {
+            st_sys(hm + 2 * k, xh_lo(v[k], tag));
+            st_sys(hm + 2 * k + 1, xh_hi(v[k], tag));
+          }
         } else {
 #pragma unroll
-          for (uint32_t k = 0; k < XH_N; k++) st_wt16(hm + 2 * k, v[k], tag);
+          for (uint32_t k = 0; k < XH_N; k++) st_wt16(hm + 2 * k, xh_lo(v[k], tag), xh_hi(v[k], tag));
         }
       }
       stamp(3, true);
@@ -4011,7 +4071,10 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       // holds them), then every granule is read once and its tag checked (re-read if late)
       while (true) {
         bool good = true;
-        if (lane < R) good = ld_gran16(S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS, S.xsys != 0).y == tag;
+        if (lane < R) {
+          const u64x2 x = ld_gran16(S.xin_hdr + ((size_t)buf * R + lane) * XH_WORDS, S.xsys != 0);
+          good = xh_ok(x.x, x.y, tag);
+        }
         if (__ballot(!good) == 0) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) {
           ok = false;
@@ -4023,9 +4086,9 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
         bool good = true;
         if (mine) {
           const u64x2 x = ld_gran16(h, S.xsys != 0), y = ld_gran16(h + 2, S.xsys != 0);
-          ga = x.x;
-          gb = y.x;
-          good = x.y == tag && (2 * jj + 1 >= XH_N || y.y == tag);
+          ga = xh_val(x.x, x.y);
+          gb = xh_val(y.x, y.y);
+          good = xh_ok(x.x, x.y, tag) && (2 * jj + 1 >= XH_N || xh_ok(y.x, y.y, tag));
         }
         if (__ballot(!good) == 0) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kXWaitTicks) ok = false;
@@ -4033,6 +4096,14 @@ __global__ __launch_bounds__(64, 2) void k_rounds_x(const XLaunch* __restrict__ 
       if (!ok) {
         if (lane == 0) atomicOr((unsigned int*)&C->overflow, OVF_TIMEOUT);
         return;
+      }
+      // System-scope acquire after the messages (peers on other GPUs): nothing this workgroup
+      // reads from here on (the bins and slots the message announces) may come from a cache
+      // older than the message. Those reads are sc0 sc1 loads of uncached memory already; the
+      // fence makes the ordering explicit rather than a property of the allocation.
+      if (kXFenceAcq && S.xsys) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       stamp(4, true);
       // the words into LDS (the event list's space, free between rounds): word k of sender q
@@ -4769,7 +4840,8 @@ int sync_ctrl_persist(sgn_ctx* ctx, uint32_t ep) {
   if (!ctx->h_mirror) return sync_ctrl(ctx);
   SGN_HIP(ctx, hipStreamSynchronize(ctx->stream));
   constexpr size_t NW = sizeof(Ctrl) / 8;
-  if (__atomic_load_n(&ctx->h_mirror[NW], __ATOMIC_ACQUIRE) != ep) return sync_ctrl(ctx);
+  if (__atomic_load_n(&ctx->h_mirror[NW], __ATOMIC_ACQUIRE) != ep || ctx->h_mirror[kMirrorWords - 1])
+    return sync_ctrl(ctx);
   std::memcpy(ctx->h_ctrl, ctx->h_mirror, sizeof(Ctrl));
   time_collect(ctx);
   return check_overflow(ctx);
@@ -5251,8 +5323,10 @@ int xpeer_upload(sgn_ctx* ctx) {
 // table in LDS, no per-packet trace) unless refused before or switched off (SGN_XPERSIST=0 or
 // SGN_PERSISTENT=0: per-round launches and the RCCL / local-copy exchange).
 bool xpersist_possible(sgn_ctx* ctx) {
-  static const bool off = (getenv("SGN_XPERSIST") && atoi(getenv("SGN_XPERSIST")) == 0) ||
-                          (getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0);
+  // (read per call, like the single-shard path's SGN_PERSISTENT: a test that changes either
+  // variable within one process must see it — ADVICE r5)
+  const bool off = (getenv("SGN_XPERSIST") && atoi(getenv("SGN_XPERSIST")) == 0) ||
+                   (getenv("SGN_PERSISTENT") && atoi(getenv("SGN_PERSISTENT")) == 0);
   return ctx->nranks > 1 && ctx->nranks <= XR_MAX && ctx->sim_ready && ctx->xin_mem && ctx->S.NB <= LDS_BSLAB &&
          !ctx->S.trace_on &&
          !ctx->x_off && !ctx->persist_off && !off;
@@ -5293,12 +5367,20 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
     sumG += c->S.G;
   }
   const uint64_t res = resident_wg(c0, rounds_x_fn(kind), lds) / std::max<uint32_t>(1, peers ? c0->x_share : 1);
-  if (!res || res < sh.size()) return 1;
+  // A refusal is decided here, from this GPU's LDS and residency alone (CAP may differ between
+  // shards after their re-layouts). A local group falls back at once; one shard per GPU must not,
+  // or its peers would launch and wait for it: it launches ONE workgroup that publishes "not
+  // resident" to every peer's census word, and every shard falls back together.
+  bool refuse = !res || res < sh.size();
+  // (test hook: this rank refuses as if its GPU could not hold the grid)
+  if (peers && getenv("SGN_XREFUSE_RANK") && atoi(getenv("SGN_XREFUSE_RANK")) == (int)c0->rank) refuse = true;
+  if (refuse && !peers) return 1;
   if (!c0->x_hxl) SGN_HIP(c0, hipHostMalloc(&c0->x_hxl, sizeof(XLaunch), 0));
   XLaunch& xl = *(XLaunch*)c0->x_hxl;
   std::memset(&xl, 0, sizeof(xl));
   xl.n_local = (uint32_t)sh.size();
   xl.peers_census = peers ? 1u : 0u;
+  xl.refuse = refuse ? 1u : 0u;
   xl.epoch = ++c0->x_epoch;
   uint32_t b = 0;
   const char* cap_env = getenv("SGN_PERSIST_GRID");
@@ -5307,6 +5389,7 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
     uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(c->S.G, res * c->S.G / sumG));
     if (cap_env) P = std::max<uint64_t>(1, std::min<uint64_t>(P, (uint64_t)atoi(cap_env)));
     P = std::min<uint64_t>(P, 64 * RB_CH);
+    if (refuse) P = 1;
     xl.base[i] = b;
     xl.S[i] = (std::remove_reference_t<decltype(xl.S[i])>)c->d_S;
     b += (uint32_t)P;
@@ -5316,7 +5399,8 @@ int x_launch(const std::vector<sgn_ctx*>& sh, bool peers, uint32_t n) {
   }
   xl.base[sh.size()] = b;
   xl.res_base = c0->res_base;  // (the census counts in the first shard's control block)
-  c0->res_base += b;
+  if (!refuse) c0->res_base += b;  // (a refused launch runs no census)
+  if (refuse) lds = 0;             // (its one workgroup leaves before touching the dynamic LDS)
   SGN_HIP(c0, hipMemcpyAsync(c0->d_xl, &xl, sizeof(XLaunch), hipMemcpyHostToDevice, c0->stream));
   time_begin(c0, K_EXECUTE);
   const dim3 grid(b), block(64);
@@ -5917,8 +6001,8 @@ int sgn_sim_init(sgn_ctx* ctx, const sgn_sim_config* cfg, const sgn_traffic* tr)
   SGN_HIP(ctx, hipMemcpy(S.ctrl, &c, sizeof(c), hipMemcpyHostToDevice));
   if (!ctx->h_ctrl) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_ctrl, sizeof(Ctrl), 0));
   static_assert(sizeof(Ctrl) % 8 == 0, "the control block's copy is written in u64 words");
-  if (!ctx->h_mirror) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_mirror, sizeof(Ctrl) + 8, 0));
-  std::memset(ctx->h_mirror, 0, sizeof(Ctrl) + 8);
+  if (!ctx->h_mirror) SGN_HIP(ctx, hipHostMalloc((void**)&ctx->h_mirror, kMirrorWords * 8, 0));
+  std::memset(ctx->h_mirror, 0, kMirrorWords * 8);
   {
     void* dm = nullptr;
     SGN_HIP(ctx, hipHostGetDevicePointer(&dm, ctx->h_mirror, 0));
@@ -6861,3 +6945,5 @@ void launch_import(sgn_ctx* ctx) {
   if (!ctx->capturing) ctx->kt[K_IMPORT].total++;
 }
 }  // namespace sgn
+
+uint64_t sgn::layout_sig_engine() { return kLayoutSig; }

@@ -1454,3 +1454,5 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
   ctx->hosts_ready = false;  // hosts map onto used nodes: re-register
   return 0;
 }
+
+uint64_t sgn::layout_sig_routes() { return kLayoutSig; }

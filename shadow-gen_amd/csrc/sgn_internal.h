@@ -118,9 +118,12 @@ struct Ctrl {
   uint64_t epoch;         // persistent rounds: round edges published (grid barrier)
   uint64_t prev_we;       // end of the last executed window (sgn_set_window's lower bound)
   uint64_t drain_n;       // drain records produced since the last sgn_drain
-  // persistent launch residency census (zeroed by the host before every k_rounds launch):
-  // workgroups that started, and the verdict (1 = whole grid resident, 2 = not: every
-  // workgroup left before touching simulation state; the host falls back to k_execute)
+  // persistent launch residency census. Never reset: res_arrive counts every workgroup of every
+  // persistent launch since sim_init (the host passes the count before a launch, sgn_ctx::res_base,
+  // and the census compares against it), and res_verdict carries the launch's epoch (epoch << 2 |
+  // verdict: 1 = whole grid resident, 2 = not, 3 = a peer shard not resident — every workgroup
+  // left before touching simulation state; the host falls back to per-round launches). A memset
+  // of either word breaks the census arithmetic.
   uint32_t res_arrive, res_verdict;
   // multi-shard exchange sizing: runs per peer the round's RCCL send/recv moves (set by the
   // host per batch; a slot holds up to xslot), 1 while a round is held because some shard
@@ -140,7 +143,10 @@ struct Ctrl {
   // has grown the pool; hold_need = the CoDel pages the held round may take
   uint64_t cal_occ;
   uint64_t spill_n;
-  uint32_t hold, pad_h;
+  uint32_t hold;
+  // one shard per GPU (k_rounds_x): the peers' census combined by this shard's deciding
+  // workgroup (epoch << 2 | verdict, as res_verdict); the shard's other workgroups read only this
+  uint32_t res_xverdict;
   uint64_t hold_need;
   uint64_t rnd_alloc, rnd_spill;  // per-round launches: the Outbox counters' target (unread)
 };
@@ -465,10 +471,21 @@ struct XPeer {
   SGN_GLB uint64_t* cen;
   SGN_GLB EvRec* bins[2];
 };
-// A message is 16 GRANULES of 16 bytes, {value, tag}, each written by one 16-byte store (the
-// receiver polls them and has the values in the same round trip; a 16-byte store is observed
-// untorn on gfx950, MI355X_MICROARCH.md): 256 bytes, XH_WORDS u64.
+// A message is 16 GRANULES of 16 bytes: granule k holds message word k as two TAGGED 8-byte
+// words {lo32 | tag32 << 32, hi32 | tag32 << 32} (xh_pack / xh_unpack), tag32 the low 32 bits
+// of the global round number + 1. Every 8-byte word carries the tag, so the receiver never
+// trusts more than one naturally aligned 8-byte store to arrive whole: across GPUs (xGMI) each
+// word is written by its own 8-byte system-scope atomic store, within one GPU a granule by one
+// 16-byte store. The receiver polls them and has the values in the same round trip: 256 bytes,
+// XH_WORDS u64.
 constexpr uint32_t XH_WORDS = 32;
+__host__ __device__ inline uint32_t xh_tag32(uint64_t tag) { return (uint32_t)tag; }
+__host__ __device__ inline uint64_t xh_lo(uint64_t v, uint64_t tag) { return (v & 0xFFFFFFFFull) | ((uint64_t)xh_tag32(tag) << 32); }
+__host__ __device__ inline uint64_t xh_hi(uint64_t v, uint64_t tag) { return (v >> 32) | ((uint64_t)xh_tag32(tag) << 32); }
+__host__ __device__ inline bool xh_ok(uint64_t lo, uint64_t hi, uint64_t tag) {
+  return (uint32_t)(lo >> 32) == xh_tag32(tag) && (uint32_t)(hi >> 32) == xh_tag32(tag);
+}
+__host__ __device__ inline uint64_t xh_val(uint64_t lo, uint64_t hi) { return (lo & 0xFFFFFFFFull) | (hi << 32); }
 enum : uint32_t {  // granule k holds message word k (its tag: the global round number + 1)
   XH_CNT = 0,    // runs the sender put in this receiver's slot this round (may exceed the slot)
   XH_MIN,        // the sender's min next event time, the runs it exported included (EMU_MAX: none)
@@ -496,7 +513,9 @@ struct XLaunch {
   uint32_t n_local;              // shards in this launch
   uint32_t peers_census;         // 1: one shard per GPU: the census is exchanged with the peers
   uint64_t epoch;                // launch number (census tags)
-  uint32_t res_base, pad_l;      // the first shard's census arrival count before this launch
+  uint32_t res_base;             // the first shard's census arrival count before this launch
+  uint32_t refuse;               // one shard per GPU: this GPU cannot hold a resident grid; the
+                                 // launch (one workgroup) only tells the peers "not resident"
   uint32_t base[XL_MAX + 1];     // workgroup range of local shard i: [base[i], base[i + 1])
   const SGN_CONST struct DevSim* S[XL_MAX];
 };
@@ -687,6 +706,21 @@ int comm_xmove_spills(sgn_ctx* ctx, const std::vector<std::vector<EvRec>>& out,
                       std::vector<EvRec>* in);  // runs past an inbox slot, to their shards (collective)
 int comm_allreduce_max_u64(sgn_ctx* ctx, uint64_t* host_v, size_t n);  // (host values, collective)
 int inject_runs(sgn_ctx* ctx, const std::vector<EvRec>& runs);      // engine.hip: into the calendar
+}  // namespace sgn
+
+// Every object of libsgn is compiled against this header. A library linked from objects built
+// against different versions of it (an experiment build linking stale objects: the round-5
+// segfault of libsgn_exp_rbrel.so) would read every struct at the wrong offsets.
+// Each translation unit reports the layout it was compiled with and sgn_create refuses a
+// mismatch (SGN_ESTATE) instead of running.
+constexpr uint64_t kLayoutSig = (uint64_t)sizeof(sgn_ctx) * 1000003ull ^ (uint64_t)sizeof(sgn::DevSim) * 7919ull ^
+                                (uint64_t)sizeof(sgn::Ctrl) * 131ull ^ (uint64_t)sizeof(sgn::HostRec) ^
+                                ((uint64_t)sizeof(sgn::XLaunch) << 40) ^ ((uint64_t)sizeof(sgn::XPeer) << 48);
+namespace sgn {
+uint64_t layout_sig_api();
+uint64_t layout_sig_engine();
+uint64_t layout_sig_routes();
+uint64_t layout_sig_comm();
 }  // namespace sgn
 
 #define SGN_HIP(ctx, call)                                   \

@@ -193,6 +193,21 @@ class KernelTimes(C.Structure):
 _lib = None
 
 
+def build_id() -> str:
+    """A fingerprint of the libsgn sources the shipped libsgn.so is built from (csrc/ and the
+    public headers): measurements filed under profiles/ carry it, and bench.py quotes a
+    measurement only for the build it was taken on."""
+    import hashlib
+    here = pathlib.Path(__file__).resolve().parent
+    files = sorted(list((here / "csrc").glob("*.hip")) + list((here / "csrc").glob("*.cpp")) +
+                   list((here / "csrc").glob("*.h")) + [here / "csrc" / "Makefile"] +
+                   list((here.parent / "include").glob("*.h")))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
 def load(path: str | os.PathLike | None = None) -> C.CDLL:
     """Load libsgn.so (raises if it was not built: the product has no fallback)."""
     global _lib

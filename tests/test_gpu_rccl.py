@@ -62,24 +62,45 @@ def test_rccl_two_ranks_one_gpu_match_unsharded(graph, xsz, port, workload, pool
         assert x["slot_runs"] > 64 and x["spills"] >= 1
 
 
-@pytest.mark.parametrize("workload,port", [("C", 29548), ("D", 29549)])
-def test_xpeer_two_processes_one_gpu_persistent(workload, port):
+@pytest.mark.parametrize("workload,port,launcher", [("C", 29548, False), ("D", 29549, True)])
+def test_xpeer_two_processes_one_gpu_persistent(workload, port, launcher):
     """The N-GPU persistent path itself (k_rounds_x with peer-mapped inboxes): two processes on
     device 0 (SGN_XPEER_SHARED=1 lets the IPC mapping accept a peer on the same GPU; each grid
     is sized for half the GPU), every round's runs stored straight into the other process's
-    inbox bins and slots, the messages and the residency census across processes — against
-    the unsharded run, bit for bit."""
+    inbox bins and slots, the messages (tagged 8-byte words, system-scope release and acquire)
+    and the residency census across processes — against the unsharded run, bit for bit.
+    Config C runs as the driver invokes the scaling bench without a launcher: `bench.py --gpus 2`
+    starts its two ranks itself and the line says n_gpus 2."""
     env = dict(os.environ, SGN_GRAPH="0", NCCL_DEBUG="WARN", TMPDIR="/tmp", SGN_XPEER_SHARED="1")
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--one-gpu", "--rounds-per-step", "70", "--workload", workload]
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] if launcher else [sys.executable, "-u"]
+    cmd += ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--one-gpu", "--rounds-per-step", "70",
+            "--workload", workload]
     if workload == "D":
         cmd += ["--hosts", "100000"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
     assert line["exchange"]["mode"] == 2 and line["exchange"]["persistent_launches"] > 0, line["exchange"]
     assert line["roofline"]["kernel"] == "k_rounds_x"
+    assert line["parity"] is True, line.get("parity_detail")
+
+
+def test_xpeer_refusal_on_one_gpu_falls_back_everywhere():
+    """a shard whose GPU cannot hold a resident k_rounds_x grid (forced on rank 1 by
+    SGN_XREFUSE_RANK) must not leave its peers waiting in a launch it never joins: it launches
+    one workgroup that tells them "not resident", and BOTH shards go on with per-round launches
+    and the RCCL exchange — bit-exact against the unsharded run."""
+    env = dict(os.environ, SGN_GRAPH="0", NCCL_DEBUG="WARN", TMPDIR="/tmp", SGN_XPEER_SHARED="1",
+               SGN_XREFUSE_RANK="1")
+    cmd = [sys.executable, "-u", "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--one-gpu",
+           "--rounds-per-step", "40", "--hosts", "20000"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["exchange"]["mode"] == 1, line["exchange"]
+    assert line["engine"]["persistent_fallbacks"] >= 1
     assert line["parity"] is True, line.get("parity_detail")
 
 

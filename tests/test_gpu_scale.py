@@ -122,14 +122,19 @@ def test_dynamic_runahead_slow_paths_calendar_horizon(oracle):
 def test_config_d_1m_hosts_bit_exact(oracle):
     """Config D (configs[3]) at its full size on one GPU: 1M hosts, every host sends 64 B to a
     uniform random peer every 1 ms (dense all-to-all; 15,625 host groups, so every workgroup
-    of the persistent round kernel serves ~9 groups per round). 120 rounds: ~120M sends and
-    the first deliveries of the ~100-ms paths."""
+    of the persistent round kernel serves ~9 groups per round). 320 rounds: ~320M sends, and
+    past the first deliveries of the longest paths the steady state — every host popping about
+    one packet a round through its CoDel queue and relay (host.rs:762-830, event_queue.rs:57-90)
+    — for the last ~200 rounds."""
     sys.path.insert(0, str(ROOT))
     import bench
     g, used, hosts, cfg, tr = bench.build_workload_d(1_000_000, 1000)
-    cfg.event_capacity = 257 * (1_000_000 // 64 + 1) * 192
-    o, c = _run_pair(oracle, g, used, hosts, cfg, tr, rounds=120)
+    cfg.event_capacity = 257 * (1_000_000 // 64 + 1) * 128
+    rounds = 320
+    o, c = _run_pair(oracle, g, used, hosts, cfg, tr, rounds=rounds)
     st = _compare(o, c, hosts.n)
-    assert st["packets_sent"] > 100_000_000 and st["packet_events_popped"] > 1_000_000
+    assert st["packets_sent"] > 300_000_000
+    # steady-state receive: most of the sends of the first ~200 rounds have been popped
+    assert st["packet_events_popped"] > 150_000_000, st["packet_events_popped"]
     info = c.engine_info()
     assert info["host_groups"] == 15_625 and info["persistent_fallbacks"] == 0

@@ -222,3 +222,32 @@ def test_config_c_eight_shards_one_launch(oracle):
     kt1, kt8 = one.kernel_times()["k_rounds"], shards[0].kernel_times()["k_rounds_x"]
     print(f"per-round kernel time: unsharded {kt1[1] / rounds * 1e3:.2f} us, 8 shards in one launch "
           f"{kt8[1] / rounds * 1e3:.2f} us (grid {[c.engine_info()['persistent_x_grid'] for c in shards]})")
+
+
+def test_config_d_1m_eight_shards_one_launch():
+    """Config D as bench.py builds it (1M hosts, every host sending 64 B to a uniform random peer
+    every 1 ms: 7/8 of all runs cross shards) as 8 shards of 125k hosts in ONE k_rounds_x launch
+    per batch — the round-edge exchange BASELINE's config #4 stresses, rehearsed on one GPU —
+    for 320 rounds, past the first deliveries into the steady state where every host pops about
+    one imported packet a round (worker.rs:603-613 is the cross-host push the inbox replaces).
+    Bit for bit against one unsharded run (itself checked against the oracle at the same size,
+    test_gpu_scale.py::test_config_d_1m_hosts_bit_exact); the inboxes grow under this load."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    n, k, rounds = 1_000_000, 8, 320
+    g, used, hosts, cfg, tr = bench.build_workload_d(n, 1000)
+    cfg.event_capacity = 257 * (n // 64 + 1) * 128
+    one = unsharded((g, used, hosts, cfg, tr), rounds=rounds)
+    s1 = one.stats()
+    assert s1["rounds"] == rounds
+    shards, _, done = local_group((g, used, hosts, cfg, tr), k, slot=1 << 13, rounds=rounds,
+                                  event_capacity=257 * (-(-n // k) // 64 + 1) * 128)
+    assert done == rounds
+    info = [c.engine_info() for c in shards]
+    assert all(i["exchange_mode"] == 2 for i in info), info[0]
+    compare(one, shards, n)
+    assert s1["packets_sent"] > 300_000_000 and s1["packet_events_popped"] > 150_000_000
+    kt1, kt8 = one.kernel_times()["k_rounds"], shards[0].kernel_times()["k_rounds_x"]
+    print(f"config D per-round kernel time: unsharded {kt1[1] / rounds * 1e3:.1f} us, 8 shards in one launch "
+          f"{kt8[1] / rounds * 1e3:.1f} us; inbox slot {info[0]['inbox_slot_runs']} runs, grown "
+          f"{info[0]['inbox_grows']}x, hwm {info[0]['exchange_hwm_runs']}")

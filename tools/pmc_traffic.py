@@ -8,7 +8,11 @@ WRITE_SIZE (KB) is taken as is; the uncorrected sum is kept beside it (the engin
 Prints one JSON entry keyed by the invocation (tools/traffic_merge.py files it)."""
 import csv
 import json
+import pathlib
 import sys
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent.parent / "shadow-gen_amd"))
+import sgn  # noqa: E402
 
 d, workload, steps, warmup = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 hosts = {"B": 10_000, "C": 100_000, "D": 1_000_000}[workload]
@@ -42,4 +46,6 @@ print(json.dumps({
     "workload": {"name": workload, "hosts_per_gpu": hosts, "graph_nodes": 1000, "rounds_per_launch": 100,
                  "n_gpus": 1, "steps": steps, "warmup": warmup},
     "bench_args": f"--workload {workload} --steps {steps} --warmup {warmup} (the timed launches of that invocation)",
+    # the libsgn sources this was measured on: bench.py quotes the entry for that build only
+    "build": sgn.build_id(),
 }, indent=1))
