@@ -419,14 +419,6 @@ constexpr uint32_t kTrainWait = SGN_TRAIN_WAIT;
 #define SGN_FWD_WAIT_LANES 24
 #endif
 constexpr uint32_t kFwdWaitLanes = SGN_FWD_WAIT_LANES;
-// Handler grouping (HostExec::run): every iteration of a wave's event loop runs ONE kind of
-// handler — the one most of the wave's looping lanes are at — and the other lanes wait. Bit per
-// traffic kind (1 PERIODIC, 2 TGEN, 4 EXTERNAL); a grouped kind does not use the waits above.
-#ifndef SGN_GROUP
-#define SGN_GROUP 0
-#endif
-template <uint32_t kApp>
-constexpr bool kGroup = (SGN_GROUP & (kApp == SGN_TRAFFIC_PERIODIC ? 1 : kApp == SGN_TRAFFIC_TGEN ? 2 : 4)) != 0;
 template <uint32_t kApp>
 #ifndef SGN_OBOX_PERIODIC
 #define SGN_OBOX_PERIODIC 24
@@ -2051,27 +2043,6 @@ struct HostExec {
         (void)tnow;
       }
 #endif
-      // Handlers side by side (kGroup): the lane's next step is of one of four kinds — a
-      // forwarding step of relay_inet_out (its task running, or its slot next), a packet run
-      // popped (with the relay_inet_in task it may chain into), relay_inet_in's task, the app's
-      // timer. The wave runs the kind most of its looping lanes are at; the others wait for a
-      // later iteration. A host's own sequence does not depend on when its lane runs (other
-      // lanes are other hosts; nothing a lane reads is written by another lane's handlers in
-      // this window), the argument the train and forwarding waits below rest on too.
-      if constexpr (kGroup<kApp>) {
-        const bool cont = (fl & F_RO_CONT) != 0;
-        const bool popn = !cont && pi < s1 && pt <= lt;
-        if (!cont && !popn && lt >= until) break;
-        const uint32_t kind = (cont || (!popn && ls == 0)) ? 0u : popn ? 1u : (uint32_t)ls + 1u;  // ro pop ri app
-        const uint32_t n0 = (uint32_t)__popcll(__ballot(kind == 0)), n1 = (uint32_t)__popcll(__ballot(kind == 1)),
-                       n2 = (uint32_t)__popcll(__ballot(kind == 2)), n3 = (uint32_t)__popcll(__ballot(kind == 3));
-        // (ties: pop, then relay_inet_in, the app, forwarding — the order the handlers chain in)
-        uint32_t kb = 1, nb = n1;
-        if (n2 > nb) { kb = 2; nb = n2; }
-        if (n3 > nb) { kb = 3; nb = n3; }
-        if (n0 > nb) kb = 0;
-        if (kind != kb) continue;
-      }
       // inside relay_inet_out's forwarding task: its next step (the one call site of
       // forward_out_step below), no other event of the host
       if (!(fl & F_RO_CONT)) {
@@ -2138,7 +2109,7 @@ struct HostExec {
       // pass per lane (config C's slowest waves ran their servers' draw loops 3 to 7 times
       // over, diag build). Waiting changes nothing of the host's own sequence: `now` is fixed
       // inside the forwarding task, and other lanes are other hosts.
-      if constexpr (kApp == SGN_TRAFFIC_TGEN && !kGroup<kApp>) {
+      if constexpr (kApp == SGN_TRAFFIC_TGEN) {
         const bool lng = !(fl & F_RO_NEXT) && fq_len > 0 && fifo_head().count > kTrainWait;
         if (lng && __ballot(1) != act) continue;
       }
@@ -2149,7 +2120,7 @@ struct HostExec {
       // the trains: `now` is fixed inside the forwarding task. Few lanes (config B's waves of 16
       // hosts, 2-6 busy) lose more in extra loop trips than they share (same-box A/B: D +6.4 %,
       // B -1.0 % when every wave waits).
-      if constexpr (kApp == SGN_TRAFFIC_PERIODIC && !kGroup<kApp>) {
+      if constexpr (kApp == SGN_TRAFFIC_PERIODIC) {
         if (__popcll(act) >= kFwdWaitLanes && __ballot(1) != act) continue;
       }
       forward_out_step();
