@@ -68,6 +68,8 @@ enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD,
        DGT_HDLD, DGT_FHLD, DGT_RTLD, DGT_SVLD, DGT_SLAB,
        DGT_DRAWS,   // (counts, not cycles) loss draws of this lane's trains
        DGT_RENTRY,  // ... and the wave's entries into the draw loop (its lowest lane counts)
+       DGT_LLANE,   // (counts) this lane's entries with a long train (more than kTrainWait draws)
+       DGT_LENTRY,  // ... and the wave's entries in which some lane draws a long train
        DGT_N };
 #ifdef SGN_DIAG
 #define DGT_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
@@ -1600,6 +1602,11 @@ struct HostExec {
 #ifdef SGN_DIAG
     dgt[DGT_DRAWS] += n;
     if ((uint32_t)(__ffsll((long long)__ballot(1)) - 1) == (threadIdx.x & 63)) dgt[DGT_RENTRY] += 1;
+    {
+      const uint64_t lb = __ballot(n > kTrainWait);
+      if (n > kTrainWait) dgt[DGT_LLANE] += 1;
+      if (lb && (uint32_t)(__ffsll((long long)lb) - 1) == (threadIdx.x & 63)) dgt[DGT_LENTRY] += 1;
+    }
 #endif
 #ifdef SGN_EXP_NORNG
     if (true) {

@@ -48,7 +48,8 @@ for r in range(3):
                   "ld_route", "ld_server", "slab_atomic", "draws(all lanes)", "draw-loop entries"]
             print("      wave cycles in: " + " ".join(f"{n}={s[i, 80 + k]}" for k, n in enumerate(tn)))
             if s[i, 92]:
-                print(f"      rngloop cycles per entry {s[i, 84] / s[i, 92]:.0f}, per draw of the wave's lanes {s[i, 84] / max(1, s[i, 91]):.1f}")
+                print(f"      rngloop cycles per entry {s[i, 84] / s[i, 92]:.0f}, per draw of the wave's lanes {s[i, 84] / max(1, s[i, 91]):.1f}"
+                      f"; long-train (lane, entry) pairs {s[i, 93]} in {s[i, 94]} wave entries")
             sec = s[i, 81] + s[i, 82] + s[i, 83] + s[i, 85]
             print(f"      load={s[i, 32]} run={s[i, 33]} store={s[i, 34]} run-outside-handlers={s[i, 33] - sec}"
                   f" iterations={s[i, 35]}")
