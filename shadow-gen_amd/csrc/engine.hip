@@ -70,6 +70,7 @@ enum { DGT_SEND = 0, DGT_FWDOUT, DGT_FWDIN, DGT_POP, DGT_APP, DGT_LOAD,
        DGT_RENTRY,  // ... and the wave's entries into the draw loop (its lowest lane counts)
        DGT_LLANE,   // (counts) this lane's entries with a long train (more than kTrainWait draws)
        DGT_LENTRY,  // ... and the wave's entries in which some lane draws a long train
+       DGT_CQALLOC, DGT_CQFREE, DGT_TBRM, DGT_DELIV,  // CoDel page alloc / free, token bucket, delivery
        DGT_N };
 #ifdef SGN_DIAG
 #define DGT_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
@@ -1022,6 +1023,13 @@ struct HostExec {
   // ---- TokenBucket::comforming_remove (network/relay/token_bucket.rs:65-154) ----
   template <int W>
   __device__ __forceinline__ bool tb_remove(uint64_t dec, uint64_t* dur) {
+    DGT_BEGIN(tt);
+    const bool ok = tb_remove_<W>(dec, dur);
+    DGT_END(DGT_TBRM, tt);
+    return ok;
+  }
+  template <int W>
+  __device__ __forceinline__ bool tb_remove_(uint64_t dec, uint64_t* dur) {
     uint64_t& bal = W == 0 ? tbb0 : tbb1;
     uint64_t& last = W == 0 ? tbl0 : tbl1;
     const uint64_t interval = 1000000ULL;  // relay/mod.rs:279
@@ -1148,15 +1156,23 @@ struct HostExec {
   // a page from the pool: the free ring's next entry, if it was freed before this round
   // (the entries of the current round are still being written by other waves)
   __device__ __forceinline__ uint32_t cq_alloc_page() {
+    DGT_BEGIN(ta);
     const uint64_t i = __hip_atomic_fetch_add(&C->pg_alloc, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cnt_add(ob->pg_allocd, 1);
     if (i >= ob->pg_avail) return NO_HOST;
-    return ld_dev(&S.cq_free[i % S.cq_pages]);
+    const uint32_t pg = ld_dev(&S.cq_free[i % S.cq_pages]);
+#ifdef SGN_DIAG
+    DGT_WAIT();
+    DGT_END(DGT_CQALLOC, ta);
+#endif
+    return pg;
   }
   __device__ __forceinline__ void cq_free_page(uint32_t pg) {
+    DGT_BEGIN(tf);
     const uint64_t j = __hip_atomic_fetch_add(&C->pg_tail, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     st_dev(&S.cq_free[j % S.cq_pages], pg);
     cnt_add(ob->pg_freed, 1);
+    DGT_END(DGT_CQFREE, tf);
   }
   // the head run left the queue: next run, next page (the old one back to the pool), or an
   // empty queue that keeps its page from the start
@@ -2983,7 +2999,7 @@ __device__ __forceinline__ void exec_group(const DevSim& S, uint32_t g, uint64_t
     for (int i = 0; i < DGT_N; i++) {
       const uint32_t v = loaded ? ex.dgt[i] : 0u;
       const uint32_t vs = wave_sum_u32(v);  // the wave's time in section i
-      if (lane == 0) st[80 + i] = vs;
+      if (lane == 0) st[i < 16 ? 80 + i : 10 + (i - 16)] = vs;  // (sections past 15: words 10..)
     }
     if (lane == 0) {
       st[32] = w_load;

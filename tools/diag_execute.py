@@ -52,7 +52,7 @@ for r in range(3):
                       f"; long-train (lane, entry) pairs {s[i, 93]} in {s[i, 94]} wave entries")
             sec = s[i, 81] + s[i, 82] + s[i, 83] + s[i, 85]
             print(f"      load={s[i, 32]} run={s[i, 33]} store={s[i, 34]} run-outside-handlers={s[i, 33] - sec}"
-                  f" iterations={s[i, 35]}")
+                  f" iterations={s[i, 35]} | cq_alloc={s[i, 10]} cq_free={s[i, 11]} tb_remove={s[i, 12]}")
     print(f"   median gather={np.median(tg):.0f} exec={np.median(tx):.0f}")
     if s[:, 80:91].any():
         tn = ["send", "fwdout", "fwdin", "pop", "rngloop", "app", "ld_codelhead", "ld_fifohead",
