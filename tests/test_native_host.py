@@ -21,6 +21,19 @@ def test_udiv64_matches_division(tmp_path):
     assert " 0 bad" in out.stdout
 
 
+def test_message_words_carry_the_tag_in_every_8_bytes(tmp_path):
+    """k_rounds_x's round-edge message encoding: a granule is accepted only
+    when both of its 8-byte words carry this round's tag, and then decodes to the value."""
+    exe = tmp_path / "xh_check"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17",
+                    "-I", str(ROOT / "include"), "-I", str(ROOT / "shadow-gen_amd" / "csrc"),
+                    str(ROOT / "tests" / "native" / "xh_check.cpp"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert " 0 bad" in out.stdout
+
+
 def _kernel_meta(so):
     """AMDGPU kernel metadata (per kernel: private segment, VGPRs, spills) of every gfx950
     code object bundled into a built library."""
