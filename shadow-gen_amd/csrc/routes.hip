@@ -553,7 +553,11 @@ __global__ __launch_bounds__(512) void loss_sweep(const uint32_t* D32, uint32_t 
 // broadcast read kept in registers, and the lanes' heads v are consecutive (conflict-free
 // reads of d[s][v]); a workgroup sweeps a range of tails. The test is d[s][v] - d[s][u] == l
 // with d[s][v] >= d[s][u] (u32; an arc of 2^32 - 1 ns or more is never tight).
-constexpr uint32_t SWEEP_HCAP = 256;  // filter hits one wave lists per 256-arc step (at most 256)
+#ifndef SGN_SWEEP_Q
+#define SGN_SWEEP_Q 16
+#endif
+constexpr uint32_t kSweepQ = SGN_SWEEP_Q;  // arcs per lane in flight per step
+constexpr uint32_t SWEEP_HCAP = 256;       // filter hits a wave lists before checking them exactly
 template <int S>
 __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc,
                                                       uint32_t U, uint32_t V, const uint32_t* rowptr,
@@ -598,21 +602,40 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
     }
 #pragma unroll
     for (int k = 0; k < S; k++) ndu[k] = 0u - du[k];
-    // four arcs per lane in flight (e, e + 64, e + 128, e + 192): the sweep waits on the arc
-    // loads (PMC, round 4: 84 % of its wave cycles waiting with one arc per lane)
+    // kSweepQ arcs per lane in flight (e, e + 64, ...): the sweep waits on the arc loads (PMC,
+    // round 4: 84 % of its wave cycles waiting with one arc per lane)
     const uint32_t e_beg = rowptr[u], e1 = rowptr[u + 1];
-    for (uint32_t e0 = e_beg + lane; e0 - lane < e1; e0 += 256) {
-      uint32_t uv[4], l[4];
+    for (uint32_t e0 = e_beg + lane; e0 - lane < e1; e0 += 64 * kSweepQ) {
+      uint32_t uv[kSweepQ], l[kSweepQ];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {  // (clamped, unconditional loads: all eight in flight at once;
+      for (int q = 0; q < (int)kSweepQ; q++) {  // (clamped, unconditional loads: all in flight at once;
         // 32-bit byte offsets from the scalar bases)
         const uint32_t off = min(e0 + 64 * q, e1 - 1) * 4u;
         uv[q] = *(const uint32_t*)((const char*)auv + off);
         l[q] = *(const uint32_t*)((const char*)al32 + off);
       }
       uint32_t nh = 0;  // (wave-uniform)
+      // the exact test of the listed hits (it also drops the clamped lanes past the tail's last
+      // arc, and arcs of 2^32 - 1 ns or more)
+      auto check = [&](uint32_t n) {
+        for (uint32_t h = lane; h < n; h += 64) {
+          const uint32_t e = hits[h];
+          if (e >= e1) continue;
+          const uint32_t lq = al32[e];
+          if (lq == SQ_INF) continue;
+          const uint32_t v = auv[e] >> 16;
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
+          for (int k = 0; k < S; k++) {
+            const uint32_t bk = row[(k >> 2) * Vp * 4 + v * 4 + (k & 3)];
+            if (du[k] == SQ_INF || bk < du[k] || bk - du[k] != lq) continue;
+            const uint32_t src = g0 + k;
+            const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+            if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+          }
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < (int)kSweepQ; q++) {
         const uint32_t v = uv[q] >> 16;
         uint32_t b[S];
 #pragma unroll
@@ -635,27 +658,13 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
         if (m) {
           if (acc == 0) hits[nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = e0 + 64 * q;
           nh += (uint32_t)__popcll(m);
-        }
-      }
-      if (nh) {
-        // the exact test (it also drops the clamped lanes past the tail's last arc, and arcs of
-        // 2^32 - 1 ns or more)
-        for (uint32_t h = lane; h < nh; h += 64) {
-          const uint32_t e = hits[h];
-          if (e >= e1) continue;
-          const uint32_t lq = al32[e];
-          if (lq == SQ_INF) continue;
-          const uint32_t v = auv[e] >> 16;
-#pragma unroll
-          for (int k = 0; k < S; k++) {
-            const uint32_t bk = row[(k >> 2) * Vp * 4 + v * 4 + (k & 3)];
-            if (du[k] == SQ_INF || bk < du[k] || bk - du[k] != lq) continue;
-            const uint32_t src = g0 + k;
-            const uint32_t pos = atomicAdd(&tcnt[src], 1u);
-            if (pos < capg) tlist[(uint64_t)src * capg + pos] = e;
+          if (nh > SWEEP_HCAP - 64) {  // (a full list is checked now: room for the next arc's 64)
+            check(nh);
+            nh = 0;
           }
         }
       }
+      if (nh) check(nh);
     }
   }
 }
