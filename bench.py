@@ -337,7 +337,10 @@ def apsp_roofline(apsp, V, U):
     panels, 8 V^3 / T; per-source relaxation (sparse graphs): every sweep reads the arc list
     (12 B per arc) for every used source, 12 U E sweeps.
     loss — multi-source sweep (kS sources per arc load): 8 B per arc per source group plus
-    the rows, 8 E ceil(U / kS) + 4 U V; one-source pass: 12 B per arc per source, 12 U E.
+    the rows, 8 E ceil(U / kS) + 4 U V; its dense form (loss_dense: a lane per head, the tails'
+    negated latencies from a V x V matrix, kS sources per workgroup): 4 B per (tail, head) per
+    source group plus the rows, 4 V^2 ceil(U / kS) + 4 U V; one-source pass: 12 B per arc per
+    source, 12 U E.
     The arc list is re-read from L2 / MALL, so these are traffic above HBM, not HBM bytes."""
     T = apsp["tile"] or 64
     E = apsp["n_tight_edges"]
@@ -348,7 +351,13 @@ def apsp_roofline(apsp, V, U):
     else:
         b_lat = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
     k = apsp.get("loss_multi", 0)
-    b_loss = 8.0 * E * -(-U // k) + 4.0 * U * V if k else 12.0 * U * E
+    dense = bool(apsp.get("loss_dense", 0))
+    if not k:
+        b_loss = 12.0 * U * E
+    elif dense:
+        b_loss = 4.0 * V * V * -(-U // k) + 4.0 * U * V
+    else:
+        b_loss = 8.0 * E * -(-U // k) + 4.0 * U * V
     # Each phase's `frac` is the fraction of the bound it meets (`bound`): 32-bit integer VALU
     # issue for the squaring passes and the multi-source sweep, HBM for the other forms. The
     # HBM fraction is always given as `hbm_frac` (against HBM_PEAK_GBS) and the loss phase's
@@ -380,7 +389,8 @@ def apsp_roofline(apsp, V, U):
     # the bound these two forms actually meet: 32-bit integer VALU work. Squaring: per pass every
     # (i, k, j) relaxation is one saturating add and half a v_min3 (1.5 lane-ops, V^3 per pass,
     # the padded V); the multi-source sweep: every (source, arc) pair is one v_add3 and half a
-    # v_min3 (1.5 lane-ops, U x E pairs)
+    # v_min3 (1.5 lane-ops, U x E pairs; the dense form also tests the absent arcs of its V x V
+    # matrix, which are not counted: the work priced is the same U x E pairs)
     Vp = -(-V // 64) * 64
 
     def valu_bound(ph, ops, ms_):
@@ -414,8 +424,10 @@ def apsp_roofline(apsp, V, U):
     out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
                    ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else
                     "u32 min-plus squaring, all passes in one launch (sq_run)"),
-                   "loss": f"{k}-source sweep (tail-ordered arcs, branch-free add3/min3 filter) + LDS fold" if k
-                   else "one-source arc sweep + LDS fold"}
+                   "loss": (f"dense {k}-source sweep (a lane per head, negated latency matrix, scalar -d[s][u], "
+                            "add3/min3 filter; a source's own out-arcs apart) + LDS fold") if k and dense else
+                           (f"{k}-source sweep (tail-ordered arcs, branch-free add3/min3 filter) + LDS fold" if k
+                            else "one-source arc sweep + LDS fold")}
     out["note"] = ("frac is the fraction of each phase's bound: the squaring passes, the per-source "
                    "relaxation and the multi-source sweep are bound by 32-bit integer VALU issue (lane-ops over the phase's time, each "
                    "phase timed whole including its launches and barrier); hbm_frac (HBM bytes / 8 TB/s) "

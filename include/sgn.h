@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SGN_ABI_VERSION 9
+#define SGN_ABI_VERSION 10
 
 /* emulated_time.rs:27-40 */
 #define SGN_SIMULATION_START 946684800000000000ULL
@@ -127,6 +127,10 @@ typedef struct sgn_routes_timing {
                               computes its block of used sources and the blocks are exchanged
                               over RCCL, so every shard ends with the whole table), else 1 */
   uint32_t shard_sources;  /* used sources whose rows this process computed */
+  uint32_t loss_dense;     /* ABI 10: 1 when the sweep ran in its dense form (at least half of all
+                              arcs, no parallel arcs: a (tail, head) matrix of arcs, loss_multi
+                              sources per workgroup); 0: the CSR / arc-list sweep or none */
+  uint32_t reserved;
 } sgn_routes_timing;
 int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
 

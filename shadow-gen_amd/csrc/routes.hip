@@ -669,6 +669,246 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
   }
 }
 
+// Dense graphs (at least half of all arcs present, no parallel arcs; round 6): the same tight
+// test as a dense sweep over (source, tail, head) with nothing from LDS in its inner loop. In
+// loss_sweep_csr every (source, arc) pair reads d[s][v] from LDS (4 B a pair: the LDS return path
+// and the VALU were both near their limits). Here a lane owns one head v and keeps the S
+// sources' d[s][v] in registers for the whole launch; a wave walks a range of tails u, and per
+// tail the lane loads one word, the arc's latency L[u][v] from the dense latency matrix
+// (coalesced over the wave's heads), while the S values -d[s][u] are scalar loads (NDT: the used
+// sources' distance columns, transposed and negated). Per pair: one v_add3_u32 and half a
+// v_min3. Arcs are looked up through a dense (tail, head) -> arc index matrix, so the tight
+// lists hold the same arc indices as the CSR form, and the fold reads them alike.
+// A source's own out-arcs (tail u = s) are left to loss_self_tails: on graphs whose edges are
+// their own shortest paths (config C's Tor graph) they are nearly all of the tight pairs, and
+// in the sweep they would fill every lane's hit list at the few tails that are sources.
+constexpr uint32_t kDenseQ = 8;  // tails whose latency loads are in flight at once
+// filter hits a wave lists before checking them exactly: room for one more batch of kDenseQ tails
+// after any fill below the threshold, so the list is checked once per batch at most (one copy
+// of the check in the code: a copy per unrolled tail made the kernel 19 k lines)
+constexpr uint32_t DENSE_HCAP = 2 * 64 * kDenseQ;  // (kDenseQ hit lists per batch: Q tails x H heads)
+
+// NL32[u][v] = minus the arc's u32 latency (1 = -SQ_INF: no arc; the filter's operand as it is
+// used), EI[u][v] = its index (no parallel arcs)
+__global__ void dense_arcs(const uint32_t* auv, const uint32_t* al32, uint32_t E2, uint32_t Vp, uint32_t* NL32,
+                           uint32_t* EI) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
+    const uint32_t uv = auv[e];
+    const size_t i = (size_t)(uv & 0xFFFFu) * Vp + (uv >> 16);
+    NL32[i] = 0u - al32[e];
+    EI[i] = e;
+  }
+}
+
+// NDT[u][j] = -d[usrc[j]][u] (u32), through a 64 x 64 LDS tile (rows of D32 read along u, NDT
+// written along j). 1 (= -SQ_INF: the filter never passes it, the exact test rejects it) for the
+// padding sources j >= ns and for u = usrc[j] (loss_self_tails takes those arcs).
+__global__ __launch_bounds__(256) void ndt_build(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t ns,
+                                                 uint32_t* NDT, uint32_t Up) {
+  __shared__ uint32_t tile[64][65];
+  const uint32_t j0 = blockIdx.x * 64, u0 = blockIdx.y * 64, c = threadIdx.x & 63;
+  for (uint32_t jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+    const uint32_t j = j0 + jj, u = u0 + c;
+    uint32_t x = 1u;
+    if (j < ns && u < Vp) {
+      const uint32_t s = usrc[j];
+      if (u != s) x = 0u - D32[(size_t)s * Vp + u];
+    }
+    tile[jj][c] = x;
+  }
+  __syncthreads();
+  for (uint32_t uu = threadIdx.x >> 6; uu < 64; uu += 4) {
+    const uint32_t u = u0 + uu, j = j0 + c;
+    if (u < Vp && j < Up) NDT[(size_t)u * Up + j] = tile[c][uu];
+  }
+}
+
+// The tight arcs out of each source itself (tail u = s): one workgroup per source, appends
+// counted once per wave
+__global__ __launch_bounds__(256) void loss_self_tails(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t V,
+                                                       const uint32_t* NL32, const uint32_t* EI, uint32_t capg,
+                                                       uint32_t* tcnt, uint32_t* tlist) {
+  const uint32_t j = blockIdx.x, s = usrc[j], lane = threadIdx.x & 63;
+  const uint32_t du = D32[(size_t)s * Vp + s];
+  for (uint32_t v0 = 0; v0 < V; v0 += 256) {
+    const uint32_t v = v0 + threadIdx.x;
+    bool tight = false;
+    if (v < V && du != SQ_INF) {
+      const uint32_t lq = 0u - NL32[(size_t)s * Vp + v], bk = D32[(size_t)s * Vp + v];
+      tight = lq != SQ_INF && bk >= du && bk - du == lq;
+    }
+    const uint64_t m = __ballot(tight);
+    if (!m) continue;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&tcnt[j], (uint32_t)__popcll(m));
+    base = __shfl(base, (int)first, 64);
+    if (tight) {
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pos < capg) tlist[(uint64_t)j * capg + pos] = EI[(size_t)s * Vp + v];
+    }
+  }
+}
+
+// 16 scalar words in one s_load_dwordx16 issued now and waited for later (swait16): the compiler
+// waits for its own scalar loads at their first use with lgkmcnt(0), which exposed the whole
+// latency at every tail (the first build ran at 60 % of VALU issue, PMC)
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
+  u32x16 r;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r) : "s"(p));
+  return r;
+}
+
+// grid (ceil(ns / S), ceil(Vp / (256 H)), tail ranges); 256 threads, thread t owns the H heads
+// v0 + t + 256 h. The filter folds the sources in groups of 8, so a hit names the groups to test
+// exactly. Per tail the S values -d[s][u] are loaded one tail ahead (asm: issued before the
+// tail's work, waited for after it) and serve H heads per lane.
+template <int S, int H>
+__global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restrict__ D32, uint32_t Vp,
+                                                        const uint32_t* __restrict__ usrc, uint32_t U, uint32_t V,
+                                                        const uint32_t* __restrict__ NDT, uint32_t Up,
+                                                        const uint32_t* __restrict__ NL32,
+                                                        const uint32_t* __restrict__ EI, uint32_t capg,
+                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tlist) {
+  static_assert(S % 16 == 0 && S <= 32, "sources per tail come in 16-word scalar loads");
+  static_assert(H == 1 || H == 2, "heads per lane");
+  constexpr int NG = S / 16, NV = S / 16;  // filter groups of 16 sources = the scalar loads
+  constexpr uint32_t Q = kDenseQ / H;  // tails per batch (Q * H latency loads in flight)
+  __shared__ uint32_t hits[4][DENSE_HCAP];
+  __shared__ uint32_t srow[S];  // the sources' row offsets in D32 (for the exact test)
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // XCD-aware order: blocks id, id + 8, ... share an XCD (MI355X_MICROARCH.md), so each XCD takes a
+  // contiguous run of (source tile, head block, tail range) with the source tile fastest — the
+  // tiles that read one block of NL32 run together on one XCD and find it in that XCD's L2
+  const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
+  const uint32_t id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const uint32_t xq = nblk >> 3, xr = nblk & 7, xc = id & 7;
+  const uint32_t lin = xc * xq + min(xc, xr) + (id >> 3);
+  const uint32_t bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
+  const uint32_t g0 = bx * S, v0 = by * 256 * H;
+  uint32_t vc[H];  // (heads past V: the exact test drops them)
+#pragma unroll
+  for (int h = 0; h < H; h++) vc[h] = min(v0 + t + 256 * h, Vp - 1);
+  if (t < S) srow[t] = usrc[g0 + t < U ? g0 + t : 0] * Vp;
+  __syncthreads();
+  uint32_t dv[H][S];
+#pragma unroll
+  for (int k = 0; k < S; k++)
+#pragma unroll
+    for (int h = 0; h < H; h++) dv[h][k] = g0 + k < U ? D32[srow[k] + vc[h]] : SQ_INF;
+  const uint32_t u0 = (uint32_t)((uint64_t)V * bz / gridDim.z);
+  const uint32_t u1 = (uint32_t)((uint64_t)V * (bz + 1) / gridDim.z);
+  // the exact test of the listed hits, lane-parallel; an entry is u << 13 | groups << 9 | head
+  // offset, and a group's 16 values of d[s][u] and d[s][v] are loaded at once
+  auto check = [&](uint32_t n) {
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t ent = hits[wave][i], u = ent >> 13, gm = (ent >> 9) & 15u, v = v0 + (ent & 511u);
+      if (v >= V) continue;
+      const uint32_t lq = 0u - NL32[(size_t)u * Vp + v];
+      if (lq == SQ_INF) continue;  // no arc (or one of 2^32 - 1 ns or more: never tight)
+      const uint32_t* nd = NDT + (size_t)u * Up + g0;
+      for (int gi = 0; gi < NG; gi++) {
+        if (!((gm >> gi) & 1u)) continue;
+        uint32_t nk[16], bk[16];
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+          const uint4 x = *(const uint4*)(nd + 16 * gi + k);
+          nk[k] = x.x;
+          nk[k + 1] = x.y;
+          nk[k + 2] = x.z;
+          nk[k + 3] = x.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) bk[k] = D32[srow[16 * gi + k] + v];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const uint32_t src = g0 + 16 * gi + k, du = 0u - nk[k];
+          if (src >= U || du == SQ_INF || bk[k] < du || bk[k] - du != lq) continue;
+          const uint32_t pos = atomicAdd(&tcnt[src], 1u);
+          if (pos < capg) tlist[(uint64_t)src * capg + pos] = EI[(size_t)u * Vp + v];
+        }
+      }
+    }
+  };
+  // (32-bit byte offsets from the scalar base: Vp <= 8192 keeps NL32 under 4 GB)
+  auto lrow = [&](uint32_t u, int h) {
+    return *(const uint32_t*)((const char*)NL32 + (min(u, u1 - 1) * Vp + vc[h]) * 4u);
+  };
+  auto ndrow = [&](uint32_t u) { return NDT + (size_t)min(u, u1 - 1) * Up + g0; };
+  uint32_t lc[Q][H];
+#pragma unroll
+  for (int q = 0; q < (int)Q; q++)
+#pragma unroll
+    for (int h = 0; h < H; h++) lc[q][h] = lrow(u0 + q, h);
+  u32x16 cur[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) cur[i] = sload16(ndrow(u0) + 16 * i);
+  if constexpr (NV == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(cur[0]));
+  else asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(cur[0]), "+s"(cur[NV - 1]));
+  uint32_t nh = 0;  // (wave-uniform)
+  for (uint32_t ub = u0; ub < u1; ub += Q) {
+    uint32_t ln[Q][H];  // the next batch's latencies, loaded while this one computes
+#pragma unroll
+    for (int q = 0; q < (int)Q; q++)
+#pragma unroll
+      for (int h = 0; h < H; h++) ln[q][h] = lrow(ub + Q + q, h);
+#pragma unroll
+    for (int q = 0; q < (int)Q; q++) {
+      const uint32_t u = ub + q;
+      if (u >= u1) break;
+      u32x16 nxt[NV];  // the next tail's -d[s][u], in flight during this tail's work
+#pragma unroll
+      for (int i = 0; i < NV; i++) nxt[i] = sload16(ndrow(u + 1) + 16 * i);
+      uint32_t amin[H], a[H][NG];
+#pragma unroll
+      for (int h = 0; h < H; h++) {
+        const uint32_t nl = lc[q][h];  // (NL32 holds -latency)
+#pragma unroll
+        for (int gi = 0; gi < NG; gi++) {
+          uint32_t acc = add3_vvs(dv[h][16 * gi], nl, cur[gi][0]);
+#pragma unroll
+          for (int k = 1; k < 16; k++) acc = min(acc, add3_vvs(dv[h][16 * gi + k], nl, cur[gi][k]));
+          a[h][gi] = acc;
+        }
+        amin[h] = a[h][0];
+#pragma unroll
+        for (int gi = 1; gi < NG; gi++) amin[h] = min(amin[h], a[h][gi]);
+      }
+#pragma unroll
+      for (int h = 0; h < H; h++) {
+        const uint64_t m = __ballot(amin[h] == 0);
+        if (m) {
+          if (amin[h] == 0) {
+            uint32_t gm = 0;
+#pragma unroll
+            for (int gi = 0; gi < NG; gi++) gm |= a[h][gi] == 0 ? 1u << gi : 0u;
+            hits[wave][nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                (u << 13) | (gm << 9) | (t + 256 * h);
+          }
+          nh += (uint32_t)__popcll(m);
+        }
+      }
+      // the next tail's scalars have arrived (the wait follows this tail's filter: amin)
+      uint32_t am = amin[0];
+#pragma unroll
+      for (int h = 1; h < H; h++) am = min(am, amin[h]);
+      if constexpr (NV == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(nxt[0]) : "v"(am));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(nxt[0]), "+s"(nxt[NV - 1]) : "v"(am));
+#pragma unroll
+      for (int i = 0; i < NV; i++) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int q = 0; q < (int)Q; q++)
+#pragma unroll
+      for (int h = 0; h < H; h++) lc[q][h] = ln[q][h];
+    if (nh > DENSE_HCAP - 64 * kDenseQ || (nh && ub + Q >= u1)) {
+      check(nh);
+      nh = 0;
+    }
+  }
+}
+
 // The loss fold of one used source over its tight list (from loss_sweep): the list into LDS,
 // then the fixed point as in loss_pass. (tcnt > capg: the caller reruns loss_pass instead.)
 __global__ __launch_bounds__(256) void loss_fold(uint32_t Vp, const uint32_t* usrc, const uint32_t* auv,
@@ -1165,7 +1405,36 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       if (!kS) lform = 0;
     }
     const size_t lds_sw = (size_t)Vp * kS * 4 + (csr ? 8 * SWEEP_HCAP * 4 : 0);
-    DevBuf dtc, dtl, dal32;
+    // the dense form of the sweep (loss_sweep_dense): at least half of all arcs present, at most
+    // one arc per (tail, head) — the dense index matrix holds one — and Vp <= 8192 (two Vp^2
+    // u32 matrices); SGN_APSP_DENSE=0 keeps the CSR sweep (A/B), SGN_APSP_DENSE_S picks the
+    // sources per workgroup
+    bool dense = false;
+    int kDS = 16, kDH = 2;  // sources per workgroup, heads per lane
+    if (lform == 1 && csr && Vp <= 8192 && 2ull * E2 >= (uint64_t)V * (V - 1) &&
+        !(getenv("SGN_APSP_DENSE") && atoi(getenv("SGN_APSP_DENSE")) == 0)) {
+      std::vector<uint32_t> seen(V, ~0u);
+      dense = true;
+      for (uint32_t u = 0; u < V && dense; u++)
+        for (uint32_t e = rowptr[u]; e < rowptr[u + 1]; e++) {
+          const uint32_t v = auv[e] >> 16;
+          if (seen[v] == u) {
+            dense = false;
+            break;
+          }
+          seen[v] = u;
+        }
+      if (getenv("SGN_APSP_DENSE_S")) kDS = atoi(getenv("SGN_APSP_DENSE_S")) == 32 ? 32 : 16;
+      if (getenv("SGN_APSP_DENSE_H")) kDH = atoi(getenv("SGN_APSP_DENSE_H")) == 1 ? 1 : 2;
+      if (kDS == 32) kDH = 1;
+    }
+    const uint32_t Upd = (U + kDS - 1) / kDS * kDS;  // NDT's row length
+    DevBuf dtc, dtl, dal32, dNL32, dEI, dNDT;
+    if (dense) {
+      SGN_HIP(ctx, hipMalloc(&dNL32.p, (size_t)Vp * Vp * 4));
+      SGN_HIP(ctx, hipMalloc(&dEI.p, (size_t)Vp * Vp * 4));
+      SGN_HIP(ctx, hipMalloc(&dNDT.p, (size_t)Vp * Upd * 4));
+    }
     if (lform) {
       SGN_HIP(ctx, hipMalloc(&dtc.p, (size_t)U * 4));
       SGN_HIP(ctx, hipMalloc(&dtl.p, (size_t)U * capg * 4));
@@ -1289,6 +1558,12 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
   loss_phase:
     if (form) {
       SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+      if (dense) {
+        SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)dNL32.p, 1, (size_t)Vp * Vp, st));  // (1 = -SQ_INF: no arc)
+        hipLaunchKernelGGL(dense_arcs, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256))),
+                           dim3(256), 0, st, (const uint32_t*)dauv.p, (const uint32_t*)dal32.p, E2, Vp,
+                           (uint32_t*)dNL32.p, (uint32_t*)dEI.p);
+      }
       for (uint32_t r = sh_first; r < sh_last; r++) {
         const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
         if (!ns) continue;
@@ -1300,7 +1575,18 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         const uint32_t* us = (const uint32_t*)dus.p + s0;
         uint32_t* tcs = (uint32_t*)dtc.p + s0;
         uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
-        if (csr && kS == 16)
+        if (dense) {
+          const uint32_t gx = (ns + kDS - 1) / kDS, gy = (Vp + 256 * kDH - 1) / (256 * kDH);
+          const uint32_t wg = getenv("SGN_APSP_DENSE_WG") ? (uint32_t)atoi(getenv("SGN_APSP_DENSE_WG")) : 4096u;
+          const uint32_t gz = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(1, V / 16), (wg + gx * gy - 1) / (gx * gy)));
+          hipLaunchKernelGGL(ndt_build, dim3((Upd + 63) / 64, (Vp + 63) / 64), dim3(256), 0, st, d32, Vp, us, ns,
+                             (uint32_t*)dNDT.p, Upd);
+          hipLaunchKernelGGL(loss_self_tails, dim3(ns), dim3(256), 0, st, d32, Vp, us, V, (const uint32_t*)dNL32.p,
+                             (const uint32_t*)dEI.p, capg, tcs, tls);
+          auto f = kDS == 16 ? (kDH == 2 ? loss_sweep_dense<16, 2> : loss_sweep_dense<16, 1>) : loss_sweep_dense<32, 1>;
+          hipLaunchKernelGGL(f, dim3(gx, gy, gz), dim3(256), 0, st, d32, Vp, us, ns, V, (const uint32_t*)dNDT.p, Upd,
+                             (const uint32_t*)dNL32.p, (const uint32_t*)dEI.p, capg, tcs, tls);
+        } else if (csr && kS == 16)
           hipLaunchKernelGGL(loss_sweep_csr<16>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
                              (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
         else if (csr && kS == 8)
@@ -1377,7 +1663,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       SGN_HIP(ctx, hipMemcpy(dres.p, res0, sizeof(res0), hipMemcpyHostToDevice));
       goto loss_phase;
     }
-    tm.loss_multi = form ? (uint32_t)kS : 0u;
+    tm.loss_multi = form ? (uint32_t)(dense ? kDS : kS) : 0u;
+    tm.loss_dense = form && dense ? 1u : 0u;
     float ms_fw = 0, ms_loss = 0, ms_total = 0;
     hipEventElapsedTime(&ms_fw, e0, e1);
     hipEventElapsedTime(&ms_loss, e1, e2);

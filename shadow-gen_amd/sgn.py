@@ -168,7 +168,8 @@ class RoutesTiming(C.Structure):
                 ("loss_iters", C.c_uint32), ("tile", C.c_uint32), ("n_tight_edges", C.c_uint64),
                 ("latency_passes", C.c_uint32), ("latency_u64", C.c_uint32),
                 ("loss_multi", C.c_uint32), ("latency_bf", C.c_uint32),
-                ("shards", C.c_uint32), ("shard_sources", C.c_uint32)]
+                ("shards", C.c_uint32), ("shard_sources", C.c_uint32),
+                ("loss_dense", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class EngineInfo(C.Structure):

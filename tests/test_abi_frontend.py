@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
     assert not extra, f"undeclared exports: {extra}"
     for n in names:
         assert hasattr(lib, n)
-    assert lib.sgn_abi_version() == 9
+    assert lib.sgn_abi_version() == 10
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -176,6 +176,54 @@ def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
         assert (forms[0] >= 4) == (k < 2), (k, forms)  # sparse graph / list overflow: one-source
 
 
+def test_apsp_dense_sweep_form(ctxf, oracle, monkeypatch):
+    """The dense form of the loss sweep (loss_sweep_dense: a lane per head, the S sources'
+    d[s][v] in registers, -d[s][u] by scalar loads, negated latency and arc-index matrices; the
+    sources' own out-arcs by loss_self_tails) against the oracle and against the CSR sweep
+    (SGN_APSP_DENSE=0): Tor graphs (whose tight arcs are nearly all a source's own), a complete
+    graph with random latencies (tight arcs through other tails, ties), a directed complete graph,
+    a used subset of the nodes (padded source tiles, sources that are not tails 0..U-1), both
+    workgroup shapes; a dense graph with one parallel arc takes the CSR form."""
+    V = 300
+    rng = np.random.default_rng(5)
+    iu, ju = np.triu_indices(V, 1)
+    lat = rng.integers(1, 40, len(iu)).astype(np.uint64) * 1_000_000  # coarse: many ties
+    loss = np.round(rng.uniform(0, 0.02, len(iu)), 6).astype(np.float32)
+    rand_c = sgn.GraphArrays(np.arange(V), np.concatenate([iu, np.arange(V)]), np.concatenate([ju, np.arange(V)]),
+                             np.concatenate([lat, np.full(V, 1_000_000, np.uint64)]),
+                             np.concatenate([loss, np.zeros(V, np.float32)]), False)
+    Vd = 200
+    ii, jj = np.nonzero(~np.eye(Vd, dtype=bool))
+    dlat = rng.integers(1, 60, len(ii)).astype(np.uint64) * 500_000
+    dloss = np.round(rng.uniform(0, 0.01, len(ii)), 6).astype(np.float32)
+    directed = sgn.GraphArrays(np.arange(Vd), np.concatenate([ii, np.arange(Vd)]), np.concatenate([jj, np.arange(Vd)]),
+                               np.concatenate([dlat, np.full(Vd, 1_000_000, np.uint64)]),
+                               np.concatenate([dloss, np.zeros(Vd, np.float32)]), True)
+    par = sgn.GraphArrays(rand_c.node_id, np.concatenate([rand_c.src, [3]]), np.concatenate([rand_c.dst, [7]]),
+                          np.concatenate([rand_c.lat, [2_000_000]]).astype(np.uint64),
+                          np.concatenate([rand_c.loss, [0.001]]).astype(np.float32), False)
+    cases = [(sgn.tor_graph(700, seed=12), None, {}), (sgn.tor_graph(700, seed=12), None, {"SGN_APSP_DENSE_H": "1"}),
+             (sgn.tor_graph(500, seed=13), np.arange(1, 500, 3), {}), (rand_c, None, {}),
+             (rand_c, None, {"SGN_APSP_DENSE_S": "32"}), (directed, None, {}), (par, None, {})]
+    for k, (g, used, env) in enumerate(cases):
+        used = np.arange(len(g.node_id)) if used is None else used
+        ol, op = oracle.routes(g, used)
+        forms = []
+        for dense_env in ({}, {"SGN_APSP_DENSE": "0"}):
+            for key, val in {**env, **dense_env}.items():
+                monkeypatch.setenv(key, val)
+            c = ctxf()
+            c.routes_build(g, used)
+            t = c.routes_timing()
+            forms.append((t["loss_dense"], t["loss_multi"]))
+            for key in {**env, **dense_env}:
+                monkeypatch.delenv(key)
+            gl, gp = c.routes_copy()
+            assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), (k, dense_env)
+        assert forms[1][0] == 0 and forms[1][1] >= 4, (k, forms)
+        assert forms[0][0] == (0 if g is par else 1) and forms[0][1] >= 4, (k, forms)
+
+
 @pytest.mark.parametrize("n_shards", [2, 3, 8])
 def test_apsp_sharded_blocks_equal_whole(ctxf, oracle, monkeypatch, n_shards):
     """The sharded build's block arithmetic (every shard computes a block of used
