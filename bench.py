@@ -352,6 +352,7 @@ def apsp_roofline(apsp, V, U):
         b_lat = max(1, apsp["latency_passes"]) * 8.0 * V ** 3 / T
     k = apsp.get("loss_multi", 0)
     dense = bool(apsp.get("loss_dense", 0))
+    fused = bool(apsp.get("loss_fused", 0))  # the tight sweep ran inside the latency phase
     if not k:
         b_loss = 12.0 * U * E
     elif dense:
@@ -400,7 +401,27 @@ def apsp_roofline(apsp, V, U):
         ph.update({"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tops (int32 lane-ops)",
                    "frac": round(tops / VALU_PEAK_TOPS, 4)})
 
-    if not apsp.get("latency_bf") and not apsp.get("latency_u64", 1) and apsp["latency_ms"] > 0:
+    if fused and apsp["latency_ms"] > 0:
+        # the fused form: the tight sweep over the direct arcs was the squaring's only pass (it
+        # found nothing to shorten), so the latency phase's work is that sweep, 1.5 lane-ops per
+        # (source, arc) pair; the loss phase is the fold alone (its tight-list bytes: HBM)
+        lp, lms = out["latency_phase"], apsp["latency_ms"]
+        b_f = 4.0 * V * V * -(-U // k) + 4.0 * U * V
+        lp.update({"alg_bytes": int(b_f), "l2_bytes": int(b_f),
+                   "l2_frac": round(b_f / (lms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)})
+        valu_bound(lp, 1.5 * U * E, lms)
+        fl = out["loss_phase"]
+        hbm_f = 2 * 4.0 * U * V + 4.0 * U * V
+        fl.update({"alg_bytes": int(hbm_f), "hbm_bytes": int(hbm_f),
+                   "achieved": round(hbm_f / (ms * 1e-3) / 1e9, 2) if ms > 0 else 0.0,
+                   "frac": round(hbm_f / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ms > 0 else 0.0,
+                   "hbm_frac": round(hbm_f / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ms > 0 else 0.0})
+        for key in ("l2_bytes", "l2_GBps", "l2_peak_GBps", "l2_frac", "hbm_GBps"):
+            fl.pop(key, None)
+        fl["bound"] = "hbm"
+        fl["unit"] = "GB/s"
+        fl["peak"] = HBM_PEAK_GBS
+    elif not apsp.get("latency_bf") and not apsp.get("latency_u64", 1) and apsp["latency_ms"] > 0:
         lp, lms = out["latency_phase"], apsp["latency_ms"]
         # compulsory HBM bytes: the u32 matrix read and written once per pass; the panel re-reads
         # of the model above (alg_bytes) are L2-served
@@ -419,9 +440,11 @@ def apsp_roofline(apsp, V, U):
                    "hbm_frac": round(hbm / (lms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "l2_bytes": int(b_lat),
                    "l2_frac": round(b_lat / (lms * 1e-3) / 1e9 / L2_PEAK_GBS, 5)})
         valu_bound(lp, 1.5 * U * E * max(1, apsp["latency_passes"]), lms)
-    if k and ms > 0:
+    if k and ms > 0 and not fused:
         valu_bound(out["loss_phase"], 1.5 * U * E, ms)
-    out["form"] = {"latency": "per-source relaxation" if apsp.get("latency_bf") else
+    out["form"] = {"latency": ("fused tight sweep over the direct arcs = the squaring's one pass (nothing to "
+                               "shorten), then sq_run returns at once") if fused else
+                              "per-source relaxation" if apsp.get("latency_bf") else
                    ("u64 Floyd-Warshall" if apsp.get("latency_u64", 1) else
                     "u32 min-plus squaring, all passes in one launch (sq_run)"),
                    "loss": (f"dense {k}-source sweep (a lane per head, negated latency matrix, scalar -d[s][u], "

@@ -130,7 +130,10 @@ typedef struct sgn_routes_timing {
   uint32_t loss_dense;     /* ABI 10: 1 when the sweep ran in its dense form (at least half of all
                               arcs, no parallel arcs: a (tail, head) matrix of arcs, loss_multi
                               sources per workgroup); 0: the CSR / arc-list sweep or none */
-  uint32_t reserved;
+  uint32_t loss_fused;     /* ABI 10: 1 when the dense sweep ran fused with the first squaring pass
+                              and found the direct arcs already closed (complete graphs whose arcs
+                              are their own shortest paths): the tight arcs were found inside the
+                              latency phase (latency_ms), and loss_ms is the fold alone */
 } sgn_routes_timing;
 int sgn_routes_timing_get(sgn_ctx* ctx, sgn_routes_timing* out);
 

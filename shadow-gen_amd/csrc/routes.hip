@@ -303,7 +303,10 @@ __global__ __launch_bounds__(256) void sq_rows(uint32_t* D, uint32_t Vp, uint32_
 constexpr int SQR_SL = 4;                                   // K slices per workgroup
 constexpr size_t SQR_LDS = 2ull * SQR_SL * SQ_K * (SQ_T + 4) * 4;  // As + Bs per slice
 __global__ __launch_bounds__(1024) void sq_run(uint32_t* D, uint32_t Vp, uint32_t* flag, uint32_t max_pass,
-                                               uint32_t* err, uint32_t* bar) {
+                                               uint32_t* err, uint32_t* bar, const uint32_t* skip) {
+  // (skip: the fused first pass's change word — 0: the matrix is already closed, and this launch
+  // is its one pass that changed nothing; flag[0] stays 0)
+  if (skip && *skip == 0) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef uint32_t Tile[SQ_K][SQ_T + 4];
   Tile* As = (Tile*)smem;
@@ -682,14 +685,26 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
 // A source's own out-arcs (tail u = s) are left to loss_self_tails: on graphs whose edges are
 // their own shortest paths (config C's Tor graph) they are nearly all of the tight pairs, and
 // in the sweep they would fill every lane's hit list at the few tails that are sources.
+// The fused form (kF, complete graphs with every latency below 2^29 ns): the sweep runs on the
+// matrix of direct arcs BEFORE the squaring. It is the squaring's first pass restricted to the
+// used sources: its filter d[s][v] - l(u,v) - d[s][u], read as a signed number, is positive
+// exactly when the arc (u, v) shortens s's path to v, and zero when it is tight. The sweep folds
+// it by a signed max: no positive value anywhere means every used source's row of direct arcs
+// is already closed (Bellman's condition on every arc, so the rows are the shortest paths) and
+// the tight lists are final; the squaring launch then returns at once (one pass that changed
+// nothing) and the loss phase only folds. Otherwise the change word is set, the squaring runs
+// as usual and the loss phase sweeps the final matrix (same form: its entries only shrank).
+// Excluded pairs carry -2^30 (`kFx`) instead of -SQ_INF, so their signed value stays negative.
+constexpr uint32_t kFx = 0xC0000000u;
 constexpr uint32_t kDenseQ = 8;  // tails whose latency loads are in flight at once
 // filter hits a wave lists before checking them exactly: room for one more batch of kDenseQ tails
 // after any fill below the threshold, so the list is checked once per batch at most (one copy
 // of the check in the code: a copy per unrolled tail made the kernel 19 k lines)
 constexpr uint32_t DENSE_HCAP = 2 * 64 * kDenseQ;  // (kDenseQ hit lists per batch: Q tails x H heads)
 
-// NL32[u][v] = minus the arc's u32 latency (1 = -SQ_INF: no arc; the filter's operand as it is
-// used), EI[u][v] = its index (no parallel arcs)
+// NL32[u][v] = minus the arc's u32 latency (the filter's operand as it is used; entries without
+// an arc keep the fill: 1 = -SQ_INF, or kFx in the fused form), EI[u][v] = its index (no
+// parallel arcs)
 __global__ void dense_arcs(const uint32_t* auv, const uint32_t* al32, uint32_t E2, uint32_t Vp, uint32_t* NL32,
                            uint32_t* EI) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E2; e += gridDim.x * blockDim.x) {
@@ -701,15 +716,18 @@ __global__ void dense_arcs(const uint32_t* auv, const uint32_t* al32, uint32_t E
 }
 
 // NDT[u][j] = -d[usrc[j]][u] (u32), through a 64 x 64 LDS tile (rows of D32 read along u, NDT
-// written along j). 1 (= -SQ_INF: the filter never passes it, the exact test rejects it) for the
-// padding sources j >= ns and for u = usrc[j] (loss_self_tails takes those arcs).
+// written along j). 1 (= -SQ_INF: the filter never passes it, the exact test rejects it; kFx in
+// the fused form) for the padding sources j >= ns and for u = usrc[j] (loss_self_tails takes
+// those arcs). gate: run only if *gate != 0 (the fused pass found a change).
+template <bool kF>
 __global__ __launch_bounds__(256) void ndt_build(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t ns,
-                                                 uint32_t* NDT, uint32_t Up) {
+                                                 uint32_t* NDT, uint32_t Up, const uint32_t* gate) {
+  if (gate && *gate == 0) return;
   __shared__ uint32_t tile[64][65];
   const uint32_t j0 = blockIdx.x * 64, u0 = blockIdx.y * 64, c = threadIdx.x & 63;
   for (uint32_t jj = threadIdx.x >> 6; jj < 64; jj += 4) {
     const uint32_t j = j0 + jj, u = u0 + c;
-    uint32_t x = 1u;
+    uint32_t x = kF ? kFx : 1u;
     if (j < ns && u < Vp) {
       const uint32_t s = usrc[j];
       if (u != s) x = 0u - D32[(size_t)s * Vp + u];
@@ -727,7 +745,8 @@ __global__ __launch_bounds__(256) void ndt_build(const uint32_t* D32, uint32_t V
 // counted once per wave
 __global__ __launch_bounds__(256) void loss_self_tails(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t V,
                                                        const uint32_t* NL32, const uint32_t* EI, uint32_t capg,
-                                                       uint32_t* tcnt, uint32_t* tlist) {
+                                                       uint32_t* tcnt, uint32_t* tlist, const uint32_t* gate) {
+  if (gate && *gate == 0) return;
   const uint32_t j = blockIdx.x, s = usrc[j], lane = threadIdx.x & 63;
   const uint32_t du = D32[(size_t)s * Vp + s];
   for (uint32_t v0 = 0; v0 < V; v0 += 256) {
@@ -750,6 +769,12 @@ __global__ __launch_bounds__(256) void loss_self_tails(const uint32_t* D32, uint
   }
 }
 
+// the tight counts zeroed for the loss phase's sweep, when the fused pass found a change
+__global__ void zero_if(uint32_t* p, uint32_t n, const uint32_t* gate) {
+  if (*gate == 0) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
+}
+
 // 16 scalar words in one s_load_dwordx16 issued now and waited for later (swait16): the compiler
 // waits for its own scalar loads at their first use with lgkmcnt(0), which exposed the whole
 // latency at every tail (the first build ran at 60 % of VALU issue, PMC)
@@ -764,13 +789,15 @@ __device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
 // v0 + t + 256 h. The filter folds the sources in groups of 8, so a hit names the groups to test
 // exactly. Per tail the S values -d[s][u] are loaded one tail ahead (asm: issued before the
 // tail's work, waited for after it) and serve H heads per lane.
-template <int S, int H>
+template <int S, int H, bool kF>
 __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restrict__ D32, uint32_t Vp,
                                                         const uint32_t* __restrict__ usrc, uint32_t U, uint32_t V,
                                                         const uint32_t* __restrict__ NDT, uint32_t Up,
                                                         const uint32_t* __restrict__ NL32,
                                                         const uint32_t* __restrict__ EI, uint32_t capg,
-                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tlist) {
+                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tlist,
+                                                        const uint32_t* gate, uint32_t* chg) {
+  if (gate && *gate == 0) return;
   static_assert(S % 16 == 0 && S <= 32, "sources per tail come in 16-word scalar loads");
   static_assert(H == 1 || H == 2, "heads per lane");
   constexpr int NG = S / 16, NV = S / 16;  // filter groups of 16 sources = the scalar loads
@@ -796,7 +823,8 @@ __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restri
 #pragma unroll
   for (int k = 0; k < S; k++)
 #pragma unroll
-    for (int h = 0; h < H; h++) dv[h][k] = g0 + k < U ? D32[srow[k] + vc[h]] : SQ_INF;
+    for (int h = 0; h < H; h++)
+      dv[h][k] = g0 + k < U && (!kF || v0 + t + 256 * h < V) ? D32[srow[k] + vc[h]] : kF ? 0u : SQ_INF;
   const uint32_t u0 = (uint32_t)((uint64_t)V * bz / gridDim.z);
   const uint32_t u1 = (uint32_t)((uint64_t)V * (bz + 1) / gridDim.z);
   // the exact test of the listed hits, lane-parallel; an entry is u << 13 | groups << 9 | head
@@ -847,6 +875,7 @@ __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restri
   if constexpr (NV == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(cur[0]));
   else asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(cur[0]), "+s"(cur[NV - 1]));
   uint32_t nh = 0;  // (wave-uniform)
+  bool grew = false;  // (kF) some arc shortens some source's path
   for (uint32_t ub = u0; ub < u1; ub += Q) {
     uint32_t ln[Q][H];  // the next batch's latencies, loaded while this one computes
 #pragma unroll
@@ -868,12 +897,16 @@ __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restri
         for (int gi = 0; gi < NG; gi++) {
           uint32_t acc = add3_vvs(dv[h][16 * gi], nl, cur[gi][0]);
 #pragma unroll
-          for (int k = 1; k < 16; k++) acc = min(acc, add3_vvs(dv[h][16 * gi + k], nl, cur[gi][k]));
+          for (int k = 1; k < 16; k++) {
+            const uint32_t x = add3_vvs(dv[h][16 * gi + k], nl, cur[gi][k]);
+            acc = kF ? (uint32_t)max((int32_t)acc, (int32_t)x) : min(acc, x);
+          }
           a[h][gi] = acc;
         }
         amin[h] = a[h][0];
 #pragma unroll
-        for (int gi = 1; gi < NG; gi++) amin[h] = min(amin[h], a[h][gi]);
+        for (int gi = 1; gi < NG; gi++) amin[h] = kF ? (uint32_t)max((int32_t)amin[h], (int32_t)a[h][gi]) : min(amin[h], a[h][gi]);
+        if constexpr (kF) grew |= (int32_t)amin[h] > 0;
       }
 #pragma unroll
       for (int h = 0; h < H; h++) {
@@ -906,6 +939,9 @@ __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restri
       check(nh);
       nh = 0;
     }
+  }
+  if constexpr (kF) {
+    if (chg && __ballot(grew) && lane == 0) atomicOr(chg, 1u);
   }
 }
 
@@ -1375,7 +1411,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     const uint32_t max_pass = 34;
     if (fast) {
       SGN_HIP(ctx, hipMalloc(&dD32.p, (size_t)Vp * Vp * 4));
-      SGN_HIP(ctx, hipMalloc(&dflag.p, (max_pass + 2) * 4));  // + sq_run's timeout word and barrier counter
+      SGN_HIP(ctx, hipMalloc(&dflag.p, (max_pass + 3) * 4));  // + sq_run's timeout word, barrier counter, the
+                                                              // fused pass's change word
     }
     // the loss phase's form and buffers (allocated here, outside the timed build)
     const uint32_t capg = std::max<uint32_t>(4096, 4 * Vp);
@@ -1429,6 +1466,11 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       if (kDS == 32) kDH = 1;
     }
     const uint32_t Upd = (U + kDS - 1) / kDS * kDS;  // NDT's row length
+    // the fused form (loss_sweep_dense<.., true> before the squaring): complete graphs whose
+    // latencies stay below 2^29 ns (signed sums), one shard; SGN_APSP_FUSED=0 turns it off (A/B)
+    const bool fused_ok = dense && kDS == 16 && kDH == 2 && E2 == (uint64_t)V * (V - 1) && max_edge < (1ull << 29) &&
+                          !(getenv("SGN_APSP_FUSED") && atoi(getenv("SGN_APSP_FUSED")) == 0);
+    bool fused = false;
     DevBuf dtc, dtl, dal32, dNL32, dEI, dNDT;
     if (dense) {
       SGN_HIP(ctx, hipMalloc(&dNL32.p, (size_t)Vp * Vp * 4));
@@ -1490,6 +1532,26 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         sq_one = false;
       }
     }
+    // the dense sweep over used sources [s0, s0 + ns): NDT, the sources' own out-arcs, the sweep
+    // (kf: the fused form; gate: run only if the fused pass found a change; chg: its change word)
+    auto dense_block = [&](uint32_t s0, uint32_t ns, bool kf, const uint32_t* gate, uint32_t* chg) {
+      const uint32_t* d32 = (const uint32_t*)dD32.p;
+      const uint32_t* us = (const uint32_t*)dus.p + s0;
+      uint32_t* tcs = (uint32_t*)dtc.p + s0;
+      uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
+      const uint32_t gx = (ns + kDS - 1) / kDS, gy = (Vp + 256 * kDH - 1) / (256 * kDH);
+      const uint32_t wg = getenv("SGN_APSP_DENSE_WG") ? (uint32_t)atoi(getenv("SGN_APSP_DENSE_WG")) : 4096u;
+      const uint32_t gz = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(1, V / 16), (wg + gx * gy - 1) / (gx * gy)));
+      hipLaunchKernelGGL(kf ? ndt_build<true> : ndt_build<false>, dim3((Upd + 63) / 64, (Vp + 63) / 64), dim3(256), 0, st,
+                         d32, Vp, us, ns, (uint32_t*)dNDT.p, Upd, gate);
+      hipLaunchKernelGGL(loss_self_tails, dim3(ns), dim3(256), 0, st, d32, Vp, us, V, (const uint32_t*)dNL32.p,
+                         (const uint32_t*)dEI.p, capg, tcs, tls, gate);
+      auto f = kf ? loss_sweep_dense<16, 2, true>
+                  : kDS == 16 ? (kDH == 2 ? loss_sweep_dense<16, 2, false> : loss_sweep_dense<16, 1, false>)
+                              : loss_sweep_dense<32, 1, false>;
+      hipLaunchKernelGGL(f, dim3(gx, gy, gz), dim3(256), 0, st, d32, Vp, us, ns, V, (const uint32_t*)dNDT.p, Upd,
+                         (const uint32_t*)dNL32.p, (const uint32_t*)dEI.p, capg, tcs, tls, gate, chg);
+    };
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
     if (bf) {  // per source: a shard's block needs no exchange until the table
@@ -1502,7 +1564,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
     } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
-      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 2) * 4, st));
+      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 3) * 4, st));
       if (csr) {
         hipLaunchKernelGGL(sq_rows, dim3(Vp), dim3(256), (size_t)Vp * 4, st, D32, Vp, V, (const uint32_t*)drp.p,
                            (const uint32_t*)dauv.p, (const uint64_t*)dal.p);
@@ -1512,13 +1574,26 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
                            st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
                            (int)g->directed);
       }
+      // the fused form: the tight sweep on the direct arcs, which is also the first squaring pass
+      // for the used sources (sq_run returns at once if it found no change)
+      fused = fused_ok && csr && sq_one && nsh == 1;
+      uint32_t* chgw = (uint32_t*)dflag.p + max_pass + 2;
+      if (fused) {
+        SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+        SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)dNL32.p, (int)kFx, (size_t)Vp * Vp, st));
+        hipLaunchKernelGGL(dense_arcs, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256))), dim3(256), 0,
+                           st, (const uint32_t*)dauv.p, (const uint32_t*)dal32.p, E2, Vp, (uint32_t*)dNL32.p,
+                           (uint32_t*)dEI.p);
+        dense_block(0, U, true, nullptr, chgw);
+      }
       // ceil(log2 Vp) passes cover every simple path; one more confirms the fixed point
       uint32_t passes = 1;
       while ((1u << (passes - 1)) < Vp) passes++;
       passes = std::min(passes + 1, max_pass);
       if (sq_one)
         hipLaunchKernelGGL(sq_run, dim3(std::min<uint32_t>(nb * nb, n_cu)), dim3(1024), SQR_LDS, st, D32, Vp,
-                           (uint32_t*)dflag.p, passes, (uint32_t*)dflag.p + max_pass, (uint32_t*)dflag.p + max_pass + 1);
+                           (uint32_t*)dflag.p, passes, (uint32_t*)dflag.p + max_pass, (uint32_t*)dflag.p + max_pass + 1,
+                           (const uint32_t*)(fused ? chgw : nullptr));
       for (uint32_t it = 0; it < passes && !sq_one; it++) {
         for (uint32_t r = sh_first; r < sh_last; r++) {
           const uint32_t t0 = (uint32_t)toff[r], nt = (uint32_t)(toff[r + 1] - t0);
@@ -1557,8 +1632,13 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     int form = lform;
   loss_phase:
     if (form) {
-      SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
-      if (dense) {
+      const uint32_t* gate = fused ? (const uint32_t*)dflag.p + max_pass + 2 : nullptr;
+      if (fused)  // (the fused pass's lists stand unless it found a change)
+        hipLaunchKernelGGL(zero_if, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (U + 255) / 256))), dim3(256), 0, st,
+                           (uint32_t*)dtc.p, U, gate);
+      else
+        SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+      if (dense && !fused) {
         SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)dNL32.p, 1, (size_t)Vp * Vp, st));  // (1 = -SQ_INF: no arc)
         hipLaunchKernelGGL(dense_arcs, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256))),
                            dim3(256), 0, st, (const uint32_t*)dauv.p, (const uint32_t*)dal32.p, E2, Vp,
@@ -1576,16 +1656,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         uint32_t* tcs = (uint32_t*)dtc.p + s0;
         uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
         if (dense) {
-          const uint32_t gx = (ns + kDS - 1) / kDS, gy = (Vp + 256 * kDH - 1) / (256 * kDH);
-          const uint32_t wg = getenv("SGN_APSP_DENSE_WG") ? (uint32_t)atoi(getenv("SGN_APSP_DENSE_WG")) : 4096u;
-          const uint32_t gz = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(1, V / 16), (wg + gx * gy - 1) / (gx * gy)));
-          hipLaunchKernelGGL(ndt_build, dim3((Upd + 63) / 64, (Vp + 63) / 64), dim3(256), 0, st, d32, Vp, us, ns,
-                             (uint32_t*)dNDT.p, Upd);
-          hipLaunchKernelGGL(loss_self_tails, dim3(ns), dim3(256), 0, st, d32, Vp, us, V, (const uint32_t*)dNL32.p,
-                             (const uint32_t*)dEI.p, capg, tcs, tls);
-          auto f = kDS == 16 ? (kDH == 2 ? loss_sweep_dense<16, 2> : loss_sweep_dense<16, 1>) : loss_sweep_dense<32, 1>;
-          hipLaunchKernelGGL(f, dim3(gx, gy, gz), dim3(256), 0, st, d32, Vp, us, ns, V, (const uint32_t*)dNDT.p, Upd,
-                             (const uint32_t*)dNL32.p, (const uint32_t*)dEI.p, capg, tcs, tls);
+          dense_block(s0, ns, fused, gate, nullptr);
         } else if (csr && kS == 16)
           hipLaunchKernelGGL(loss_sweep_csr<16>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
                              (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
@@ -1684,8 +1755,9 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
               n_global, cap);
     uint32_t sq_passes = 0;
     if (fast) {
-      std::vector<uint32_t> fl(max_pass + 1);
-      SGN_HIP(ctx, hipMemcpy(fl.data(), dflag.p, (max_pass + 1) * 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> fl(max_pass + 3);
+      SGN_HIP(ctx, hipMemcpy(fl.data(), dflag.p, (max_pass + 3) * 4, hipMemcpyDeviceToHost));
+      tm.loss_fused = fused && fl[max_pass + 2] == 0 ? 1u : 0u;
       if (sq_one && fl[max_pass]) {  // sq_run's grid barrier timed out: redo with sq_pass launches
         fprintf(stderr, "libsgn: APSP squaring grid not resident; one launch per pass\n");
         sq_one = false;

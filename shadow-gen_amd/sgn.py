@@ -169,7 +169,7 @@ class RoutesTiming(C.Structure):
                 ("latency_passes", C.c_uint32), ("latency_u64", C.c_uint32),
                 ("loss_multi", C.c_uint32), ("latency_bf", C.c_uint32),
                 ("shards", C.c_uint32), ("shard_sources", C.c_uint32),
-                ("loss_dense", C.c_uint32), ("reserved", C.c_uint32)]
+                ("loss_dense", C.c_uint32), ("loss_fused", C.c_uint32)]
 
 
 class EngineInfo(C.Structure):

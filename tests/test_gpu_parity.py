@@ -179,11 +179,16 @@ def test_apsp_loss_forms_agree(ctxf, oracle, monkeypatch):
 def test_apsp_dense_sweep_form(ctxf, oracle, monkeypatch):
     """The dense form of the loss sweep (loss_sweep_dense: a lane per head, the S sources'
     d[s][v] in registers, -d[s][u] by scalar loads, negated latency and arc-index matrices; the
-    sources' own out-arcs by loss_self_tails) against the oracle and against the CSR sweep
-    (SGN_APSP_DENSE=0): Tor graphs (whose tight arcs are nearly all a source's own), a complete
-    graph with random latencies (tight arcs through other tails, ties), a directed complete graph,
-    a used subset of the nodes (padded source tiles, sources that are not tails 0..U-1), both
-    workgroup shapes; a dense graph with one parallel arc takes the CSR form."""
+    sources' own out-arcs by loss_self_tails) and its fused form (the sweep on the direct arcs
+    before the squaring, as its first pass: complete graphs) against the oracle, against the
+    unfused dense sweep (SGN_APSP_FUSED=0) and against the CSR sweep (SGN_APSP_DENSE=0):
+    - Tor graphs: complete, every arc its own shortest path — fused, nothing to shorten;
+    - points on a line (complete, every collinear triple a tie): fused, tight arcs through
+      other tails in nearly every wave step;
+    - a complete graph with random latencies and a directed complete graph: the fused pass finds
+      paths to shorten, the squaring runs and the loss phase sweeps the final matrix;
+    - a used subset of the nodes (padded source tiles, sources that are not tails 0..U-1), the
+      other workgroup shapes (unfused), and a dense graph with one parallel arc (CSR form)."""
     V = 300
     rng = np.random.default_rng(5)
     iu, ju = np.triu_indices(V, 1)
@@ -199,29 +204,41 @@ def test_apsp_dense_sweep_form(ctxf, oracle, monkeypatch):
     directed = sgn.GraphArrays(np.arange(Vd), np.concatenate([ii, np.arange(Vd)]), np.concatenate([jj, np.arange(Vd)]),
                                np.concatenate([dlat, np.full(Vd, 1_000_000, np.uint64)]),
                                np.concatenate([dloss, np.zeros(Vd, np.float32)]), True)
+    Vl = 60
+    x = rng.permutation(Vl).astype(np.int64)
+    li, lj = np.triu_indices(Vl, 1)
+    llat = (np.abs(x[li] - x[lj]) * 1_000_000).astype(np.uint64)
+    lloss = np.round(rng.uniform(0, 0.01, len(li)), 6).astype(np.float32)
+    line = sgn.GraphArrays(np.arange(Vl), np.concatenate([li, np.arange(Vl)]), np.concatenate([lj, np.arange(Vl)]),
+                           np.concatenate([llat, np.full(Vl, 1_000_000, np.uint64)]),
+                           np.concatenate([lloss, np.zeros(Vl, np.float32)]), False)
     par = sgn.GraphArrays(rand_c.node_id, np.concatenate([rand_c.src, [3]]), np.concatenate([rand_c.dst, [7]]),
                           np.concatenate([rand_c.lat, [2_000_000]]).astype(np.uint64),
                           np.concatenate([rand_c.loss, [0.001]]).astype(np.float32), False)
-    cases = [(sgn.tor_graph(700, seed=12), None, {}), (sgn.tor_graph(700, seed=12), None, {"SGN_APSP_DENSE_H": "1"}),
-             (sgn.tor_graph(500, seed=13), np.arange(1, 500, 3), {}), (rand_c, None, {}),
-             (rand_c, None, {"SGN_APSP_DENSE_S": "32"}), (directed, None, {}), (par, None, {})]
-    for k, (g, used, env) in enumerate(cases):
+    tor = sgn.tor_graph(700, seed=12)
+    # (graph, used, env, expected (loss_dense, loss_fused) of the default run)
+    cases = [(tor, None, {}, (1, 1)), (tor, None, {"SGN_APSP_DENSE_H": "1"}, (1, 0)),
+             (sgn.tor_graph(500, seed=13), np.arange(1, 500, 3), {}, (1, 1)), (line, None, {}, (1, 1)),
+             (rand_c, None, {}, (1, 0)), (rand_c, None, {"SGN_APSP_DENSE_S": "32"}, (1, 0)),
+             (directed, None, {}, (1, 0)), (par, None, {}, (0, 0))]
+    for k, (g, used, env, want) in enumerate(cases):
         used = np.arange(len(g.node_id)) if used is None else used
         ol, op = oracle.routes(g, used)
         forms = []
-        for dense_env in ({}, {"SGN_APSP_DENSE": "0"}):
-            for key, val in {**env, **dense_env}.items():
+        for form_env in ({}, {"SGN_APSP_FUSED": "0"}, {"SGN_APSP_DENSE": "0"}):
+            for key, val in {**env, **form_env}.items():
                 monkeypatch.setenv(key, val)
             c = ctxf()
             c.routes_build(g, used)
             t = c.routes_timing()
-            forms.append((t["loss_dense"], t["loss_multi"]))
-            for key in {**env, **dense_env}:
+            forms.append((t["loss_dense"], t["loss_fused"], t["loss_multi"]))
+            for key in {**env, **form_env}:
                 monkeypatch.delenv(key)
             gl, gp = c.routes_copy()
-            assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), (k, dense_env)
-        assert forms[1][0] == 0 and forms[1][1] >= 4, (k, forms)
-        assert forms[0][0] == (0 if g is par else 1) and forms[0][1] >= 4, (k, forms)
+            assert np.array_equal(ol, gl) and np.array_equal(op.view(np.uint32), gp.view(np.uint32)), (k, form_env)
+        assert forms[0][:2] == want and forms[0][2] >= 4, (k, forms)
+        assert forms[1][:2] == (want[0], 0) and forms[1][2] >= 4, (k, forms)
+        assert forms[2][:2] == (0, 0) and forms[2][2] >= 4, (k, forms)
 
 
 @pytest.mark.parametrize("n_shards", [2, 3, 8])

@@ -28,7 +28,8 @@ def run(kind, V):
             **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()},
             "form": "per-source relaxation (u64)" if t["latency_bf"] else
                     ("u64 Floyd-Warshall" if t["latency_u64"] else "u32 min-plus squaring"),
-            "loss_form": (f"dense {t['loss_multi']}-source sweep + fold" if t.get("loss_dense") else
+            "loss_form": (f"dense {t['loss_multi']}-source sweep + fold" + (" (fused with the first pass)" if t.get("loss_fused") else "")
+                          if t.get("loss_dense") else
                           f"{t['loss_multi']}-source sweep + fold") if t["loss_multi"] else "one-source pass"}
 
 
