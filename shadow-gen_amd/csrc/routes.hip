@@ -196,6 +196,7 @@ __global__ __launch_bounds__(256) void fw_phase3(uint64_t* D, uint32_t Vp, int k
 // above. In place: a tile may read entries another workgroup already lowered this pass,
 // which are still real path lengths, so the fixed point is the same.
 constexpr uint32_t SQ_INF = 0xFFFFFFFFu;
+constexpr uint32_t kFx = 0xC0000000u;  // -2^30: the fused sweep's excluded pairs (loss_sweep_dense)
 constexpr int SQ_T = 64, SQ_K = 32;
 
 __global__ void sq_init(uint32_t* D, uint32_t Vp) {
@@ -275,19 +276,45 @@ __global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_
 // sq_init + sq_edges for a graph whose arcs are in tail order (CSR): one workgroup per row u
 // builds d[u][.] in LDS (the diagonal 0, each arc's latency by LDS atomic min: parallel
 // arcs keep the shortest) and writes it whole — no global atomics, one coalesced row write.
+// NL, EI (the fused form of the loss sweep: no parallel arcs): the same row negated, with kFx on
+// the diagonal and where there is no arc, and each arc's index (dense_arcs' matrices). NDT
+// (undirected graphs: the matrix is symmetric, so row u is column u): the sweep's transposed
+// used-source entries of row u, NDT[u][j] = -d[usrc[j]][u], as ndt_build<true> makes them.
 __global__ __launch_bounds__(256) void sq_rows(uint32_t* D, uint32_t Vp, uint32_t V, const uint32_t* rowptr,
-                                               const uint32_t* auv, const uint64_t* al) {
+                                               const uint32_t* auv, const uint64_t* al, uint32_t* NL, uint32_t* EI,
+                                               uint32_t* NDT, const uint32_t* usrc, uint32_t ns, uint32_t Up) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* row = (uint32_t*)smem;
   const uint32_t u = blockIdx.x;
   for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) row[v] = v == u ? 0u : SQ_INF;
   __syncthreads();
   if (u < V)
-    for (uint32_t e = rowptr[u] + threadIdx.x; e < rowptr[u + 1]; e += blockDim.x)
-      atomicMin(&row[auv[e] >> 16], (uint32_t)al[e]);  // (< 2^32 - 1: the fast form's bound)
+    for (uint32_t e = rowptr[u] + threadIdx.x; e < rowptr[u + 1]; e += blockDim.x) {
+      const uint32_t v = auv[e] >> 16;
+      atomicMin(&row[v], (uint32_t)al[e]);  // (< 2^32 - 1: the fast form's bound)
+      if (EI) EI[(uint64_t)u * Vp + v] = e;
+    }
   __syncthreads();
-  for (uint32_t v = 4 * threadIdx.x; v < Vp; v += 4 * blockDim.x)
-    *(uint4*)&D[(uint64_t)u * Vp + v] = *(const uint4*)&row[v];
+  for (uint32_t v = 4 * threadIdx.x; v < Vp; v += 4 * blockDim.x) {
+    const uint4 r = *(const uint4*)&row[v];
+    *(uint4*)&D[(uint64_t)u * Vp + v] = r;
+    if (NL) {
+      const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
+      uint32_t nv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) nv[k] = v + k == u || rv[k] == SQ_INF ? kFx : 0u - rv[k];
+      *(uint4*)&NL[(uint64_t)u * Vp + v] = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+    }
+  }
+  if (NDT)
+    for (uint32_t j = threadIdx.x; j < Up; j += blockDim.x) {
+      uint32_t x = kFx;
+      if (j < ns) {
+        const uint32_t sj = usrc[j];
+        if (sj != u) x = 0u - row[sj];
+      }
+      NDT[(uint64_t)u * Up + j] = x;
+    }
 }
 
 // All squaring passes in ONE launch (one shard): a 1024-thread workgroup per 64 x 64 output tile
@@ -682,7 +709,8 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
 // sources' distance columns, transposed and negated). Per pair: one v_add3_u32 and half a
 // v_min3. Arcs are looked up through a dense (tail, head) -> arc index matrix, so the tight
 // lists hold the same arc indices as the CSR form, and the fold reads them alike.
-// A source's own out-arcs (tail u = s) are left to loss_self_tails: on graphs whose edges are
+// A source's own out-arcs (tail u = s) are taken apart (the first tail range's workgroups test
+// them from registers before the sweep): on graphs whose edges are
 // their own shortest paths (config C's Tor graph) they are nearly all of the tight pairs, and
 // in the sweep they would fill every lane's hit list at the few tails that are sources.
 // The fused form (kF, complete graphs with every latency below 2^29 ns): the sweep runs on the
@@ -695,7 +723,6 @@ __global__ __launch_bounds__(512) void loss_sweep_csr(const uint32_t* D32, uint3
 // nothing) and the loss phase only folds. Otherwise the change word is set, the squaring runs
 // as usual and the loss phase sweeps the final matrix (same form: its entries only shrank).
 // Excluded pairs carry -2^30 (`kFx`) instead of -SQ_INF, so their signed value stays negative.
-constexpr uint32_t kFx = 0xC0000000u;
 constexpr uint32_t kDenseQ = 8;  // tails whose latency loads are in flight at once
 // filter hits a wave lists before checking them exactly: room for one more batch of kDenseQ tails
 // after any fill below the threshold, so the list is checked once per batch at most (one copy
@@ -717,14 +744,19 @@ __global__ void dense_arcs(const uint32_t* auv, const uint32_t* al32, uint32_t E
 
 // NDT[u][j] = -d[usrc[j]][u] (u32), through a 64 x 64 LDS tile (rows of D32 read along u, NDT
 // written along j). 1 (= -SQ_INF: the filter never passes it, the exact test rejects it; kFx in
-// the fused form) for the padding sources j >= ns and for u = usrc[j] (loss_self_tails takes
-// those arcs). gate: run only if *gate != 0 (the fused pass found a change).
+// the fused form) for the padding sources j >= ns and for u = usrc[j] (the sweep's own-arc step takes
+// those arcs). gate: run only if *gate != 0 (the fused pass found a change); zero: the tight
+// counts to clear first (the loss phase's sweep after a change).
 template <bool kF>
 __global__ __launch_bounds__(256) void ndt_build(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t ns,
-                                                 uint32_t* NDT, uint32_t Up, const uint32_t* gate) {
+                                                 uint32_t* NDT, uint32_t Up, const uint32_t* gate, uint32_t* zero) {
   if (gate && *gate == 0) return;
+  if (zero)
+    for (uint32_t i = (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; i < ns; i += gridDim.x * gridDim.y * 256)
+      zero[i] = 0;
   __shared__ uint32_t tile[64][65];
   const uint32_t j0 = blockIdx.x * 64, u0 = blockIdx.y * 64, c = threadIdx.x & 63;
+#pragma unroll
   for (uint32_t jj = threadIdx.x >> 6; jj < 64; jj += 4) {
     const uint32_t j = j0 + jj, u = u0 + c;
     uint32_t x = kF ? kFx : 1u;
@@ -739,40 +771,6 @@ __global__ __launch_bounds__(256) void ndt_build(const uint32_t* D32, uint32_t V
     const uint32_t u = u0 + uu, j = j0 + c;
     if (u < Vp && j < Up) NDT[(size_t)u * Up + j] = tile[c][uu];
   }
-}
-
-// The tight arcs out of each source itself (tail u = s): one workgroup per source, appends
-// counted once per wave
-__global__ __launch_bounds__(256) void loss_self_tails(const uint32_t* D32, uint32_t Vp, const uint32_t* usrc, uint32_t V,
-                                                       const uint32_t* NL32, const uint32_t* EI, uint32_t capg,
-                                                       uint32_t* tcnt, uint32_t* tlist, const uint32_t* gate) {
-  if (gate && *gate == 0) return;
-  const uint32_t j = blockIdx.x, s = usrc[j], lane = threadIdx.x & 63;
-  const uint32_t du = D32[(size_t)s * Vp + s];
-  for (uint32_t v0 = 0; v0 < V; v0 += 256) {
-    const uint32_t v = v0 + threadIdx.x;
-    bool tight = false;
-    if (v < V && du != SQ_INF) {
-      const uint32_t lq = 0u - NL32[(size_t)s * Vp + v], bk = D32[(size_t)s * Vp + v];
-      tight = lq != SQ_INF && bk >= du && bk - du == lq;
-    }
-    const uint64_t m = __ballot(tight);
-    if (!m) continue;
-    const uint32_t first = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(&tcnt[j], (uint32_t)__popcll(m));
-    base = __shfl(base, (int)first, 64);
-    if (tight) {
-      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (pos < capg) tlist[(uint64_t)j * capg + pos] = EI[(size_t)s * Vp + v];
-    }
-  }
-}
-
-// the tight counts zeroed for the loss phase's sweep, when the fused pass found a change
-__global__ void zero_if(uint32_t* p, uint32_t n, const uint32_t* gate) {
-  if (*gate == 0) return;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
 }
 
 // 16 scalar words in one s_load_dwordx16 issued now and waited for later (swait16): the compiler
@@ -827,6 +825,36 @@ __global__ __launch_bounds__(256) void loss_sweep_dense(const uint32_t* __restri
       dv[h][k] = g0 + k < U && (!kF || v0 + t + 256 * h < V) ? D32[srow[k] + vc[h]] : kF ? 0u : SQ_INF;
   const uint32_t u0 = (uint32_t)((uint64_t)V * bz / gridDim.z);
   const uint32_t u1 = (uint32_t)((uint64_t)V * (bz + 1) / gridDim.z);
+  // the sources' own out-arcs (tail u = s, excluded from the sweep below: NDT holds -SQ_INF or
+  // kFx there), source k by the workgroups of tail range k mod (tail ranges): d[s][v] is in
+  // registers, one append per wave and (source, head) with a tight lane
+  {
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      if (g0 + k >= U) break;
+      if ((uint32_t)k % gridDim.z != bz) continue;
+      const uint32_t sr = srow[k], sn = sr / Vp, du = D32[sr + sn];
+#pragma unroll
+      for (int h = 0; h < H; h++) {
+        const uint32_t v = v0 + t + 256 * h;
+        bool tight = false;
+        if (v < V && du != SQ_INF) {
+          const uint32_t lq = 0u - NL32[sr + v], bk = dv[h][k];
+          tight = lq != SQ_INF && bk >= du && bk - du == lq;
+        }
+        const uint64_t m = __ballot(tight);
+        if (!m) continue;
+        const uint32_t first = (uint32_t)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(&tcnt[g0 + k], (uint32_t)__popcll(m));
+        base = __shfl(base, (int)first, 64);
+        if (tight) {
+          const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (pos < capg) tlist[(uint64_t)(g0 + k) * capg + pos] = EI[sr + v];
+        }
+      }
+    }
+  }
   // the exact test of the listed hits, lane-parallel; an entry is u << 13 | groups << 9 | head
   // offset, and a group's 16 values of d[s][u] and d[s][v] are loaded at once
   auto check = [&](uint32_t n) {
@@ -1110,14 +1138,16 @@ __global__ __launch_bounds__(512) void loss_pass(const uint64_t* D, uint32_t Vp,
 // {first disconnected column, min latency, max latency} go to rowres[3 i ..] with plain
 // stores (no same-address atomics across thousands of waves: that serialised the old form
 // at ~88 atomics/us on one word), and extract_fold reduces the rows into res.
-__global__ __launch_bounds__(256) void extract(const uint64_t* __restrict__ D, uint32_t Vp,
+template <bool k32>  // the distances as the u32 squaring left them (SQ_INF: no u32 path) or u64
+__global__ __launch_bounds__(256) void extract(const void* __restrict__ Dv, uint32_t Vp,
                                                const float* __restrict__ Lrows, const uint32_t* __restrict__ uidx,
                                                uint32_t U, const uint64_t* self_lat, const float* self_loss,
                                                uint64_t* lat, float* loss, uint64_t* rowres, uint32_t row0) {
   __shared__ uint64_t sh[3][4];
   const uint32_t i = row0 + blockIdx.x;
   const uint64_t base = (uint64_t)i * U;
-  const uint64_t* drow = D + (uint64_t)uidx[i] * Vp;
+  const uint64_t* drow = (const uint64_t*)Dv + (uint64_t)uidx[i] * Vp;
+  const uint32_t* drow32 = (const uint32_t*)Dv + (uint64_t)uidx[i] * Vp;
   const float* lrow = Lrows + (uint64_t)i * Vp;
   uint64_t mn = ~0ULL, mx = 0;
   uint32_t bad = 0xFFFFFFFFu;
@@ -1129,7 +1159,12 @@ __global__ __launch_bounds__(256) void extract(const uint64_t* __restrict__ D, u
       p = self_loss[i];
     } else {
       const uint32_t c = uidx[j];
-      l = drow[c];
+      if constexpr (k32) {
+        const uint32_t d = drow32[c];
+        l = d == SQ_INF ? FW_INF : d;
+      } else {
+        l = drow[c];
+      }
       p = lrow[c];
       if (l >= FW_INF && j < bad) bad = j;
     }
@@ -1534,7 +1569,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     // the dense sweep over used sources [s0, s0 + ns): NDT, the sources' own out-arcs, the sweep
     // (kf: the fused form; gate: run only if the fused pass found a change; chg: its change word)
-    auto dense_block = [&](uint32_t s0, uint32_t ns, bool kf, const uint32_t* gate, uint32_t* chg) {
+    auto dense_block = [&](uint32_t s0, uint32_t ns, bool kf, const uint32_t* gate, uint32_t* chg, bool zero,
+                           bool ndt_ready) {
       const uint32_t* d32 = (const uint32_t*)dD32.p;
       const uint32_t* us = (const uint32_t*)dus.p + s0;
       uint32_t* tcs = (uint32_t*)dtc.p + s0;
@@ -1542,18 +1578,19 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       const uint32_t gx = (ns + kDS - 1) / kDS, gy = (Vp + 256 * kDH - 1) / (256 * kDH);
       const uint32_t wg = getenv("SGN_APSP_DENSE_WG") ? (uint32_t)atoi(getenv("SGN_APSP_DENSE_WG")) : 4096u;
       const uint32_t gz = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(1, V / 16), (wg + gx * gy - 1) / (gx * gy)));
-      hipLaunchKernelGGL(kf ? ndt_build<true> : ndt_build<false>, dim3((Upd + 63) / 64, (Vp + 63) / 64), dim3(256), 0, st,
-                         d32, Vp, us, ns, (uint32_t*)dNDT.p, Upd, gate);
-      hipLaunchKernelGGL(loss_self_tails, dim3(ns), dim3(256), 0, st, d32, Vp, us, V, (const uint32_t*)dNL32.p,
-                         (const uint32_t*)dEI.p, capg, tcs, tls, gate);
+      if (!ndt_ready)
+        hipLaunchKernelGGL(kf ? ndt_build<true> : ndt_build<false>, dim3((Upd + 63) / 64, (Vp + 63) / 64), dim3(256), 0,
+                           st, d32, Vp, us, ns, (uint32_t*)dNDT.p, Upd, gate, zero ? tcs : nullptr);
       auto f = kf ? loss_sweep_dense<16, 2, true>
                   : kDS == 16 ? (kDH == 2 ? loss_sweep_dense<16, 2, false> : loss_sweep_dense<16, 1, false>)
                               : loss_sweep_dense<32, 1, false>;
       hipLaunchKernelGGL(f, dim3(gx, gy, gz), dim3(256), 0, st, d32, Vp, us, ns, V, (const uint32_t*)dNDT.p, Upd,
                          (const uint32_t*)dNL32.p, (const uint32_t*)dEI.p, capg, tcs, tls, gate, chg);
     };
+    bool wide = true;  // D (u64) holds the distances; false: only D32 (u32 squaring)
   latency_phase:
     SGN_HIP(ctx, hipEventRecord(e0, st));
+    wide = true;
     if (bf) {  // per source: a shard's block needs no exchange until the table
       for (uint32_t r = sh_first; r < sh_last; r++) {
         const uint32_t s0 = (uint32_t)soff[r], ns = (uint32_t)(soff[r + 1] - s0);
@@ -1565,26 +1602,25 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
       SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 3) * 4, st));
+      // the fused form: the tight sweep on the direct arcs, which is also the first squaring pass
+      // for the used sources (sq_run returns at once if it found no change); sq_rows writes the
+      // sweep's negated latency and arc-index matrices beside the rows
+      fused = fused_ok && csr && sq_one && nsh == 1;
+      uint32_t* chgw = (uint32_t*)dflag.p + max_pass + 2;
       if (csr) {
         hipLaunchKernelGGL(sq_rows, dim3(Vp), dim3(256), (size_t)Vp * 4, st, D32, Vp, V, (const uint32_t*)drp.p,
-                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p);
+                           (const uint32_t*)dauv.p, (const uint64_t*)dal.p, fused ? (uint32_t*)dNL32.p : nullptr,
+                           fused ? (uint32_t*)dEI.p : nullptr, fused && !g->directed ? (uint32_t*)dNDT.p : nullptr,
+                           (const uint32_t*)dus.p, U, Upd);
       } else {
         hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
         hipLaunchKernelGGL(sq_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0,
                            st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
                            (int)g->directed);
       }
-      // the fused form: the tight sweep on the direct arcs, which is also the first squaring pass
-      // for the used sources (sq_run returns at once if it found no change)
-      fused = fused_ok && csr && sq_one && nsh == 1;
-      uint32_t* chgw = (uint32_t*)dflag.p + max_pass + 2;
       if (fused) {
         SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
-        SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)dNL32.p, (int)kFx, (size_t)Vp * Vp, st));
-        hipLaunchKernelGGL(dense_arcs, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256))), dim3(256), 0,
-                           st, (const uint32_t*)dauv.p, (const uint32_t*)dal32.p, E2, Vp, (uint32_t*)dNL32.p,
-                           (uint32_t*)dEI.p);
-        dense_block(0, U, true, nullptr, chgw);
+        dense_block(0, U, true, nullptr, chgw, false, !g->directed);
       }
       // ceil(log2 Vp) passes cover every simple path; one more confirms the fixed point
       uint32_t passes = 1;
@@ -1610,7 +1646,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
           if (!f) break;
         }
       }
-      hipLaunchKernelGGL(sq_widen, dim3(2048), dim3(256), 0, st, D32, D, (uint64_t)Vp * Vp);
+      wide = false;  // (the tight forms and the extraction read the u32 matrix; sq_widen only for
+                     // the one-source loss pass)
     } else {
       hipLaunchKernelGGL(fw_init, dim3(2048), dim3(256), 0, st, D, Vp);
       hipLaunchKernelGGL(fw_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0, st,
@@ -1631,13 +1668,14 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     // SGN_APSP_LOSS1 take the one-source kernel.
     int form = lform;
   loss_phase:
+    if (!form && !wide) {  // the one-source loss pass reads the u64 matrix
+      hipLaunchKernelGGL(sq_widen, dim3(2048), dim3(256), 0, st, (const uint32_t*)dD32.p, D, (uint64_t)Vp * Vp);
+      wide = true;
+    }
     if (form) {
       const uint32_t* gate = fused ? (const uint32_t*)dflag.p + max_pass + 2 : nullptr;
-      if (fused)  // (the fused pass's lists stand unless it found a change)
-        hipLaunchKernelGGL(zero_if, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (U + 255) / 256))), dim3(256), 0, st,
-                           (uint32_t*)dtc.p, U, gate);
-      else
-        SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+      // (the fused pass's lists stand unless it found a change; then ndt_build clears the counts)
+      if (!fused) SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
       if (dense && !fused) {
         SGN_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)dNL32.p, 1, (size_t)Vp * Vp, st));  // (1 = -SQ_INF: no arc)
         hipLaunchKernelGGL(dense_arcs, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E2 + 255) / 256))),
@@ -1656,7 +1694,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         uint32_t* tcs = (uint32_t*)dtc.p + s0;
         uint32_t* tls = (uint32_t*)dtl.p + (size_t)s0 * capg;
         if (dense) {
-          dense_block(s0, ns, fused, gate, nullptr);
+          dense_block(s0, ns, fused, gate, nullptr, fused, false);
         } else if (csr && kS == 16)
           hipLaunchKernelGGL(loss_sweep_csr<16>, grid, dim3(512), lds_sw, st, d32, Vp, us, ns, V,
                              (const uint32_t*)drp.p, (const uint32_t*)dauv.p, a32, capg, tcs, tls);
@@ -1709,7 +1747,8 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
     }
     for (uint32_t r = sh_first; r < sh_last; r++)
       if (soff[r + 1] > soff[r]) {
-        hipLaunchKernelGGL(extract, dim3((uint32_t)(soff[r + 1] - soff[r])), dim3(256), 0, st, D, Vp,
+        hipLaunchKernelGGL(wide ? extract<false> : extract<true>, dim3((uint32_t)(soff[r + 1] - soff[r])), dim3(256), 0, st,
+                           wide ? (const void*)D : (const void*)dD32.p, Vp,
                            (const float*)dL.p, (const uint32_t*)dus.p, U, (const uint64_t*)dsl.p,
                            (const float*)dsp.p, ctx->d_lat, ctx->d_loss, (uint64_t*)drowres.p, (uint32_t)soff[r]);
         hipLaunchKernelGGL(extract_fold, dim3(1), dim3(256), 0, st, (const uint64_t*)drowres.p,
