@@ -282,10 +282,17 @@ __global__ __launch_bounds__(256) void sq_pass(uint32_t* D, uint32_t Vp, uint32_
 // used-source entries of row u, NDT[u][j] = -d[usrc[j]][u], as ndt_build<true> makes them.
 __global__ __launch_bounds__(256) void sq_rows(uint32_t* D, uint32_t Vp, uint32_t V, const uint32_t* rowptr,
                                                const uint32_t* auv, const uint64_t* al, uint32_t* NL, uint32_t* EI,
-                                               uint32_t* NDT, const uint32_t* usrc, uint32_t ns, uint32_t Up) {
+                                               uint32_t* NDT, const uint32_t* usrc, uint32_t ns, uint32_t Up,
+                                               uint32_t* z0, uint32_t n0, uint32_t* z1, uint32_t n1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t* row = (uint32_t*)smem;
   const uint32_t u = blockIdx.x;
+  // (block 0 clears the squaring's flag words and, in the fused form, the tight counts: two
+  // buffer fills less on the build's path)
+  if (u == 0) {
+    for (uint32_t i = threadIdx.x; z0 && i < n0; i += blockDim.x) z0[i] = 0;
+    for (uint32_t i = threadIdx.x; z1 && i < n1; i += blockDim.x) z1[i] = 0;
+  }
   for (uint32_t v = threadIdx.x; v < Vp; v += blockDim.x) row[v] = v == u ? 0u : SQ_INF;
   __syncthreads();
   if (u < V)
@@ -1601,7 +1608,7 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
       }
     } else if (fast) {
       uint32_t* D32 = (uint32_t*)dD32.p;
-      SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 3) * 4, st));
+      if (!csr) SGN_HIP(ctx, hipMemsetAsync(dflag.p, 0, (max_pass + 3) * 4, st));  // (sq_rows clears them)
       // the fused form: the tight sweep on the direct arcs, which is also the first squaring pass
       // for the used sources (sq_run returns at once if it found no change); sq_rows writes the
       // sweep's negated latency and arc-index matrices beside the rows
@@ -1611,15 +1618,15 @@ extern "C" int sgn_routes_build(sgn_ctx* ctx, const sgn_graph* g, const uint32_t
         hipLaunchKernelGGL(sq_rows, dim3(Vp), dim3(256), (size_t)Vp * 4, st, D32, Vp, V, (const uint32_t*)drp.p,
                            (const uint32_t*)dauv.p, (const uint64_t*)dal.p, fused ? (uint32_t*)dNL32.p : nullptr,
                            fused ? (uint32_t*)dEI.p : nullptr, fused && !g->directed ? (uint32_t*)dNDT.p : nullptr,
-                           (const uint32_t*)dus.p, U, Upd);
+                           (const uint32_t*)dus.p, U, Upd, (uint32_t*)dflag.p, max_pass + 3,
+                           fused ? (uint32_t*)dtc.p : nullptr, U);
       } else {
         hipLaunchKernelGGL(sq_init, dim3(2048), dim3(256), 0, st, D32, Vp);
         hipLaunchKernelGGL(sq_edges, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (E + 255) / 256))), dim3(256), 0,
                            st, D32, Vp, (const uint32_t*)deu.p, (const uint32_t*)dev.p, (const uint64_t*)del.p, E,
                            (int)g->directed);
       }
-      if (fused) {
-        SGN_HIP(ctx, hipMemsetAsync(dtc.p, 0, (size_t)U * 4, st));
+      if (fused) {  // (sq_rows cleared the tight counts)
         dense_block(0, U, true, nullptr, chgw, false, !g->directed);
       }
       // ceil(log2 Vp) passes cover every simple path; one more confirms the fixed point
