@@ -216,11 +216,22 @@ def test_apsp_dense_sweep_form(ctxf, oracle, monkeypatch):
                           np.concatenate([rand_c.lat, [2_000_000]]).astype(np.uint64),
                           np.concatenate([rand_c.loss, [0.001]]).astype(np.float32), False)
     tor = sgn.tor_graph(700, seed=12)
+    # a directed metric graph (asymmetric: +1 ms one way), complete: fused with nothing to
+    # shorten, its transposed rows built by ndt_build (sq_rows builds them for undirected ones)
+    Vm = 240
+    P = rng.uniform(0, 1, (Vm, 2))
+    mi, mj = np.nonzero(~np.eye(Vm, dtype=bool))
+    mlat = (6_000_000 + np.round(np.hypot(*(P[mi] - P[mj]).T) * 50_000_000) + np.where(mi < mj, 1_000_000, 0)).astype(np.uint64)
+    mloss = np.round(rng.uniform(0, 0.01, len(mi)), 6).astype(np.float32)
+    dmetric = sgn.GraphArrays(np.arange(Vm), np.concatenate([mi, np.arange(Vm)]), np.concatenate([mj, np.arange(Vm)]),
+                              np.concatenate([mlat, np.full(Vm, 1_000_000, np.uint64)]),
+                              np.concatenate([mloss, np.zeros(Vm, np.float32)]), True)
     # (graph, used, env, expected (loss_dense, loss_fused) of the default run)
     cases = [(tor, None, {}, (1, 1)), (tor, None, {"SGN_APSP_DENSE_H": "1"}, (1, 0)),
              (sgn.tor_graph(500, seed=13), np.arange(1, 500, 3), {}, (1, 1)), (line, None, {}, (1, 1)),
              (rand_c, None, {}, (1, 0)), (rand_c, None, {"SGN_APSP_DENSE_S": "32"}, (1, 0)),
-             (directed, None, {}, (1, 0)), (par, None, {}, (0, 0))]
+             (directed, None, {}, (1, 0)), (dmetric, None, {}, (1, 1)), (dmetric, np.arange(0, Vm, 7), {}, (1, 1)),
+             (par, None, {}, (0, 0))]
     for k, (g, used, env, want) in enumerate(cases):
         used = np.arange(len(g.node_id)) if used is None else used
         ol, op = oracle.routes(g, used)
